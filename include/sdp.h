@@ -1,0 +1,243 @@
+/*
+ * sdp.h -- C ABI of libsdp.so, the MI355X (gfx950) statistics engine behind
+ * spark_df_profiling's describe().
+ *
+ * The reference has no FFI: every statistic is a Spark SQL aggregate issued from
+ * Python (/root/reference/spark_df_profiling/describe.py).  Each entry point below
+ * replaces one group of those Spark calls; the comment on each names the
+ * reference lines it stands in for.  Python binds these through ctypes
+ * (spark-df-profiling_amd/spark_df_profiling/_native.py).
+ *
+ * Conventions (all entry points):
+ *   - pointers named d_* are DEVICE pointers (HBM), owned by the caller (the torch
+ *     caching allocator); the library never allocates or frees them;
+ *   - work is enqueued on `stream` (a hipStream_t passed as void*); nothing
+ *     synchronises unless the name says so;
+ *   - return value: 0 on success, otherwise an SDP_E* code; sdp_last_error()
+ *     returns a message for the calling thread;
+ *   - value buffers must be 16-byte aligned; validity bitmaps are Arrow LSB-first
+ *     bitmaps addressed with a bit offset and may be NULL (all rows valid).
+ */
+#ifndef SDP_H
+#define SDP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- element types ------------------------------------------------------ */
+enum sdp_dtype {
+    SDP_I8 = 1, SDP_I16 = 2, SDP_I32 = 3, SDP_I64 = 4,
+    SDP_F32 = 5, SDP_F64 = 6,
+    SDP_U8 = 7, SDP_U16 = 8, SDP_U32 = 9, SDP_U64 = 10,
+    SDP_BOOL = 11            /* Arrow bit-packed booleans */
+};
+
+enum sdp_status {
+    SDP_OK = 0, SDP_EINVAL = 1, SDP_EALIGN = 2, SDP_EHIP = 3, SDP_ECAP = 4
+};
+
+#define SDP_MAX_WINDOWS 5     /* quantile windows per pass-1 launch */
+
+/* One Arrow column slice resident in HBM. */
+typedef struct sdp_column {
+    const void    *d_values;           /* element 0 of the slice; 16-B aligned      */
+    const uint8_t *d_validity;         /* Arrow bitmap or NULL                      */
+    int64_t        validity_bit_offset;
+    int64_t        length;             /* rows                                      */
+    int32_t        dtype;              /* enum sdp_dtype                            */
+    int32_t        _pad;
+} sdp_column;
+
+/* Variable-length byte keys (Arrow utf8 / binary, or fixed width). */
+typedef struct sdp_bytes_column {
+    const uint8_t *d_data;             /* value bytes (+16 readable padding bytes)  */
+    const void    *d_offsets;          /* int32 or int64 offsets (length+1), or NULL */
+    const uint8_t *d_validity;
+    int64_t        validity_bit_offset;
+    int64_t        length;
+    int32_t        offset_width;       /* 4 or 8; ignored when fixed_width > 0      */
+    int32_t        fixed_width;        /* >0: row i = d_data[i*w .. (i+1)*w)        */
+} sdp_bytes_column;
+
+/* Quantile windows chosen from a row sample (see sdp_quantile_plan). */
+typedef struct sdp_qplan {
+    uint64_t lo[SDP_MAX_WINDOWS];      /* order-preserving keys, inclusive         */
+    uint64_t hi[SDP_MAX_WINDOWS];
+    int32_t  in_sample[SDP_MAX_WINDOWS]; /* sample keys strictly inside window w */
+    double   shift;                    /* moment shift K (sample median)           */
+    int32_t  n_windows;
+    int32_t  n_sample;                 /* valid, non-NaN sample elements           */
+} sdp_qplan;
+
+/* Pass-1 result: replaces describe.py:143-144 (count), :193-201 (one agg of
+ * mean/min/max/variance/kurtosis/stddev/skewness/sum) and :220 (n_zeros). */
+typedef struct sdp_pass1_result {
+    uint64_t count;                    /* valid and not NaN (na.drop)              */
+    uint64_t n_valid;                  /* valid (not null), NaN included           */
+    uint64_t n_nan;
+    uint64_t n_zero;                   /* x == 0.0 over valid rows (NaN never 0)   */
+    int64_t  isum;                     /* integral: two's-complement wrapping sum  */
+    int64_t  imin, imax;               /* integral min/max                         */
+    double   dmin, dmax;               /* floating min/max (NaN excluded)          */
+    double   shift;                    /* K used for the power sums                */
+    double   s1_hi, s1_lo;             /* sum (x-K), compensated                   */
+    double   s2;                       /* sum (x-K)^2                              */
+    double   s3_hi, s3_lo;             /* sum (x-K)^3, compensated                 */
+    double   s4;                       /* sum (x-K)^4                              */
+    /* per quantile window w */
+    uint64_t w_gt[SDP_MAX_WINDOWS];    /* #(key > hi)                              */
+    uint64_t w_eq_lo[SDP_MAX_WINDOWS]; /* #(key == lo)                             */
+    uint64_t w_eq_hi[SDP_MAX_WINDOWS]; /* #(key == hi), 0 when hi == lo            */
+    uint64_t w_in[SDP_MAX_WINDOWS];    /* #(lo < key < hi) = candidates            */
+    uint32_t w_overflow;               /* bit w: a block overflowed its slots       */
+    uint32_t _pad;
+} sdp_pass1_result;
+
+/* Pass-2 result: replaces describe.py:215-218 (mad), :222-223 (high/low idx)
+ * and :49 (the CASE-WHEN histogram groupBy).  hist counts follow separately. */
+typedef struct sdp_pass2_result {
+    double   abs_dev_sum;              /* sum |x - mean| over na.drop rows         */
+    uint64_t n_high;                   /* #(x > hi_t), NaN counts (Spark order)    */
+    uint64_t n_low;                    /* #(x < lo_t)                              */
+    uint64_t n_unbinned;               /* na.drop rows matching no CASE branch     */
+} sdp_pass2_result;
+
+/* ---- diagnostics ---------------------------------------------------------- */
+const char *sdp_last_error(void);
+const char *sdp_version(void);
+
+/* ---- workspace sizing (host-only, no device work) --------------------------- */
+/* Bytes of d_work each entry point needs for a column of `length` rows. */
+int64_t sdp_pass1_workspace_bytes(int64_t length, int32_t dtype);
+int64_t sdp_pass2_workspace_bytes(int64_t length, int32_t dtype, int32_t bins);
+
+/* ---- numeric column path (describe_numeric_1d, describe.py:192-229) ------- */
+
+/* Sample up to `n_sample` rows at evenly spaced positions; writes their
+ * order-preserving keys (UINT64_MAX for null/NaN rows) to d_sample. */
+int sdp_sample_keys(const sdp_column *col, int32_t n_sample, uint64_t *d_sample,
+                    void *stream);
+
+/* Sort a key sample (<= 16384 keys) and choose one value window per target
+ * probability around its sample rank, merged where windows overlap.  Replaces
+ * the five `percentile`/`percentile_approx` jobs of describe.py:203-208 (the
+ * windows let pass 1 resolve them in the same scan). */
+int sdp_quantile_plan(uint64_t *d_sample, int32_t n_sample, const double *probs,
+                      int32_t n_probs, int32_t is_float, sdp_qplan *d_plan,
+                      void *stream);
+
+/* Fused pass 1 over one numeric column (see sdp_pass1_result).  Candidates
+ * (keys strictly inside window w) go to per-block slots
+ * d_cand[(w*grid + b)*slot_capacity ...]; per-block counts (clamped to
+ * slot_capacity; overflow flagged in w_overflow) to d_cand_counts[w*grid + b]. */
+int sdp_pass1(const sdp_column *col, const sdp_qplan *d_plan, void *d_work,
+              int64_t work_bytes, uint64_t *d_cand, uint32_t *d_cand_counts,
+              int64_t slot_capacity, sdp_pass1_result *d_result, void *stream);
+
+/* Grid size sdp_pass1 uses for `length` rows (host-only). */
+int32_t sdp_pass1_grid(int64_t length, int32_t dtype);
+
+/* Gather the per-block candidate slots of window w into a dense array. */
+int sdp_compact_candidates(const uint64_t *d_cand, const uint32_t *d_cand_counts,
+                           int32_t grid, int64_t slot_capacity, uint64_t *d_out,
+                           uint64_t *d_out_count, void *stream);
+
+/* Radix-select support: 2048-bin histogram of key bits [shift, shift+11) over
+ * keys whose bits above shift+11 equal `prefix` (prefix_bits = 64-shift-11). */
+int sdp_radix_hist(const uint64_t *d_keys, const uint64_t *d_n, uint64_t prefix,
+                   int32_t shift, uint64_t *d_hist, void *stream);
+/* Keep keys whose bits >= shift equal `prefix`; append to d_out. */
+int sdp_radix_filter(const uint64_t *d_keys, const uint64_t *d_n, uint64_t prefix,
+                     int32_t shift, uint64_t *d_out, uint64_t *d_out_n, void *stream);
+/* Sort <= 16384 keys in place (one workgroup, LDS bitonic). */
+int sdp_sort_small(uint64_t *d_keys, const uint64_t *d_n, void *stream);
+/* Write the order-preserving keys of all na.drop rows (fallback select). */
+int sdp_column_keys(const sdp_column *col, uint64_t *d_out, uint64_t *d_out_n,
+                    void *stream);
+
+/* Fused pass 2: mad, histogram over host-built CASE edges, outlier counts. */
+int sdp_pass2(const sdp_column *col, double mean, const double *d_edges,
+              int32_t bins, int32_t edges_monotone, double hi_t, double lo_t,
+              void *d_work, int64_t work_bytes, sdp_pass2_result *d_result,
+              uint64_t *d_hist, void *stream);
+
+/* ---- distinct / value counts (describe.py:143, :250-271) ------------------ */
+
+/* Open-addressing tables: capacity must be a power of two >= 2 x the groups
+ * expected; d_slots must be pre-filled by sdp_table_clear. */
+int sdp_table_clear(uint64_t *d_slots, uint64_t *d_counts, int64_t capacity,
+                    int32_t bytes_keys, void *stream);
+
+/* countDistinct over a fixed-width column: NaN one value, -0.0 == 0.0, nulls
+ * ignored.  with_counts != 0 also accumulates per-key row counts (CAT path).
+ * d_stats: [0] groups, [1] rows inserted, [2] rows with key UINT64_MAX. */
+int sdp_hash_u64(const sdp_column *col, uint64_t *d_slots, uint64_t *d_counts,
+                 int64_t capacity, int32_t with_counts, uint64_t *d_stats,
+                 void *stream);
+
+/* Same for byte keys; slots hold (24-bit hash tag << 40 | row+1), equal keys
+ * are confirmed by byte comparison. d_stats: [0] groups, [1] rows inserted. */
+int sdp_hash_bytes(const sdp_bytes_column *col, uint64_t *d_slots, uint64_t *d_counts,
+                   int64_t capacity, uint64_t *d_stats, void *stream);
+
+/* Top-k groups by (count desc, key asc) from a table built with counts.
+ * Histogram of floor(log2(count)) over occupied slots (64 bins). */
+int sdp_table_count_log2_hist(const uint64_t *d_slots, const uint64_t *d_counts,
+                              int64_t capacity, int32_t bytes_keys, uint64_t *d_hist,
+                              void *stream);
+/* Histogram of counts in [lo, lo + 2048*step) with bucket width `step`. */
+int sdp_table_count_hist(const uint64_t *d_slots, const uint64_t *d_counts,
+                         int64_t capacity, int32_t bytes_keys, uint64_t lo,
+                         uint64_t step, uint64_t *d_hist, void *stream);
+/* Slot indices with count >= min_count (and <= max_count), appended. */
+int sdp_table_select(const uint64_t *d_slots, const uint64_t *d_counts, int64_t capacity,
+                     int32_t bytes_keys, uint64_t min_count, uint64_t max_count,
+                     uint64_t *d_out, uint64_t *d_out_n, uint64_t out_capacity,
+                     void *stream);
+/* Sort <= 16384 selected slots by (count desc, key asc), in place. */
+int sdp_sort_groups(uint64_t *d_sel, const uint64_t *d_n, const uint64_t *d_slots,
+                    const uint64_t *d_counts, const sdp_bytes_column *bytes_col,
+                    void *stream);
+/* 8-byte big-endian prefix at byte `offset` of each selected group's key
+ * (byte keys) -- radix keys for tie-breaking among equal counts. */
+int sdp_group_prefix(const uint64_t *d_sel, const uint64_t *d_n, const uint64_t *d_slots,
+                     const sdp_bytes_column *col, int32_t offset, uint64_t *d_out,
+                     void *stream);
+
+/* Keep entries of d_sel whose parallel value d_vals[i] is in [lo, hi]. */
+int sdp_select_by_value(const uint64_t *d_sel, const uint64_t *d_vals, const uint64_t *d_n,
+                        uint64_t lo, uint64_t hi, uint64_t *d_out, uint64_t *d_out_vals,
+                        uint64_t *d_out_n, void *stream);
+
+/* Number of set validity bits (non-null rows), accumulated into *d_out. */
+int sdp_count_valid(const uint8_t *d_validity, int64_t bit_offset, int64_t length,
+                    uint64_t *d_out, void *stream);
+
+/* ---- first rows (describe.py:276 limit(1), :282 limit(50)) ---------------- */
+/* Indices of the first k rows that survive na.drop (null, and NaN for floats). */
+int sdp_first_valid(const sdp_column *col, int32_t k, int64_t *d_idx, int64_t *d_found,
+                    void *stream);
+
+/* ---- Pearson matrix (utils.py:20-36) -------------------------------------- */
+/* Listwise-deletion row mask over `ncols` columns (host array): bit r set iff
+ * every column is valid and (where check_nan[i]) not NaN at row r.  d_keep has
+ * ceil(length/32) uint32 words; d_work >= sdp_gram_workspace_bytes.  The column
+ * descriptors are staged through d_work; this call synchronises the stream once
+ * (the host descriptor copy), as does sdp_gram. */
+int sdp_rowmask(const sdp_column *cols, const int32_t *check_nan, int32_t ncols,
+                void *d_work, int64_t work_bytes, uint32_t *d_keep, void *stream);
+/* Shifted Gram: G[i][j] = sum_r keep_r (x_ir - K_i)(x_jr - K_j), s[i] = sum_r keep_r
+ * (x_ir - K_i), n = sum keep_r, on v_mfma_f64_16x16x4_f64.  Writes G (ncols^2,
+ * row-major, upper and lower), s (ncols) and n (1, as double). */
+int64_t sdp_gram_workspace_bytes(int64_t length, int32_t ncols);
+int sdp_gram(const sdp_column *cols, int32_t ncols, const uint32_t *d_keep,
+             const double *d_shift, void *d_work, int64_t work_bytes,
+             double *d_gram, double *d_colsum, double *d_n, void *stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* SDP_H */

@@ -1,0 +1,180 @@
+// sdp_common.h -- device helpers shared by the libsdp kernels (gfx950, wave64).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <string.h>
+#include "../../include/sdp.h"
+
+namespace sdp {
+
+constexpr int WAVE = 64;
+constexpr uint64_t KEY_NAN = 0xFFF8000000000000ull;   // key of the canonical NaN
+constexpr uint64_t EMPTY64 = 0xFFFFFFFFFFFFFFFFull;
+
+// ---- error plumbing (sdp_abi.cpp) -------------------------------------------
+int set_error(int code, const char *fmt, ...);
+int check_launch(const char *what);
+bool aligned16(const void *p);
+
+// ---- order-preserving keys (A.8: NaN above +inf, -0.0 == 0.0) ----------------
+__host__ __device__ __forceinline__ uint64_t f64_key(double d) {
+    uint64_t b;
+    memcpy(&b, &d, 8);
+    if (d == 0.0) b = 0;                       // -0.0 groups with 0.0
+    if (d != d) b = 0x7FF8000000000000ull;     // one NaN
+    return (b >> 63) ? ~b : (b | 0x8000000000000000ull);
+}
+__host__ __device__ __forceinline__ double key_f64(uint64_t k) {
+    uint64_t b = (k >> 63) ? (k & 0x7FFFFFFFFFFFFFFFull) : ~k;
+    double d;
+    memcpy(&d, &b, 8);
+    return d;
+}
+__host__ __device__ __forceinline__ uint64_t i64_key(int64_t v) {
+    return (uint64_t)v ^ 0x8000000000000000ull;
+}
+__host__ __device__ __forceinline__ int64_t key_i64(uint64_t k) {
+    return (int64_t)(k ^ 0x8000000000000000ull);
+}
+
+// element traits: how a stored element becomes a double, an int64 and a key
+template <typename T> struct Elem;
+template <> struct Elem<double> {
+    static constexpr bool is_float = true;
+    __device__ static double d(double v) { return v; }
+    __device__ static int64_t i(double) { return 0; }
+    __device__ static uint64_t key(double v) { return f64_key(v); }
+};
+template <> struct Elem<float> {
+    static constexpr bool is_float = true;
+    __device__ static double d(float v) { return (double)v; }
+    __device__ static int64_t i(float) { return 0; }
+    __device__ static uint64_t key(float v) { return f64_key((double)v); }
+};
+#define SDP_INT_ELEM(T)                                                          \
+    template <> struct Elem<T> {                                                 \
+        static constexpr bool is_float = false;                                  \
+        __device__ static double d(T v) { return (double)(int64_t)v; }           \
+        __device__ static int64_t i(T v) { return (int64_t)v; }                  \
+        __device__ static uint64_t key(T v) { return i64_key((int64_t)v); }      \
+    };
+SDP_INT_ELEM(int64_t)
+SDP_INT_ELEM(int32_t)
+SDP_INT_ELEM(int16_t)
+SDP_INT_ELEM(int8_t)
+SDP_INT_ELEM(uint32_t)
+SDP_INT_ELEM(uint16_t)
+SDP_INT_ELEM(uint8_t)
+#undef SDP_INT_ELEM
+
+// 16-byte vector of T (one global_load_dwordx4 per lane)
+template <typename T> struct alignas(16) Vec16 {
+    static constexpr int N = 16 / sizeof(T);
+    T v[N];
+};
+
+// Validity bits [idx, idx+cnt) of an Arrow bitmap (cnt <= 32), LSB = row idx.
+__device__ __forceinline__ uint32_t valid_bits(const uint8_t *bm, int64_t bitoff, int64_t idx,
+                                               int cnt) {
+    if (bm == nullptr) return cnt >= 32 ? 0xFFFFFFFFu : ((1u << cnt) - 1u);
+    const int64_t b = bitoff + idx;
+    const int64_t byte0 = b >> 3;
+    const int sh = (int)(b & 7);
+    // read 5 bytes max (cnt<=32 plus shift<8 -> <= 39 bits)
+    uint64_t w = 0;
+    const int nbytes = (sh + cnt + 7) >> 3;
+    for (int k = 0; k < nbytes; ++k) w |= (uint64_t)bm[byte0 + k] << (8 * k);
+    w >>= sh;
+    return cnt >= 32 ? (uint32_t)w : (uint32_t)(w & ((1ull << cnt) - 1ull));
+}
+__device__ __forceinline__ bool valid_bit(const uint8_t *bm, int64_t bitoff, int64_t idx) {
+    if (bm == nullptr) return true;
+    const int64_t b = bitoff + idx;
+    return (bm[b >> 3] >> (b & 7)) & 1;
+}
+
+// ---- compensated summation (TwoSum) -----------------------------------------
+__device__ __forceinline__ void two_sum_acc(double &s, double &c, double x) {
+    const double t = s + x;
+    const double bp = t - s;
+    c += (s - (t - bp)) + (x - bp);
+    s = t;
+}
+__device__ __forceinline__ void dd_add(double &ah, double &al, double bh, double bl) {
+    double s = ah + bh;
+    double bp = s - ah;
+    double e = (ah - (s - bp)) + (bh - bp);
+    e += al + bl;
+    ah = s + e;
+    al = e - (ah - s);
+}
+
+// ---- wave reductions (64 lanes, DPP/shuffle via __shfl_xor) ------------------
+__device__ __forceinline__ uint64_t wave_sum_u64(uint64_t v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, WAVE);
+    return v;
+}
+__device__ __forceinline__ double wave_sum_f64(double v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, WAVE);
+    return v;
+}
+__device__ __forceinline__ void wave_sum_dd(double &h, double &l) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        double oh = __shfl_xor(h, o, WAVE), ol = __shfl_xor(l, o, WAVE);
+        dd_add(h, l, oh, ol);
+    }
+}
+__device__ __forceinline__ double wave_min_f64(double v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v = fmin(v, __shfl_xor(v, o, WAVE));
+    return v;
+}
+__device__ __forceinline__ double wave_max_f64(double v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v = fmax(v, __shfl_xor(v, o, WAVE));
+    return v;
+}
+__device__ __forceinline__ int64_t wave_min_i64(int64_t v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) { int64_t w = __shfl_xor(v, o, WAVE); v = w < v ? w : v; }
+    return v;
+}
+__device__ __forceinline__ int64_t wave_max_i64(int64_t v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) { int64_t w = __shfl_xor(v, o, WAVE); v = w > v ? w : v; }
+    return v;
+}
+__device__ __forceinline__ int64_t wave_sum_i64(int64_t v) {
+    return (int64_t)wave_sum_u64((uint64_t)v);
+}
+
+__device__ __forceinline__ int lane_id() { return threadIdx.x & (WAVE - 1); }
+// number of set bits of `mask` below this lane
+__device__ __forceinline__ int lane_rank(uint64_t mask) {
+    return __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32),
+                                     __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0));
+}
+
+// 64-bit mixer (splitmix64 / murmur3 fmix64)
+__host__ __device__ __forceinline__ uint64_t mix64(uint64_t x) {
+    x ^= x >> 30;
+    x *= 0xBF58476D1CE4E5B9ull;
+    x ^= x >> 27;
+    x *= 0x94D049BB133111EBull;
+    x ^= x >> 31;
+    return x;
+}
+
+// Spark comparisons on doubles with NaN ordered above every number (A.8)
+__device__ __forceinline__ bool spark_lt(double x, double t) {
+    return (t != t) ? (x == x) : (x == x && x < t);
+}
+__device__ __forceinline__ bool spark_gt(double x, double t) {
+    return (t != t) ? false : (x != x || x > t);
+}
+__device__ __forceinline__ bool spark_ge(double x, double t) { return !spark_lt(x, t); }
+
+}  // namespace sdp

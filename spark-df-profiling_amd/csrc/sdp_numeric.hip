@@ -1,0 +1,842 @@
+// sdp_numeric.hip -- numeric column path of describe() on gfx950.
+//
+// Replaces the per-column Spark job chain of describe_numeric_1d
+// (/root/reference/spark_df_profiling/describe.py:192-229) and the common block
+// of describe_1d (:143-151):
+//   sample + plan  -> value windows around each requested quantile
+//   pass 1         -> count / min / max / sum / shifted power sums / zeros and
+//                     the window statistics + candidates (one HBM read)
+//   radix select   -> exact order statistics inside a window (small arrays)
+//   pass 2         -> mad, CASE-WHEN histogram, outlier counts (one HBM read)
+// All block partials are merged by a single-block kernel in block order, so
+// every result is deterministic for a given grid.
+#include "sdp_common.h"
+
+namespace sdp {
+
+constexpr int P1_BLOCK = 256;
+constexpr int P1_UNROLL = 4;          // 16-B vectors per thread per tile
+constexpr int P1_MAX_GRID = 1024;     // 4 blocks per CU on 256 CUs
+constexpr int SORT_MAX = 16384;       // one-workgroup LDS bitonic sort (128 KiB)
+
+#define SDP_DISPATCH_NUMERIC(DT, ...)                                             \
+    switch (DT) {                                                                 \
+    case SDP_I8: { using T = int8_t; __VA_ARGS__; } break;                        \
+    case SDP_I16: { using T = int16_t; __VA_ARGS__; } break;                      \
+    case SDP_I32: { using T = int32_t; __VA_ARGS__; } break;                      \
+    case SDP_I64: { using T = int64_t; __VA_ARGS__; } break;                      \
+    case SDP_U8: { using T = uint8_t; __VA_ARGS__; } break;                       \
+    case SDP_U16: { using T = uint16_t; __VA_ARGS__; } break;                     \
+    case SDP_U32: { using T = uint32_t; __VA_ARGS__; } break;                     \
+    case SDP_F32: { using T = float; __VA_ARGS__; } break;                        \
+    case SDP_F64: { using T = double; __VA_ARGS__; } break;                       \
+    default: return set_error(SDP_EINVAL, "unsupported numeric dtype %d", (int)(DT)); \
+    }
+
+static int elem_size(int dt) {
+    switch (dt) {
+    case SDP_I8: case SDP_U8: return 1;
+    case SDP_I16: case SDP_U16: return 2;
+    case SDP_I32: case SDP_U32: case SDP_F32: return 4;
+    case SDP_I64: case SDP_U64: case SDP_F64: return 8;
+    default: return 0;
+    }
+}
+
+static int check_col(const sdp_column *c, const char *who) {
+    if (c == nullptr) return set_error(SDP_EINVAL, "%s: null column", who);
+    if (c->length < 0) return set_error(SDP_EINVAL, "%s: negative length", who);
+    if (c->length > 0 && c->d_values == nullptr) return set_error(SDP_EINVAL, "%s: null values", who);
+    if (!aligned16(c->d_values)) return set_error(SDP_EALIGN, "%s: values not 16-byte aligned", who);
+    if (elem_size(c->dtype) == 0 || c->dtype == SDP_U64)
+        return set_error(SDP_EINVAL, "%s: dtype %d is not a numeric column", who, c->dtype);
+    return SDP_OK;
+}
+
+static int p1_grid(int64_t n, int dt) {
+    const int vpt = 16 / elem_size(dt);
+    const int64_t nvec = n / vpt;
+    int64_t tiles = (nvec + (int64_t)P1_BLOCK * P1_UNROLL - 1) / ((int64_t)P1_BLOCK * P1_UNROLL);
+    if (tiles < 1) tiles = 1;
+    return (int)(tiles < P1_MAX_GRID ? tiles : P1_MAX_GRID);
+}
+
+// ============================================================================
+// sampling and window planning
+// ============================================================================
+
+template <typename T>
+__global__ void sample_keys_kernel(sdp_column col, int32_t ns, uint64_t *out) {
+    const int j = blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= ns) return;
+    const int64_t n = col.length;
+    const int64_t i = (int64_t)(((double)j + 0.5) * (double)n / (double)ns);
+    uint64_t k = EMPTY64;
+    if (i < n && valid_bit(col.d_validity, col.validity_bit_offset, i)) {
+        const T x = ((const T *)col.d_values)[i];
+        const double xd = Elem<T>::d(x);
+        if (xd == xd) k = Elem<T>::key(x);
+    }
+    out[j] = k;
+}
+
+// LDS bitonic sort of `n` keys (n <= SORT_MAX); pads with EMPTY64.
+__device__ void block_sort_keys(uint64_t *s, int n) {
+    int P = 2;
+    while (P < n) P <<= 1;
+    for (int i = n + threadIdx.x; i < P; i += blockDim.x) s[i] = EMPTY64;
+    __syncthreads();
+    for (int k = 2; k <= P; k <<= 1) {
+        for (int j = k >> 1; j > 0; j >>= 1) {
+            for (int i = threadIdx.x; i < P; i += blockDim.x) {
+                const int ixj = i ^ j;
+                if (ixj > i) {
+                    const uint64_t a = s[i], b = s[ixj];
+                    const bool asc = (i & k) == 0;
+                    if ((a > b) == asc) { s[i] = b; s[ixj] = a; }
+                }
+            }
+            __syncthreads();
+        }
+    }
+}
+
+__global__ void __launch_bounds__(1024) quantile_plan_kernel(uint64_t *sample, int32_t ns,
+                                                             const double *probs, int32_t np,
+                                                             int32_t is_float, sdp_qplan *plan) {
+    __shared__ uint64_t s[SORT_MAX];
+    for (int i = threadIdx.x; i < ns; i += blockDim.x) s[i] = sample[i];
+    __syncthreads();
+    block_sort_keys(s, ns);
+    for (int i = threadIdx.x; i < ns; i += blockDim.x) sample[i] = s[i];
+    if (threadIdx.x != 0) return;
+    int m = 0;
+    {   // valid sample keys sort before the EMPTY64 markers
+        int lo = 0, hi = ns;
+        while (lo < hi) { int mid = (lo + hi) >> 1; if (s[mid] != EMPTY64) lo = mid + 1; else hi = mid; }
+        m = lo;
+    }
+    sdp_qplan p;
+    for (int w = 0; w < SDP_MAX_WINDOWS; ++w) { p.lo[w] = 0; p.hi[w] = EMPTY64; p.in_sample[w] = 0; }
+    p.n_sample = m;
+    if (m == 0) {
+        p.n_windows = np > 0 ? 1 : 0;
+        p.shift = 0.0;
+        *plan = p;
+        return;
+    }
+    const uint64_t med = s[(m - 1) / 2];
+    p.shift = is_float ? key_f64(med) : (double)key_i64(med);
+    int nw = 0;
+    for (int t = 0; t < np && t < SDP_MAX_WINDOWS; ++t) {
+        const double q = probs[t];
+        const double r = q * (double)(m - 1);
+        const int d = (int)ceil(4.0 * sqrt((double)m * q * (1.0 - q))) + 2;
+        int il = (int)floor(r) - d, ih = (int)ceil(r) + d;
+        if (il < 0) il = 0;
+        if (ih > m - 1) ih = m - 1;
+        const uint64_t lo = (il == 0) ? 0ull : s[il];
+        const uint64_t hi = (ih == m - 1) ? EMPTY64 : s[ih];
+        if (nw > 0 && lo <= p.hi[nw - 1]) {
+            if (hi > p.hi[nw - 1]) p.hi[nw - 1] = hi;
+        } else {
+            p.lo[nw] = lo;
+            p.hi[nw] = hi;
+            ++nw;
+        }
+    }
+    for (int w = 0; w < nw; ++w) {
+        // #(s < hi) - #(s <= lo) by binary search on the sorted sample
+        int a = 0, b = m;
+        while (a < b) { int mid = (a + b) >> 1; if (s[mid] < p.hi[w]) a = mid + 1; else b = mid; }
+        const int below_hi = a;
+        a = 0; b = m;
+        while (a < b) { int mid = (a + b) >> 1; if (s[mid] <= p.lo[w]) a = mid + 1; else b = mid; }
+        p.in_sample[w] = below_hi > a ? below_hi - a : 0;
+    }
+    p.n_windows = nw;
+    *plan = p;
+}
+
+// ============================================================================
+// pass 1
+// ============================================================================
+
+// Per-block partial: plain arrays so the epilogue reduces field-wise without
+// runtime-indexed register arrays (which hipcc would place in scratch).
+constexpr int W_ = SDP_MAX_WINDOWS;
+constexpr int NU = 4 + 4 * W_;   // count, n_valid, n_nan, n_zero, gt[W], eqlo[W], eqhi[W], in[W]
+struct P1Partial {
+    uint64_t u[NU];
+    int64_t i[3];                // isum, imin, imax
+    double d[8];                 // s1h, s1l, s2, s3h, s3l, s4, dmin, dmax
+    uint32_t overflow, _pad;
+};
+
+struct P1Thread {
+    uint32_t count, n_valid, n_nan, n_zero;
+    int64_t isum, imin, imax;
+    double dmin, dmax;
+    double s1, s1c, s2, s3, s3c, s4;
+    uint32_t gt[SDP_MAX_WINDOWS], eqlo[SDP_MAX_WINDOWS], eqhi[SDP_MAX_WINDOWS];
+};
+
+struct P1Ctx {
+    uint64_t lo[SDP_MAX_WINDOWS], hi[SDP_MAX_WINDOWS];
+    int nw;
+    double K;
+    uint64_t *cand;           // [nw][grid][cap]
+    int64_t cap;
+    int grid;
+    uint32_t *cursor;         // LDS [SDP_MAX_WINDOWS]
+    uint32_t *overflow;       // LDS
+};
+
+// One element; every lane of the wave calls this in lockstep (ballots inside).
+template <typename T>
+__device__ __forceinline__ void p1_elem(P1Thread &st, const P1Ctx &cx, T x, bool valid) {
+    const double xd = Elem<T>::d(x);
+    const bool isnan_ = Elem<T>::is_float && (xd != xd);
+    const bool ok = valid && !isnan_;
+    st.n_valid += valid;
+    st.n_nan += (valid && isnan_);
+    uint64_t key = 0;
+    if (ok) {
+        st.count += 1;
+        if (Elem<T>::is_float) {
+            st.dmin = fmin(st.dmin, xd);
+            st.dmax = fmax(st.dmax, xd);
+        } else {
+            const int64_t xi = Elem<T>::i(x);
+            st.imin = xi < st.imin ? xi : st.imin;
+            st.imax = xi > st.imax ? xi : st.imax;
+            st.isum = (int64_t)((uint64_t)st.isum + (uint64_t)xi);
+        }
+        st.n_zero += (xd == 0.0);
+        const double d = xd - cx.K;
+        const double d2 = d * d;
+        two_sum_acc(st.s1, st.s1c, d);
+        st.s2 += d2;
+        two_sum_acc(st.s3, st.s3c, d2 * d);
+        st.s4 = fma(d2, d2, st.s4);
+        key = Elem<T>::key(x);
+    }
+#pragma unroll
+    for (int w = 0; w < SDP_MAX_WINDOWS; ++w) {
+        if (w < cx.nw) {
+            const uint64_t lo = cx.lo[w], hi = cx.hi[w];
+            st.gt[w] += (ok && key > hi);
+            st.eqlo[w] += (ok && key == lo);
+            st.eqhi[w] += (ok && key == hi && hi != lo);
+            const bool inside = ok && key > lo && key < hi;
+            const uint64_t m = __ballot(inside);
+            if (m) {
+                const int leader = __ffsll((long long)m) - 1;
+                uint32_t base = 0;
+                if (lane_id() == leader) base = atomicAdd(&cx.cursor[w], (uint32_t)__popcll(m));
+                base = __shfl(base, leader, WAVE);
+                if (inside) {
+                    const uint32_t pos = base + (uint32_t)lane_rank(m);
+                    if ((int64_t)pos < cx.cap)
+                        cx.cand[((int64_t)w * cx.grid + blockIdx.x) * cx.cap + pos] = key;
+                }
+            }
+        }
+    }
+}
+
+template <typename T>
+__global__ void __launch_bounds__(P1_BLOCK, 4) pass1_kernel(sdp_column col, const sdp_qplan *plan,
+                                                         P1Partial *partials, uint64_t *cand,
+                                                         uint32_t *cand_counts, int64_t cap) {
+    constexpr int VPT = Vec16<T>::N;
+    __shared__ uint32_t s_cursor[SDP_MAX_WINDOWS];
+    __shared__ uint32_t s_overflow;
+
+    if (threadIdx.x < SDP_MAX_WINDOWS) s_cursor[threadIdx.x] = 0;
+    if (threadIdx.x == 0) s_overflow = 0;
+
+    P1Ctx cx;
+    cx.nw = plan->n_windows;
+#pragma unroll
+    for (int w = 0; w < SDP_MAX_WINDOWS; ++w) { cx.lo[w] = plan->lo[w]; cx.hi[w] = plan->hi[w]; }
+    cx.K = plan->shift;
+    cx.cand = cand;
+    cx.cap = cap;
+    cx.grid = gridDim.x;
+    cx.cursor = s_cursor;
+    cx.overflow = &s_overflow;
+    __syncthreads();
+
+    P1Thread st;
+    st.count = st.n_valid = st.n_nan = st.n_zero = 0;
+    st.isum = 0;
+    st.imin = INT64_MAX;
+    st.imax = INT64_MIN;
+    st.dmin = __builtin_inf();
+    st.dmax = -__builtin_inf();
+    st.s1 = st.s1c = st.s2 = st.s3 = st.s3c = st.s4 = 0.0;
+#pragma unroll
+    for (int w = 0; w < SDP_MAX_WINDOWS; ++w) st.gt[w] = st.eqlo[w] = st.eqhi[w] = 0;
+
+    const int64_t n = col.length;
+    const int64_t nvec = n / VPT;
+    const Vec16<T> *vals = (const Vec16<T> *)col.d_values;
+    const int64_t tile_vecs = (int64_t)P1_BLOCK * P1_UNROLL;
+    const int64_t ntiles = (nvec + tile_vecs - 1) / tile_vecs;
+    for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+        Vec16<T> v[P1_UNROLL];
+        uint32_t vb[P1_UNROLL];
+#pragma unroll
+        for (int u = 0; u < P1_UNROLL; ++u) {
+            const int64_t vi = tile * tile_vecs + (int64_t)u * P1_BLOCK + threadIdx.x;
+            if (vi < nvec) {
+                v[u] = vals[vi];
+                vb[u] = valid_bits(col.d_validity, col.validity_bit_offset, vi * VPT, VPT);
+            } else {
+                vb[u] = 0;
+#pragma unroll
+                for (int e = 0; e < VPT; ++e) v[u].v[e] = (T)0;
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < P1_UNROLL; ++u) {
+#pragma unroll
+            for (int e = 0; e < VPT; ++e) p1_elem<T>(st, cx, v[u].v[e], (vb[u] >> e) & 1u);
+        }
+    }
+    // tail elements (n % VPT) by the first wave of block 0
+    if (blockIdx.x == 0 && threadIdx.x < WAVE) {
+        const int64_t i = nvec * VPT + threadIdx.x;
+        const bool inb = i < n;
+        T x = inb ? ((const T *)col.d_values)[i] : (T)0;
+        const bool valid = inb && valid_bit(col.d_validity, col.validity_bit_offset, i);
+        p1_elem<T>(st, cx, x, valid);
+    }
+
+    // ---- block reduction: waves, then LDS, fixed order ----------------------
+    __shared__ uint64_t s_u[P1_BLOCK / WAVE][NU];
+    __shared__ int64_t s_i[P1_BLOCK / WAVE][3];
+    __shared__ double s_d[P1_BLOCK / WAVE][8];
+    const int wid = threadIdx.x / WAVE, lane = lane_id();
+    {
+        double h = st.s1, l = st.s1c;
+        wave_sum_dd(h, l);
+        double h3 = st.s3, l3 = st.s3c;
+        wave_sum_dd(h3, l3);
+        const double s2 = wave_sum_f64(st.s2), s4 = wave_sum_f64(st.s4);
+        const double dmn = wave_min_f64(st.dmin), dmx = wave_max_f64(st.dmax);
+        const int64_t isum = wave_sum_i64(st.isum), imn = wave_min_i64(st.imin), imx = wave_max_i64(st.imax);
+        const uint64_t c0 = wave_sum_u64(st.count), c1 = wave_sum_u64(st.n_valid);
+        const uint64_t c2 = wave_sum_u64(st.n_nan), c3 = wave_sum_u64(st.n_zero);
+        if (lane == 0) {
+            s_d[wid][0] = h; s_d[wid][1] = l; s_d[wid][2] = s2; s_d[wid][3] = h3;
+            s_d[wid][4] = l3; s_d[wid][5] = s4; s_d[wid][6] = dmn; s_d[wid][7] = dmx;
+            s_i[wid][0] = isum; s_i[wid][1] = imn; s_i[wid][2] = imx;
+            s_u[wid][0] = c0; s_u[wid][1] = c1; s_u[wid][2] = c2; s_u[wid][3] = c3;
+        }
+#pragma unroll
+        for (int w = 0; w < W_; ++w) {
+            const uint64_t g = wave_sum_u64(st.gt[w]);
+            const uint64_t e1 = wave_sum_u64(st.eqlo[w]);
+            const uint64_t e2 = wave_sum_u64(st.eqhi[w]);
+            if (lane == 0) { s_u[wid][4 + w] = g; s_u[wid][4 + W_ + w] = e1; s_u[wid][4 + 2 * W_ + w] = e2; }
+        }
+    }
+    __syncthreads();
+    P1Partial *out = partials + blockIdx.x;
+    const int t = threadIdx.x;
+    constexpr int NW = P1_BLOCK / WAVE;
+    if (t < 4 + 3 * W_) {
+        uint64_t a = 0;
+        for (int w = 0; w < NW; ++w) a += s_u[w][t];
+        out->u[t] = a;
+    } else if (t < 4 + 4 * W_) {
+        const int w = t - (4 + 3 * W_);
+        out->u[t] = s_cursor[w];
+        if (w < cx.nw)
+            cand_counts[(int64_t)w * gridDim.x + blockIdx.x] =
+                (int64_t)s_cursor[w] < cap ? s_cursor[w] : (uint32_t)cap;
+    } else if (t == 64) {
+        int64_t a = s_i[0][0], mn = s_i[0][1], mx = s_i[0][2];
+        for (int w = 1; w < NW; ++w) {
+            a = (int64_t)((uint64_t)a + (uint64_t)s_i[w][0]);
+            mn = s_i[w][1] < mn ? s_i[w][1] : mn;
+            mx = s_i[w][2] > mx ? s_i[w][2] : mx;
+        }
+        out->i[0] = a; out->i[1] = mn; out->i[2] = mx;
+    } else if (t == 65 || t == 66) {
+        const int o = (t == 65) ? 0 : 3;   // (s1h,s1l) or (s3h,s3l)
+        double h = s_d[0][o], l = s_d[0][o + 1];
+        for (int w = 1; w < NW; ++w) dd_add(h, l, s_d[w][o], s_d[w][o + 1]);
+        out->d[o] = h; out->d[o + 1] = l;
+    } else if (t == 67) {
+        double a = 0.0, b = 0.0, mn = s_d[0][6], mx = s_d[0][7];
+        for (int w = 0; w < NW; ++w) { a += s_d[w][2]; b += s_d[w][5]; }
+        for (int w = 1; w < NW; ++w) { mn = fmin(mn, s_d[w][6]); mx = fmax(mx, s_d[w][7]); }
+        out->d[2] = a; out->d[5] = b; out->d[6] = mn; out->d[7] = mx;
+    } else if (t == 68) {
+        uint32_t ovf = 0;
+        for (int w = 0; w < cx.nw; ++w)
+            if ((int64_t)s_cursor[w] > cap) ovf |= 1u << w;
+        out->overflow = ovf;
+        out->_pad = 0;
+    }
+}
+
+__global__ void pass1_merge_kernel(const P1Partial *partials, int grid, const sdp_qplan *plan,
+                                   sdp_pass1_result *out) {
+    // one thread per field, partials visited in block order (deterministic)
+    const int t = threadIdx.x;
+    if (t < NU) {
+        uint64_t a = 0;
+        for (int b = 0; b < grid; ++b) a += partials[b].u[t];
+        uint64_t *dst;
+        if (t < 4) dst = (&out->count) + t;                 // count, n_valid, n_nan, n_zero
+        else if (t < 4 + W_) dst = out->w_gt + (t - 4);
+        else if (t < 4 + 2 * W_) dst = out->w_eq_lo + (t - 4 - W_);
+        else if (t < 4 + 3 * W_) dst = out->w_eq_hi + (t - 4 - 2 * W_);
+        else dst = out->w_in + (t - 4 - 3 * W_);
+        *dst = a;
+    } else if (t == 32) {
+        int64_t a = 0, mn = INT64_MAX, mx = INT64_MIN;
+        for (int b = 0; b < grid; ++b) {
+            a = (int64_t)((uint64_t)a + (uint64_t)partials[b].i[0]);
+            mn = partials[b].i[1] < mn ? partials[b].i[1] : mn;
+            mx = partials[b].i[2] > mx ? partials[b].i[2] : mx;
+        }
+        out->isum = a; out->imin = mn; out->imax = mx;
+    } else if (t == 33 || t == 34) {
+        const int o = (t == 33) ? 0 : 3;
+        double h = 0.0, l = 0.0;
+        for (int b = 0; b < grid; ++b) dd_add(h, l, partials[b].d[o], partials[b].d[o + 1]);
+        if (o == 0) { out->s1_hi = h; out->s1_lo = l; } else { out->s3_hi = h; out->s3_lo = l; }
+    } else if (t == 35) {
+        double a = 0.0, c = 0.0, mn = __builtin_inf(), mx = -__builtin_inf();
+        uint32_t ovf = 0;
+        for (int b = 0; b < grid; ++b) {
+            a += partials[b].d[2]; c += partials[b].d[5];
+            mn = fmin(mn, partials[b].d[6]); mx = fmax(mx, partials[b].d[7]);
+            ovf |= partials[b].overflow;
+        }
+        out->s2 = a; out->s4 = c; out->dmin = mn; out->dmax = mx;
+        out->w_overflow = ovf;
+        out->_pad = 0;
+        out->shift = plan->shift;
+    }
+}
+
+// ============================================================================
+// candidate compaction and radix select
+// ============================================================================
+
+// d_counts[grid] per-block counts -> dense copy.  One workgroup per source block;
+// the exclusive prefix is recomputed per workgroup (grid <= 1024).
+__global__ void compact_cand_kernel(const uint64_t *cand, const uint32_t *counts, int grid,
+                                    int64_t cap, uint64_t *out, uint64_t *out_n) {
+    const int b = blockIdx.x;
+    __shared__ uint64_t s_base;
+    if (threadIdx.x == 0) {
+        uint64_t base = 0;
+        for (int i = 0; i < b; ++i) base += counts[i];
+        s_base = base;
+        if (b == grid - 1) *out_n = base + counts[b];
+    }
+    __syncthreads();
+    const uint32_t c = counts[b];
+    const uint64_t *src = cand + (int64_t)b * cap;
+    for (uint32_t i = threadIdx.x; i < c; i += blockDim.x) out[s_base + i] = src[i];
+}
+
+__global__ void radix_hist_kernel(const uint64_t *keys, const uint64_t *n_ptr, uint64_t prefix,
+                                  int shift, uint64_t *hist) {
+    __shared__ uint32_t h[2048];
+    for (int i = threadIdx.x; i < 2048; i += blockDim.x) h[i] = 0;
+    __syncthreads();
+    const uint64_t n = *n_ptr;
+    const int top = shift + 11;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+         i += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t k = keys[i];
+        const bool match = top >= 64 ? true : ((k >> top) == prefix);
+        if (match) atomicAdd(&h[(k >> shift) & 2047u], 1u);
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < 2048; i += blockDim.x)
+        if (h[i]) atomicAdd((unsigned long long *)&hist[i], (unsigned long long)h[i]);
+}
+
+__global__ void radix_filter_kernel(const uint64_t *keys, const uint64_t *n_ptr, uint64_t prefix,
+                                    int shift, uint64_t *out, uint64_t *out_n) {
+    const uint64_t n = *n_ptr;
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    const uint64_t iters = (n + stride - 1) / stride;
+    for (uint64_t it = 0; it < iters; ++it) {
+        const uint64_t i = it * stride + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+        uint64_t k = 0;
+        bool keep = false;
+        if (i < n) {
+            k = keys[i];
+            keep = shift >= 64 ? true : ((k >> shift) == prefix);
+        }
+        const uint64_t m = __ballot(keep);
+        if (m) {
+            const int leader = __ffsll((long long)m) - 1;
+            unsigned long long base = 0;
+            if (lane_id() == leader) base = atomicAdd((unsigned long long *)out_n, (unsigned long long)__popcll(m));
+            base = __shfl(base, leader, WAVE);
+            if (keep) out[base + lane_rank(m)] = k;
+        }
+    }
+}
+
+__global__ void __launch_bounds__(1024) sort_small_kernel(uint64_t *keys, const uint64_t *n_ptr) {
+    __shared__ uint64_t s[SORT_MAX];
+    const int n = (int)min((uint64_t)SORT_MAX, *n_ptr);
+    for (int i = threadIdx.x; i < n; i += blockDim.x) s[i] = keys[i];
+    __syncthreads();
+    block_sort_keys(s, n);
+    for (int i = threadIdx.x; i < n; i += blockDim.x) keys[i] = s[i];
+}
+
+template <typename T>
+__global__ void column_keys_kernel(sdp_column col, uint64_t *out, uint64_t *out_n) {
+    const int64_t n = col.length;
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    const int64_t iters = (n + stride - 1) / stride;
+    for (int64_t it = 0; it < iters; ++it) {
+        const int64_t i = it * stride + (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+        bool keep = false;
+        uint64_t k = 0;
+        if (i < n && valid_bit(col.d_validity, col.validity_bit_offset, i)) {
+            const T x = ((const T *)col.d_values)[i];
+            const double xd = Elem<T>::d(x);
+            keep = xd == xd;
+            k = Elem<T>::key(x);
+        }
+        const uint64_t m = __ballot(keep);
+        if (m) {
+            const int leader = __ffsll((long long)m) - 1;
+            unsigned long long base = 0;
+            if (lane_id() == leader) base = atomicAdd((unsigned long long *)out_n, (unsigned long long)__popcll(m));
+            base = __shfl(base, leader, WAVE);
+            if (keep) out[base + lane_rank(m)] = k;
+        }
+    }
+}
+
+// ============================================================================
+// pass 2: mad + histogram + outliers
+// ============================================================================
+
+constexpr int P2_BLOCK = 256;
+constexpr int P2_UNROLL = 2;
+constexpr int P2_MAX_BALLOT_BINS = 256;   // lane-owned counters: 4 per lane
+
+struct P2Ctx {
+    double mean, hi_t, lo_t, e0, inv_w;
+    const double *edges;      // LDS copy
+    int bins;
+    bool monotone;
+};
+
+// bin per the CASE-WHEN chain (describe.py:46, :20-35); -1 = no branch matched
+__device__ __forceinline__ int case_bin(const P2Ctx &c, double x) {
+    const int b = c.bins;
+    if (c.monotone) {
+        if (!(x >= c.e0)) return -1;
+        double f = (x - c.e0) * c.inv_w;
+        int j = (f >= (double)(b - 1)) ? b - 1 : (f > 0.0 ? (int)f : 0);
+        while (j + 1 < b && x >= c.edges[j + 1]) ++j;
+        while (j > 0 && x < c.edges[j]) --j;
+        return j;
+    }
+    for (int i = 0; i < b; ++i) {
+        const bool cond = (i < b - 1) ? (spark_ge(x, c.edges[i]) && spark_lt(x, c.edges[i + 1]))
+                                      : spark_ge(x, c.edges[i]);
+        if (cond) return i;
+    }
+    return -1;
+}
+
+struct P2Thread {
+    double mad;
+    uint32_t high, low, unbinned;
+};
+
+template <typename T, bool BALLOT>
+__device__ __forceinline__ void p2_elem(P2Thread &st, const P2Ctx &c, uint32_t *lds_hist, T x,
+                                        bool valid) {
+    const double xd = Elem<T>::d(x);
+    const bool isnan_ = Elem<T>::is_float && (xd != xd);
+    const bool ok = valid && !isnan_;
+    if (valid) {
+        st.high += spark_gt(xd, c.hi_t);
+        st.low += spark_lt(xd, c.lo_t);
+    }
+    int bin = -1;
+    if (ok) {
+        st.mad += fabs(xd - c.mean);
+        bin = case_bin(c, xd);
+        st.unbinned += (bin < 0);
+    }
+    if (BALLOT) {
+        // conflict-free counting: one ballot per bin, one single-lane LDS add
+        int jlo = 0, jhi = c.bins - 1;
+        if (c.bins > 32) {   // scan only the bins present in this wave
+            int bmin = bin < 0 ? 0x7fffffff : bin, bmax = bin;
+#pragma unroll
+            for (int o = 32; o > 0; o >>= 1) {
+                bmin = min(bmin, __shfl_xor(bmin, o, WAVE));
+                bmax = max(bmax, __shfl_xor(bmax, o, WAVE));
+            }
+            jlo = bmin;
+            jhi = bmax;
+        }
+        for (int j = jlo; j <= jhi; ++j) {
+            const uint64_t m = __ballot(bin == j);
+            if (m && lane_id() == 0) atomicAdd(&lds_hist[j], (uint32_t)__popcll(m));
+        }
+    } else {
+        if (bin >= 0) atomicAdd(&lds_hist[bin], 1u);
+    }
+}
+
+template <typename T, bool BALLOT>
+__global__ void __launch_bounds__(P2_BLOCK, 4) pass2_kernel(sdp_column col, double mean, const double *edges,
+                                                         int bins, int monotone, double hi_t, double lo_t,
+                                                         double *part_mad, uint64_t *part_cnt) {
+    constexpr int VPT = Vec16<T>::N;
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    double *s_edges = (double *)smem;
+    uint32_t *s_hist = (uint32_t *)(smem + sizeof(double) * bins);
+    for (int i = threadIdx.x; i < bins; i += blockDim.x) { s_edges[i] = edges[i]; s_hist[i] = 0; }
+    __syncthreads();
+    P2Ctx c;
+    c.mean = mean; c.hi_t = hi_t; c.lo_t = lo_t; c.edges = s_edges; c.bins = bins;
+    c.monotone = monotone != 0;
+    c.e0 = s_edges[0];
+    {
+        const double w = (bins > 1) ? (s_edges[bins - 1] - s_edges[0]) / (double)(bins - 1) : 0.0;
+        c.inv_w = (w > 0.0) ? 1.0 / w : 0.0;
+    }
+    P2Thread st;
+    st.mad = 0.0; st.high = st.low = st.unbinned = 0;
+
+    const int64_t n = col.length;
+    const int64_t nvec = n / VPT;
+    const Vec16<T> *vals = (const Vec16<T> *)col.d_values;
+    const int64_t tile_vecs = (int64_t)P2_BLOCK * P2_UNROLL;
+    const int64_t ntiles = (nvec + tile_vecs - 1) / tile_vecs;
+    for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+        Vec16<T> v[P2_UNROLL];
+        uint32_t vb[P2_UNROLL];
+#pragma unroll
+        for (int u = 0; u < P2_UNROLL; ++u) {
+            const int64_t vi = tile * tile_vecs + (int64_t)u * P2_BLOCK + threadIdx.x;
+            if (vi < nvec) {
+                v[u] = vals[vi];
+                vb[u] = valid_bits(col.d_validity, col.validity_bit_offset, vi * VPT, VPT);
+            } else {
+                vb[u] = 0;
+#pragma unroll
+                for (int e = 0; e < VPT; ++e) v[u].v[e] = (T)0;
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < P2_UNROLL; ++u)
+#pragma unroll
+            for (int e = 0; e < VPT; ++e) p2_elem<T, BALLOT>(st, c, s_hist, v[u].v[e], (vb[u] >> e) & 1u);
+    }
+    if (blockIdx.x == 0 && threadIdx.x < WAVE) {
+        const int64_t i = nvec * VPT + threadIdx.x;
+        const bool inb = i < n;
+        T x = inb ? ((const T *)col.d_values)[i] : (T)0;
+        const bool valid = inb && valid_bit(col.d_validity, col.validity_bit_offset, i);
+        p2_elem<T, BALLOT>(st, c, s_hist, x, valid);
+    }
+    // ---- block reduction (fixed order) ----
+    __shared__ double s_mad[P2_BLOCK / WAVE];
+    __shared__ uint64_t s_u[P2_BLOCK / WAVE][3];
+    const int wid = threadIdx.x / WAVE, lane = lane_id();
+    const double mad = wave_sum_f64(st.mad);
+    const uint64_t hi = wave_sum_u64(st.high), lo = wave_sum_u64(st.low), ub = wave_sum_u64(st.unbinned);
+    if (lane == 0) { s_mad[wid] = mad; s_u[wid][0] = hi; s_u[wid][1] = lo; s_u[wid][2] = ub; }
+    __syncthreads();
+    const int stride = 3 + bins;
+    if (threadIdx.x == 0) {
+        double m = 0.0;
+        uint64_t a = 0, b = 0, u = 0;
+        for (int w = 0; w < P2_BLOCK / WAVE; ++w) { m += s_mad[w]; a += s_u[w][0]; b += s_u[w][1]; u += s_u[w][2]; }
+        part_mad[blockIdx.x] = m;
+        part_cnt[(int64_t)blockIdx.x * stride + 0] = a;
+        part_cnt[(int64_t)blockIdx.x * stride + 1] = b;
+        part_cnt[(int64_t)blockIdx.x * stride + 2] = u;
+    }
+    for (int i = threadIdx.x; i < bins; i += blockDim.x)
+        part_cnt[(int64_t)blockIdx.x * stride + 3 + i] = s_hist[i];
+}
+
+__global__ void pass2_merge_kernel(const double *part_mad, const uint64_t *part_cnt, int grid, int bins,
+                                   sdp_pass2_result *out, uint64_t *hist) {
+    const int stride = 3 + bins;
+    for (int i = threadIdx.x; i < bins; i += blockDim.x) {
+        uint64_t s = 0;
+        for (int b = 0; b < grid; ++b) s += part_cnt[(int64_t)b * stride + 3 + i];
+        hist[i] = s;
+    }
+    if (threadIdx.x == 0) {
+        sdp_pass2_result r;
+        r.abs_dev_sum = 0.0;
+        r.n_high = r.n_low = r.n_unbinned = 0;
+        for (int b = 0; b < grid; ++b) {
+            r.abs_dev_sum += part_mad[b];
+            r.n_high += part_cnt[(int64_t)b * stride + 0];
+            r.n_low += part_cnt[(int64_t)b * stride + 1];
+            r.n_unbinned += part_cnt[(int64_t)b * stride + 2];
+        }
+        *out = r;
+    }
+}
+
+static int p2_grid(int64_t n, int dt) {
+    const int vpt = 16 / elem_size(dt);
+    const int64_t nvec = n / vpt;
+    int64_t tiles = (nvec + (int64_t)P2_BLOCK * P2_UNROLL - 1) / ((int64_t)P2_BLOCK * P2_UNROLL);
+    if (tiles < 1) tiles = 1;
+    return (int)(tiles < 2048 ? tiles : 2048);
+}
+
+}  // namespace sdp
+
+using namespace sdp;
+
+// ============================================================================
+// C ABI
+// ============================================================================
+
+extern "C" int32_t sdp_pass1_grid(int64_t length, int32_t dtype) {
+    if (elem_size(dtype) == 0) return 0;
+    return p1_grid(length, dtype);
+}
+
+extern "C" int64_t sdp_pass1_workspace_bytes(int64_t length, int32_t dtype) {
+    if (elem_size(dtype) == 0) return -1;
+    return (int64_t)p1_grid(length, dtype) * (int64_t)sizeof(P1Partial);
+}
+
+extern "C" int64_t sdp_pass2_workspace_bytes(int64_t length, int32_t dtype, int32_t bins) {
+    if (elem_size(dtype) == 0 || bins < 1) return -1;
+    const int64_t g = p2_grid(length, dtype);
+    return g * (int64_t)sizeof(double) + g * (int64_t)(3 + bins) * (int64_t)sizeof(uint64_t);
+}
+
+extern "C" int sdp_sample_keys(const sdp_column *col, int32_t n_sample, uint64_t *d_sample, void *stream) {
+    int rc = check_col(col, "sdp_sample_keys");
+    if (rc) return rc;
+    if (n_sample < 1 || n_sample > SORT_MAX) return set_error(SDP_EINVAL, "sdp_sample_keys: n_sample %d", n_sample);
+    hipStream_t s = (hipStream_t)stream;
+    const int blocks = (n_sample + 255) / 256;
+    SDP_DISPATCH_NUMERIC(col->dtype,
+        hipLaunchKernelGGL(sample_keys_kernel<T>, dim3(blocks), dim3(256), 0, s, *col, n_sample, d_sample));
+    return check_launch("sample_keys_kernel");
+}
+
+extern "C" int sdp_quantile_plan(uint64_t *d_sample, int32_t n_sample, const double *d_probs, int32_t n_probs,
+                                 int32_t is_float, sdp_qplan *d_plan, void *stream) {
+    if (n_sample < 1 || n_sample > SORT_MAX) return set_error(SDP_EINVAL, "sdp_quantile_plan: n_sample %d", n_sample);
+    if (n_probs < 0 || n_probs > SDP_MAX_WINDOWS) return set_error(SDP_EINVAL, "sdp_quantile_plan: n_probs %d", n_probs);
+    hipLaunchKernelGGL(quantile_plan_kernel, dim3(1), dim3(1024), 0, (hipStream_t)stream, d_sample, n_sample,
+                       d_probs, n_probs, is_float, d_plan);
+    return check_launch("quantile_plan_kernel");
+}
+
+extern "C" int sdp_pass1(const sdp_column *col, const sdp_qplan *d_plan, void *d_work, int64_t work_bytes,
+                         uint64_t *d_cand, uint32_t *d_cand_counts, int64_t slot_capacity,
+                         sdp_pass1_result *d_result, void *stream) {
+    int rc = check_col(col, "sdp_pass1");
+    if (rc) return rc;
+    const int grid = p1_grid(col->length, col->dtype);
+    if (work_bytes < (int64_t)grid * (int64_t)sizeof(P1Partial))
+        return set_error(SDP_ECAP, "sdp_pass1: workspace %lld < %lld", (long long)work_bytes,
+                         (long long)grid * (long long)sizeof(P1Partial));
+    if (slot_capacity < 0 || slot_capacity > 0xFFFFFFFFll) return set_error(SDP_EINVAL, "sdp_pass1: slot_capacity");
+    hipStream_t s = (hipStream_t)stream;
+    P1Partial *parts = (P1Partial *)d_work;
+    SDP_DISPATCH_NUMERIC(col->dtype,
+        hipLaunchKernelGGL(pass1_kernel<T>, dim3(grid), dim3(P1_BLOCK), 0, s, *col, d_plan, parts, d_cand,
+                           d_cand_counts, slot_capacity));
+    rc = check_launch("pass1_kernel");
+    if (rc) return rc;
+    hipLaunchKernelGGL(pass1_merge_kernel, dim3(1), dim3(64), 0, s, parts, grid, d_plan, d_result);
+    static_assert(NU <= 32, "merge thread map");
+    return check_launch("pass1_merge_kernel");
+}
+
+extern "C" int sdp_compact_candidates(const uint64_t *d_cand, const uint32_t *d_cand_counts, int32_t grid,
+                                      int64_t slot_capacity, uint64_t *d_out, uint64_t *d_out_count,
+                                      void *stream) {
+    if (grid < 1) return set_error(SDP_EINVAL, "sdp_compact_candidates: grid %d", grid);
+    hipLaunchKernelGGL(compact_cand_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream, d_cand, d_cand_counts,
+                       grid, slot_capacity, d_out, d_out_count);
+    return check_launch("compact_cand_kernel");
+}
+
+extern "C" int sdp_radix_hist(const uint64_t *d_keys, const uint64_t *d_n, uint64_t prefix, int32_t shift,
+                              uint64_t *d_hist, void *stream) {
+    if (shift < 0 || shift > 53) return set_error(SDP_EINVAL, "sdp_radix_hist: shift %d", shift);
+    hipLaunchKernelGGL(radix_hist_kernel, dim3(512), dim3(256), 0, (hipStream_t)stream, d_keys, d_n, prefix, shift,
+                       d_hist);
+    return check_launch("radix_hist_kernel");
+}
+
+extern "C" int sdp_radix_filter(const uint64_t *d_keys, const uint64_t *d_n, uint64_t prefix, int32_t shift,
+                                uint64_t *d_out, uint64_t *d_out_n, void *stream) {
+    if (shift < 0 || shift > 64) return set_error(SDP_EINVAL, "sdp_radix_filter: shift %d", shift);
+    hipLaunchKernelGGL(radix_filter_kernel, dim3(512), dim3(256), 0, (hipStream_t)stream, d_keys, d_n, prefix,
+                       shift, d_out, d_out_n);
+    return check_launch("radix_filter_kernel");
+}
+
+extern "C" int sdp_sort_small(uint64_t *d_keys, const uint64_t *d_n, void *stream) {
+    hipLaunchKernelGGL(sort_small_kernel, dim3(1), dim3(1024), 0, (hipStream_t)stream, d_keys, d_n);
+    return check_launch("sort_small_kernel");
+}
+
+extern "C" int sdp_column_keys(const sdp_column *col, uint64_t *d_out, uint64_t *d_out_n, void *stream) {
+    int rc = check_col(col, "sdp_column_keys");
+    if (rc) return rc;
+    hipStream_t s = (hipStream_t)stream;
+    SDP_DISPATCH_NUMERIC(col->dtype,
+        hipLaunchKernelGGL(column_keys_kernel<T>, dim3(1024), dim3(256), 0, s, *col, d_out, d_out_n));
+    return check_launch("column_keys_kernel");
+}
+
+extern "C" int sdp_pass2(const sdp_column *col, double mean, const double *d_edges, int32_t bins,
+                         int32_t edges_monotone, double hi_t, double lo_t, void *d_work, int64_t work_bytes,
+                         sdp_pass2_result *d_result, uint64_t *d_hist, void *stream) {
+    int rc = check_col(col, "sdp_pass2");
+    if (rc) return rc;
+    if (bins < 2 || bins > 8192) return set_error(SDP_EINVAL, "sdp_pass2: bins %d", bins);
+    const int grid = p2_grid(col->length, col->dtype);
+    const int64_t need = sdp_pass2_workspace_bytes(col->length, col->dtype, bins);
+    if (work_bytes < need) return set_error(SDP_ECAP, "sdp_pass2: workspace %lld < %lld", (long long)work_bytes,
+                                            (long long)need);
+    double *pm = (double *)d_work;
+    uint64_t *pc = (uint64_t *)((char *)d_work + (int64_t)grid * sizeof(double));
+    const size_t lds = (size_t)bins * (sizeof(double) + sizeof(uint32_t)) + 16;
+    hipStream_t s = (hipStream_t)stream;
+    if (bins <= P2_MAX_BALLOT_BINS) {
+        SDP_DISPATCH_NUMERIC(col->dtype,
+            hipLaunchKernelGGL((pass2_kernel<T, true>), dim3(grid), dim3(P2_BLOCK), lds, s, *col, mean, d_edges,
+                               bins, edges_monotone, hi_t, lo_t, pm, pc));
+    } else {
+        SDP_DISPATCH_NUMERIC(col->dtype,
+            hipLaunchKernelGGL((pass2_kernel<T, false>), dim3(grid), dim3(P2_BLOCK), lds, s, *col, mean, d_edges,
+                               bins, edges_monotone, hi_t, lo_t, pm, pc));
+    }
+    rc = check_launch("pass2_kernel");
+    if (rc) return rc;
+    hipLaunchKernelGGL(pass2_merge_kernel, dim3(1), dim3(256), 0, s, pm, pc, grid, bins, d_result, d_hist);
+    return check_launch("pass2_merge_kernel");
+}

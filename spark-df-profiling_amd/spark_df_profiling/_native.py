@@ -1,0 +1,169 @@
+"""ctypes binding of libsdp.so (include/sdp.h).
+
+The library is the product: there is no Python or CPU fallback.  Loading fails
+loudly when the shared object is missing, and every call raises
+``NativeError`` with the library's message when it returns a non-zero status.
+
+torch is imported first on purpose: torch-ROCm loads its own libamdhip64.so.7,
+and libsdp.so (NEEDED libamdhip64.so.7) then binds to that same runtime, so
+device pointers from the torch caching allocator are valid in our kernels.
+"""
+
+from __future__ import annotations
+
+import ctypes
+import os
+
+import torch  # noqa: F401  (must precede the dlopen, see module docstring)
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get('SDP_LIBRARY', os.path.join(_HERE, 'lib', 'libsdp.so'))
+
+MAX_WINDOWS = 5
+
+# enum sdp_dtype
+I8, I16, I32, I64, F32, F64, U8, U16, U32, U64, BOOL = 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11
+FLOAT_DTYPES = (F32, F64)
+ELEM_SIZE = {I8: 1, I16: 2, I32: 4, I64: 8, F32: 4, F64: 8, U8: 1, U16: 2, U32: 4, U64: 8}
+
+
+class NativeError(RuntimeError):
+    pass
+
+
+class SdpColumn(ctypes.Structure):
+    _fields_ = [('d_values', ctypes.c_void_p), ('d_validity', ctypes.c_void_p),
+                ('validity_bit_offset', ctypes.c_int64), ('length', ctypes.c_int64),
+                ('dtype', ctypes.c_int32), ('_pad', ctypes.c_int32)]
+
+
+class SdpBytesColumn(ctypes.Structure):
+    _fields_ = [('d_data', ctypes.c_void_p), ('d_offsets', ctypes.c_void_p), ('d_validity', ctypes.c_void_p),
+                ('validity_bit_offset', ctypes.c_int64), ('length', ctypes.c_int64),
+                ('offset_width', ctypes.c_int32), ('fixed_width', ctypes.c_int32)]
+
+
+class SdpQPlan(ctypes.Structure):
+    _fields_ = [('lo', ctypes.c_uint64 * MAX_WINDOWS), ('hi', ctypes.c_uint64 * MAX_WINDOWS),
+                ('in_sample', ctypes.c_int32 * MAX_WINDOWS), ('shift', ctypes.c_double),
+                ('n_windows', ctypes.c_int32), ('n_sample', ctypes.c_int32)]
+
+
+class SdpPass1Result(ctypes.Structure):
+    _fields_ = [('count', ctypes.c_uint64), ('n_valid', ctypes.c_uint64), ('n_nan', ctypes.c_uint64),
+                ('n_zero', ctypes.c_uint64), ('isum', ctypes.c_int64), ('imin', ctypes.c_int64),
+                ('imax', ctypes.c_int64), ('dmin', ctypes.c_double), ('dmax', ctypes.c_double),
+                ('shift', ctypes.c_double), ('s1_hi', ctypes.c_double), ('s1_lo', ctypes.c_double),
+                ('s2', ctypes.c_double), ('s3_hi', ctypes.c_double), ('s3_lo', ctypes.c_double),
+                ('s4', ctypes.c_double),
+                ('w_gt', ctypes.c_uint64 * MAX_WINDOWS), ('w_eq_lo', ctypes.c_uint64 * MAX_WINDOWS),
+                ('w_eq_hi', ctypes.c_uint64 * MAX_WINDOWS), ('w_in', ctypes.c_uint64 * MAX_WINDOWS),
+                ('w_overflow', ctypes.c_uint32), ('_pad', ctypes.c_uint32)]
+
+
+class SdpPass2Result(ctypes.Structure):
+    _fields_ = [('abs_dev_sum', ctypes.c_double), ('n_high', ctypes.c_uint64), ('n_low', ctypes.c_uint64),
+                ('n_unbinned', ctypes.c_uint64)]
+
+
+_P = ctypes.c_void_p
+_I32 = ctypes.c_int32
+_I64 = ctypes.c_int64
+_U64 = ctypes.c_uint64
+_D = ctypes.c_double
+_COL = ctypes.POINTER(SdpColumn)
+_BCOL = ctypes.POINTER(SdpBytesColumn)
+
+# name -> (restype, argtypes); every status-returning entry is checked
+_SIGNATURES = {
+    'sdp_last_error': (ctypes.c_char_p, []),
+    'sdp_version': (ctypes.c_char_p, []),
+    'sdp_pass1_workspace_bytes': (_I64, [_I64, _I32]),
+    'sdp_pass2_workspace_bytes': (_I64, [_I64, _I32, _I32]),
+    'sdp_pass1_grid': (_I32, [_I64, _I32]),
+    'sdp_sample_keys': (ctypes.c_int, [_COL, _I32, _P, _P]),
+    'sdp_quantile_plan': (ctypes.c_int, [_P, _I32, _P, _I32, _I32, _P, _P]),
+    'sdp_pass1': (ctypes.c_int, [_COL, _P, _P, _I64, _P, _P, _I64, _P, _P]),
+    'sdp_compact_candidates': (ctypes.c_int, [_P, _P, _I32, _I64, _P, _P, _P]),
+    'sdp_radix_hist': (ctypes.c_int, [_P, _P, _U64, _I32, _P, _P]),
+    'sdp_radix_filter': (ctypes.c_int, [_P, _P, _U64, _I32, _P, _P, _P]),
+    'sdp_sort_small': (ctypes.c_int, [_P, _P, _P]),
+    'sdp_column_keys': (ctypes.c_int, [_COL, _P, _P, _P]),
+    'sdp_pass2': (ctypes.c_int, [_COL, _D, _P, _I32, _I32, _D, _D, _P, _I64, _P, _P, _P]),
+    'sdp_table_clear': (ctypes.c_int, [_P, _P, _I64, _I32, _P]),
+    'sdp_hash_u64': (ctypes.c_int, [_COL, _P, _P, _I64, _I32, _P, _P]),
+    'sdp_hash_bytes': (ctypes.c_int, [_BCOL, _P, _P, _I64, _P, _P]),
+    'sdp_table_count_log2_hist': (ctypes.c_int, [_P, _P, _I64, _I32, _P, _P]),
+    'sdp_table_count_hist': (ctypes.c_int, [_P, _P, _I64, _I32, _U64, _U64, _P, _P]),
+    'sdp_table_select': (ctypes.c_int, [_P, _P, _I64, _I32, _U64, _U64, _P, _P, _U64, _P]),
+    'sdp_sort_groups': (ctypes.c_int, [_P, _P, _P, _P, _BCOL, _P]),
+    'sdp_group_prefix': (ctypes.c_int, [_P, _P, _P, _BCOL, _I32, _P, _P]),
+    'sdp_select_by_value': (ctypes.c_int, [_P, _P, _P, _U64, _U64, _P, _P, _P, _P]),
+    'sdp_count_valid': (ctypes.c_int, [_P, _I64, _I64, _P, _P]),
+    'sdp_first_valid': (ctypes.c_int, [_COL, _I32, _P, _P, _P]),
+    'sdp_rowmask': (ctypes.c_int, [_COL, ctypes.POINTER(_I32), _I32, _P, _I64, _P, _P]),
+    'sdp_gram_workspace_bytes': (_I64, [_I64, _I32]),
+    'sdp_gram': (ctypes.c_int, [_COL, _I32, _P, _P, _P, _I64, _P, _P, _P, _P]),
+}
+
+_STATUS_FUNCS = {k for k, (r, _) in _SIGNATURES.items() if r is ctypes.c_int}
+
+_lib = None
+
+
+def _load():
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise NativeError('libsdp.so not found at %s -- build it with `make -C spark-df-profiling_amd/csrc` '
+                          '(or __graft_entry__.build()); there is no CPU fallback' % LIB_PATH)
+    lib = ctypes.CDLL(LIB_PATH)
+    for name, (res, args) in _SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = lib
+    return lib
+
+
+def exported_symbols():
+    """Names declared in include/sdp.h that this binding resolves."""
+    lib = _load()
+    return [n for n in _SIGNATURES if hasattr(lib, n)]
+
+
+class _Caller:
+    def __getattr__(self, name):
+        lib = _load()
+        fn = getattr(lib, name)
+        if name not in _STATUS_FUNCS:
+            return fn
+
+        def call(*args):
+            rc = fn(*args)
+            if rc != 0:
+                msg = lib.sdp_last_error().decode(errors='replace')
+                raise NativeError('%s failed (status %d): %s' % (name, rc, msg))
+            return rc
+        call.__name__ = name
+        return call
+
+
+sdp = _Caller()
+
+
+def ptr(t):
+    """Device pointer of a torch tensor (or None -> NULL)."""
+    if t is None:
+        return None
+    return ctypes.c_void_p(t.data_ptr())
+
+
+def stream_handle(stream=None):
+    s = stream if stream is not None else torch.cuda.current_stream()
+    return ctypes.c_void_p(s.cuda_stream)
+
+
+def version():
+    return _load().sdp_version().decode()

@@ -1,0 +1,104 @@
+"""Rank communication for the row-sharded engine.
+
+One process per GPU; each rank holds a contiguous row range of every column.
+Every statistic resolves through one of three collectives:
+
+* ``allgather``  -- pass-1 states, quantile samples, small candidate sets, top-k
+  lists; merged on every rank in rank order (deterministic results);
+* ``allreduce_sum`` -- histograms, radix digit histograms, Gram partials, counts
+  (int64 sums are exact, so order does not matter);
+* ``alltoallv`` -- hash-partitioned distinct keys / (key, count) groups.
+
+`LocalComm` is the single-process identity.  `TorchComm` uses
+torch.distributed: backend 'nccl' is RCCL over xGMI on ROCm; 'gloo' is used by
+the CPU tests (tensors are moved to the host for the collective).  gloo has no
+all_to_all, so alltoallv falls back to all_gather + local selection there.
+"""
+
+from __future__ import annotations
+
+from typing import List
+
+import torch
+
+
+class LocalComm:
+    rank = 0
+    world = 1
+
+    def allgather(self, t: torch.Tensor) -> List[torch.Tensor]:
+        return [t]
+
+    def allgatherv(self, t: torch.Tensor) -> List[torch.Tensor]:
+        return [t]
+
+    def allreduce_sum(self, t: torch.Tensor) -> torch.Tensor:
+        return t
+
+    def alltoallv(self, send: torch.Tensor, send_counts: List[int]) -> torch.Tensor:
+        assert len(send_counts) == 1
+        return send
+
+    def barrier(self):
+        pass
+
+
+class TorchComm:
+    def __init__(self, group=None):
+        import torch.distributed as dist
+        self.dist = dist
+        self.group = group
+        self.rank = dist.get_rank(group)
+        self.world = dist.get_world_size(group)
+        self.backend = dist.get_backend(group)
+        self.cpu = self.backend == 'gloo'
+
+    def _io(self, t):
+        return t.cpu() if self.cpu else t
+
+    def allgather(self, t):
+        x = self._io(t.contiguous())
+        outs = [torch.empty_like(x) for _ in range(self.world)]
+        self.dist.all_gather(outs, x, group=self.group)
+        return [o.to(t.device) for o in outs]
+
+    def allgatherv(self, t):
+        """all_gather of 1-D tensors whose lengths differ per rank."""
+        n = torch.tensor([t.numel()], dtype=torch.int64, device=t.device)
+        sizes = [int(s.item()) for s in self.allgather(n)]
+        m = max(sizes) if sizes else 0
+        pad = torch.zeros(m, dtype=t.dtype, device=t.device)
+        if t.numel():
+            pad[:t.numel()] = t.reshape(-1)
+        outs = self.allgather(pad)
+        return [o[:s] for o, s in zip(outs, sizes)]
+
+    def allreduce_sum(self, t):
+        x = self._io(t.contiguous()).clone()
+        self.dist.all_reduce(x, op=self.dist.ReduceOp.SUM, group=self.group)
+        return x.to(t.device)
+
+    def alltoallv(self, send, send_counts):
+        """send is laid out rank-major (send_counts[r] elements for rank r)."""
+        dev = send.device
+        counts = torch.tensor(send_counts, dtype=torch.int64, device=dev)
+        if self.cpu:
+            # gloo: no all_to_all -- gather everything and keep our slice
+            all_counts = self.allgather(counts)
+            all_send = self.allgatherv(send)
+            parts = []
+            for r in range(self.world):
+                c = all_counts[r].tolist()
+                start = sum(c[:self.rank])
+                parts.append(all_send[r][start:start + c[self.rank]])
+            return torch.cat(parts) if parts else send[:0]
+        recv_counts = torch.empty_like(counts)
+        self.dist.all_to_all_single(recv_counts, counts, group=self.group)
+        rc = recv_counts.tolist()
+        out = torch.empty(sum(rc), dtype=send.dtype, device=dev)
+        self.dist.all_to_all_single(out, send, output_split_sizes=rc, input_split_sizes=list(send_counts),
+                                    group=self.group)
+        return out
+
+    def barrier(self):
+        self.dist.barrier(group=self.group)

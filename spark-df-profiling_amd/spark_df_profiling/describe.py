@@ -1,0 +1,300 @@
+"""describe(): the reference's statistics entry point, computed on MI355X.
+
+Drop-in for /root/reference/spark_df_profiling/describe.py:66 -- same
+signature, same {'table', 'variables', 'freq'} result, same per-type key sets
+(SURVEY.md Appendix B), same quirks (Appendix C) and the same errors
+(TypeError for an unsupported input, ValueError('df cannot be empty'),
+NotImplementedError for array/struct/map columns).  The input widens from a
+Spark DataFrame to Arrow: a pyarrow Table/RecordBatch, a Spark DataFrame
+(collected as Arrow when pyspark is present) or a DeviceTable already in HBM.
+
+All row-level work runs in libsdp.so (engine.py); this module only performs the
+driver-side assembly the reference performs in pandas.
+"""
+
+from __future__ import annotations
+
+import math
+from collections import OrderedDict
+
+import numpy as np
+import pandas as pd
+import pyarrow as pa
+
+from .columns import DATE_TYPES, FLOAT_TYPES, INT_TYPES, DeviceColumn, DeviceTable
+from .engine import PROBS, TOPK, Engine, hist_edges  # noqa: F401
+from .utils import corr_from_gram, pretty_name
+
+OTHER_VALUES = '***Other Values***'                           # describe.py:262
+OTHER_DISTINCT = '***Other Values Distinct Count***'          # describe.py:263
+
+
+def fmt_bytesize(num, suffix='B'):
+    """Human-readable byte size, as the reference's formatters.fmt_bytesize."""
+    units = ['', 'Ki', 'Mi', 'Gi', 'Ti', 'Pi', 'Ei', 'Zi']
+    for u in units:
+        if abs(num) < 1024.0:
+            return "%3.1f %s%s" % (num, u, suffix)
+        num /= 1024.0
+    return "%.1f %s%s" % (num, 'Yi', suffix)
+
+
+def as_device_table(df, device=None) -> DeviceTable:
+    if isinstance(df, DeviceTable):
+        return df
+    if isinstance(df, (pa.Table, pa.RecordBatch)):
+        return DeviceTable.from_arrow(df, device)
+    # Spark DataFrame (pyspark optional): collect as Arrow, never row by row
+    to_arrow = getattr(df, 'toArrow', None) or getattr(df, '_collect_as_arrow', None)
+    if to_arrow is not None and type(df).__module__.startswith('pyspark'):
+        got = to_arrow()
+        if isinstance(got, list):
+            got = pa.Table.from_batches(got)
+        return DeviceTable.from_arrow(got, device)
+    raise TypeError('df must be of type pyspark.sql.DataFrame, pyarrow.Table or DeviceTable')
+
+
+def _series(values, col: DeviceColumn) -> pd.Series:
+    """The one-column pandas frame `toPandas().ix[:, 0]` yields for `values`."""
+    st = col.spark_type
+    if st in INT_TYPES:
+        return pd.Series(np.asarray(values, dtype=np.int64))
+    if st in ('float', 'double'):
+        return pd.Series(np.asarray(values, dtype=np.float64))
+    if st == 'boolean':
+        return pd.Series(np.asarray(values, dtype=bool))
+    if st == 'timestamp':
+        return pd.Series(pd.to_datetime(list(values)) if len(values) else pd.Series([], dtype='datetime64[ns]'))
+    return pd.Series(list(values), dtype=object)
+
+
+def _value_counts_first(engine, col, k):
+    """`df.select(c).na.drop().limit(k).toPandas().ix[:, 0].value_counts()`
+    (describe.py:276, :282) -- the rows are found on the GPU."""
+    return _series(engine.first_rows(col, k), col).value_counts()
+
+
+def describe_1d(engine: Engine, col: DeviceColumn, nrows, bins, k, freq, bundle):
+    """describe.py:136-189 for one column; `bundle` receives raw engine outputs."""
+    spark_t = col.spark_type
+    if ('array' in spark_t) or ('struct' in spark_t) or ('map' in spark_t) or col.kind == 'nested':
+        raise NotImplementedError('Column {c} is of type {t} and cannot be analyzed'.format(c=col.name, t=spark_t))
+
+    numeric = spark_t in INT_TYPES or spark_t in ('float', 'double')
+    tab = None
+    p1_pack = None
+    if col.kind == 'null':
+        distinct, count = 0, 0
+    elif numeric:
+        p1_pack = engine.numeric_pass1(col)
+        p1 = p1_pack[0]
+        count = p1['count']
+        hint = p1['n_valid']
+        if spark_t in INT_TYPES and p1['count']:
+            hint = min(hint, p1['imax'] - p1['imin'] + 1 + (p1['n_valid'] - p1['count']))
+        distinct = engine.distinct_fixed(col, with_counts=False, capacity_hint=hint)['groups']
+    elif spark_t in DATE_TYPES:
+        p1 = engine.minmax_pass(col)
+        bundle['minmax'] = p1
+        count = p1['count']
+        hint = p1['n_valid']
+        if p1['count']:
+            hint = min(hint, p1['imax'] - p1['imin'] + 1)
+        distinct = engine.distinct_fixed(col, with_counts=False, capacity_hint=hint)['groups']
+    elif col.kind == 'fixed':                      # boolean, decimal(20,0) from uint64
+        tab = engine.distinct_fixed(col, with_counts=True)
+        distinct, count = tab['groups'], tab['rows']
+    else:                                          # string, binary, decimal
+        tab = engine.value_counts_bytes(col)
+        distinct, count = tab['groups'], tab['rows']
+
+    res = OrderedDict()
+    res['distinct_count'] = np.int64(distinct)
+    res['count'] = np.int64(count)
+    with np.errstate(divide='ignore', invalid='ignore'):
+        res['p_unique'] = np.float64(distinct) / np.float64(count)
+    res['is_unique'] = np.bool_(distinct == nrows)
+    res['n_missing'] = np.int64(nrows - count)
+    res['p_missing'] = np.float64(nrows - count) / float(nrows)
+    res['p_infinite'] = np.int64(0)
+    res['n_infinite'] = np.int64(0)
+    res['memorysize'] = 0
+    bundle.update({'distinct_count': int(distinct), 'count': int(count)})
+
+    if distinct <= 1:
+        stats = OrderedDict([('type', 'CONST')])
+        stats['value_counts'] = _value_counts_first(engine, col, 1)
+    elif numeric:
+        st = engine.numeric_stats(col, bins=bins, k=k, p1_pack=p1_pack)
+        bundle['numeric'] = st
+        stats = _numeric_series(st, nrows)
+    elif spark_t in DATE_TYPES:
+        stats = _date_series(engine, col, bundle['minmax'], distinct, freq.upper())
+    elif bool(res['is_unique']):
+        stats = OrderedDict([('type', 'UNIQUE')])
+        stats['value_counts'] = _value_counts_first(engine, col, 50)
+    else:
+        stats = _categorical_series(engine, col, tab, count, bundle)
+    res.update(stats)
+    if res['type'] == 'CAT' and res['n_missing'] > 0:           # describe.py:169-170
+        res['distinct_count'] += 1
+    # mode (describe.py:174-187)
+    if res['count'] > res['distinct_count'] > 1:
+        res['mode'] = res['top'] if 'top' in res else 0
+    elif 'value_counts' in res:
+        vc = res['value_counts']
+        res['mode'] = vc.index[0] if len(vc) else 'MISSING'
+    else:
+        res['mode'] = 0
+    return res
+
+
+def _numeric_series(st, nrows):
+    """Key order and scalar types of describe_numeric_1d (describe.py:193-229)."""
+    s = OrderedDict()
+    for key in ('mean', 'min', 'max', 'variance', 'kurtosis', 'std', 'skewness', 'sum'):
+        s[key] = np.float64(getattr(st, key))
+    for p in PROBS:
+        s[pretty_name(p)] = np.float64(st.quantiles[p])
+    with np.errstate(all='ignore'):
+        s['range'] = np.float64(st.max) - np.float64(st.min)
+        q3, q1 = s[pretty_name(0.75)], s[pretty_name(0.25)]
+        s['iqr'] = q3 - q1
+        s['cv'] = s['std'] / float(s['mean'])
+        s['mad'] = np.float64(st.mad) / float(st.count)
+    s['type'] = 'NUM'
+    s['n_zeros'] = int(st.n_zero)
+    s['p_zeros'] = st.n_zero / float(nrows)
+    s['high_idx'] = int(st.high_idx)
+    s['low_idx'] = int(st.low_idx)
+    s['histogram'] = None            # filled after the GPU work (PNG rendering, plot.py)
+    s['mini_histogram'] = None
+    return s
+
+
+def _date_series(engine, col, p1, distinct, freq):
+    """describe_date_1d (describe.py:232-247)."""
+    from .engine import host_value
+    mn = host_value(p1['imin'], col)
+    mx = host_value(p1['imax'], col)
+    s = OrderedDict()
+    if isinstance(mx, pd.Timestamp):
+        s['min'] = str(mn.to_pydatetime())
+        s['max'] = str(mx.to_pydatetime())
+    else:
+        s['min'] = mn
+        s['max'] = mx
+        s['range'] = mx - mn
+    s['type'] = 'DATE'
+    s['completeness_idx'] = float(distinct) / len(pd.date_range(start=s['min'], end=s['max'], freq=freq))
+    return s
+
+
+def _categorical_series(engine, col, tab, count, bundle):
+    """describe_categorical_1d (describe.py:250-271).  Groups ordered by count
+    desc then key asc (the reference's orderBy leaves ties unspecified)."""
+    top = engine.topk(tab, TOPK)
+    values = engine.group_values(tab, [s for s, _ in top], col)
+    counts = [int(c) for _, c in top]
+    bundle['topk'] = list(zip(values, counts))
+    groups = tab['groups']
+    s = OrderedDict()
+    s['top'] = values[0]
+    s['freq'] = np.int64(counts[0])
+    others_count = int(count) - sum(counts)
+    others_distinct = int(groups) - len(counts)
+    s['value_counts'] = pd.Series(counts + [others_count, others_distinct],
+                                  index=pd.Index(values + [OTHER_VALUES, OTHER_DISTINCT], dtype=object),
+                                  dtype=np.int64)
+    s['type'] = 'CAT'
+    return s
+
+
+def describe(df, bins=10, corr_reject=0.9, **kwargs):
+    """describe.py:66-133.  Extra keyword arguments beyond the reference's
+    (k_vals, t_freq): ``comm`` (a comm.TorchComm for a row-sharded table -- each
+    rank passes its own row range), ``device``, ``plots`` (default True:
+    histogram PNGs as the reference stores them) and ``raw`` (a dict that
+    receives the per-column engine outputs, e.g. exact histogram counts)."""
+    comm = kwargs.pop('comm', None)
+    device = kwargs.pop('device', None)
+    plots = kwargs.pop('plots', True)
+    raw = kwargs.pop('raw', None)
+    table = as_device_table(df, device)
+    engine = Engine(device=device, comm=comm)
+    import torch
+    n_local = table.num_rows
+    n = int(engine.comm.allreduce_sum(torch.tensor([n_local], dtype=torch.int64, device=engine.device)).item())
+    table_stats = {'n': n}
+    if n == 0:
+        raise ValueError('df cannot be empty')
+
+    k_vals, t_freq = kwargs.get('k_vals') or {}, kwargs.get('t_freq') or {}
+    bundles = OrderedDict()
+    ldesc = OrderedDict()
+    for col in table.columns:
+        b = bundles.setdefault(col.name, {'spark_type': col.spark_type})
+        ldesc[col.name] = describe_1d(engine, col, n, bins, k_vals.get(col.name, 2), t_freq.get(col.name, 'D'), b)
+
+    if plots:
+        from .plot import complete_histogram, mini_histogram, hist_frame
+        for name, s in ldesc.items():
+            if s['type'] == 'NUM':
+                st = bundles[name]['numeric']
+                frame = hist_frame(st.hist_counts, st.edges, st.width)
+                s['histogram'] = complete_histogram(frame)
+                s['mini_histogram'] = mini_histogram(frame)
+
+    # correlation rejection (describe.py:89-100)
+    corr = None
+    if corr_reject is not None:
+        computable = [c for c in ldesc if ldesc[c]['type'] == 'NUM']
+        if len(computable) > 0:
+            corr = corr_matrix(engine, table, computable, bundles)
+            for x, corr_x in corr.iterrows():
+                for y, cv in corr_x.items():
+                    if x == y:
+                        break
+                    if cv >= corr_reject:
+                        ldesc[x] = OrderedDict([('type', 'CORR'), ('correlation_var', y), ('correlation', cv)])
+    if raw is not None:
+        raw.update({'columns': bundles, 'corr': corr})
+    return _assemble(ldesc, table_stats, len(table.columns))
+
+
+def corr_matrix(engine, table, columns, bundles):
+    """utils.py:20-36 on the GPU: one listwise-deletion mask + one Gram product."""
+    cols = [table.column(c) for c in columns]
+    shifts = [bundles[c]['numeric'].mean for c in columns]
+    check_nan = [bundles[c]['numeric'].n_nan > 0 for c in columns]
+    G, s, nk = engine.gram(cols, shifts, check_nan)
+    rho = corr_from_gram(G, s, nk)
+    return pd.DataFrame(rho, index=list(columns), columns=list(columns))
+
+
+def _assemble(ldesc, table_stats, nvar):
+    """describe.py:102-133."""
+    variable_stats = pd.DataFrame({k: pd.Series(list(v.values()), index=list(v.keys()), name=k, dtype=object)
+                                   for k, v in ldesc.items()})
+    table_stats['nvar'] = nvar
+    n = table_stats['n']
+    n_missing = pd.to_numeric(variable_stats.loc['n_missing'], errors='coerce')
+    table_stats['total_missing'] = float(n_missing.sum()) / (n * nvar)
+    high = pd.to_numeric(variable_stats.loc['high_idx'], errors='coerce')     # KeyError without NUM (:108)
+    low = pd.to_numeric(variable_stats.loc['low_idx'], errors='coerce')
+    cnt = pd.to_numeric(variable_stats.loc['count'], errors='coerce')
+    table_stats['accuracy_idx'] = 1 - ((high + low) / cnt).mean(skipna=True)
+    memsize = 0
+    table_stats['memsize'] = fmt_bytesize(memsize)
+    table_stats['recordsize'] = fmt_bytesize(memsize / n)
+    table_stats.update({k: 0 for k in ('NUM', 'DATE', 'CONST', 'CAT', 'UNIQUE', 'CORR')})
+    table_stats.update(dict(variable_stats.loc['type'].value_counts()))
+    table_stats['REJECTED'] = table_stats['CONST'] + table_stats['CORR']
+    freq_dict = {}
+    if 'value_counts' in variable_stats.index:
+        for var in variable_stats:
+            v = variable_stats[var]['value_counts']
+            if isinstance(v, pd.Series):
+                freq_dict[var] = v
+        variable_stats = variable_stats.drop('value_counts')
+    return {'table': table_stats, 'variables': variable_stats.T, 'freq': freq_dict}

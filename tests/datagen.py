@@ -1,0 +1,152 @@
+"""Seeded Arrow tables for the parity tests (numpy PCG64, fixed seeds)."""
+
+import datetime
+import decimal
+
+import numpy as np
+import pyarrow as pa
+
+
+def rng(seed):
+    return np.random.Generator(np.random.PCG64(seed))
+
+
+def legacy_table():
+    """tests.py.old.py:23-37 data as Spark would type it:
+    x bigint with a null, y double with a null, somedate timestamp."""
+    return pa.table({
+        'id': pa.array([chr(97 + c) for c in range(1, 10)]),
+        'x': pa.array([50, 50, -10, 0, 0, 5, 15, -3, None], pa.int64()),
+        'y': pa.array([0.000001, 654.152, None, 15.984512, 3122, -3.1415926535, 111, 15.9, 13.5], pa.float64()),
+        'cat': pa.array(['a', 'long text value', u'Élysée', '', None, 'some <b> B.s </div> </div> HTML stuff',
+                         'c', 'c', 'c']),
+        's1': pa.array(np.ones(9)),
+        's2': pa.array([u'some constant text $ % value {obj} ' for _ in range(1, 10)]),
+        'somedate': pa.array([datetime.datetime(2011, 7, 4), datetime.datetime(2022, 1, 1, 13, 57),
+                              datetime.datetime(1990, 12, 9), None, datetime.datetime(1990, 12, 9),
+                              datetime.datetime(1950, 12, 9), datetime.datetime(1898, 1, 2),
+                              datetime.datetime(1950, 12, 9), datetime.datetime(1950, 12, 9)],
+                             pa.timestamp('us')),
+    })
+
+
+def legacy_table_pandas_typed():
+    """The same data typed as pandas -> Spark would: x double with NaN."""
+    t = legacy_table()
+    x = pa.array([50.0, 50.0, -10.0, 0.0, 0.0, 5.0, 15.0, -3.0, float('nan')], pa.float64())
+    return t.set_column(t.schema.get_field_index('x'), 'x', x)
+
+
+def _mask(g, n, p):
+    return g.random(n) < p
+
+
+def numeric_table(n, seed=20261015, null_p=0.05):
+    g = rng(seed)
+    cols = {}
+    cols['f64_norm'] = g.standard_normal(n)
+    cols['f64_shift'] = 1e9 + g.standard_normal(n)
+    cols['f64_logn'] = g.lognormal(3, 2, n)
+    f = g.standard_normal(n)
+    f[_mask(g, n, 0.01)] = np.nan
+    f[_mask(g, n, 0.02)] = 0.0
+    f[_mask(g, n, 0.005)] = -0.0
+    cols['f64_nan_zero'] = f
+    cols['f32_unif'] = g.random(n).astype(np.float32)
+    cols['i64_small'] = g.integers(0, 1000, n)
+    cols['i64_wide'] = g.integers(-2 ** 31, 2 ** 31, n)
+    cols['i64_zipf'] = np.minimum(g.zipf(1.3, n), 10 ** 6).astype(np.int64)
+    cols['i32_seq'] = np.arange(n, dtype=np.int32)
+    cols['i16'] = g.integers(-300, 300, n).astype(np.int16)
+    cols['i8'] = g.integers(-128, 128, n).astype(np.int8)
+    cols['u8'] = g.integers(0, 256, n).astype(np.uint8)
+    cols['u32'] = g.integers(0, 2 ** 32, n, dtype=np.uint64).astype(np.uint32)
+    out = {}
+    for k, v in cols.items():
+        m = _mask(g, n, null_p) if k not in ('i32_seq',) else None
+        out[k] = pa.array(v, mask=m)
+    # heavy ties at the quartiles: 40% one value
+    h = g.standard_normal(n)
+    h[_mask(g, n, 0.4)] = 1.5
+    out['f64_heavy'] = pa.array(h)
+    return pa.table(out)
+
+
+def small_edge_table():
+    """Edge cases the reference's semantics define (App. C)."""
+    return pa.table({
+        'const_int': pa.array([7] * 6, pa.int64()),
+        'const_float_nan': pa.array([np.nan, 2.0, np.nan, 2.0, 2.0, np.nan], pa.float64()),
+        'all_null': pa.array([None] * 6, pa.int32()),
+        'all_nan': pa.array([np.nan] * 6, pa.float64()),
+        'two_vals': pa.array([1, 2, 1, 2, 1, 2], pa.int16()),
+        'one_valid': pa.array([None, None, 3.5, None, np.nan, None], pa.float64()),
+        'neg_zero': pa.array([0.0, -0.0, 1.0, -1.0, 0.0, 2.0], pa.float64()),
+        'int_extremes': pa.array([2 ** 63 - 1, -2 ** 63, 0, 1, -1, 5], pa.int64()),
+        'bools': pa.array([True, False, None, True, True, False], pa.bool_()),
+        'nulltype': pa.nulls(6),
+    })
+
+
+def categorical_table(n, seed=7, card=(100, 5000)):
+    g = rng(seed)
+    words = np.array(['w%05d_%s' % (i, 'x' * (i % 13)) for i in range(max(card))], dtype=object)
+    out = {}
+    z = np.minimum(g.zipf(1.2, n), card[0]) - 1
+    out['cat_zipf'] = pa.array(words[z], mask=_mask(g, n, 0.05))
+    u = g.integers(0, card[1], n)
+    out['cat_unif'] = pa.array(words[u])
+    out['cat_big'] = pa.array(['u%d' % i for i in g.permutation(n)])          # UNIQUE
+    out['cat_two'] = pa.array(np.where(g.random(n) < 0.7, 'Found', 'Fell').astype(object), mask=_mask(g, n, 0.01))
+    out['cat_empty'] = pa.array(np.where(g.random(n) < 0.5, '', 'Élysée').astype(object))
+    out['bool'] = pa.array(g.random(n) < 0.3, mask=_mask(g, n, 0.1))
+    out['large'] = pa.array(words[z].tolist(), type=pa.large_string())
+    out['bin'] = pa.array([w.encode() for w in words[u]], type=pa.binary())
+    out['dec'] = pa.array([decimal.Decimal(int(x)).scaleb(-2) for x in g.integers(-500, 500, n)],
+                          type=pa.decimal128(10, 2))
+    out['num'] = pa.array(g.integers(0, 50, n))     # describe.py:108 needs one NUM column
+    return pa.table(out)
+
+
+def date_table(n, seed=11):
+    g = rng(seed)
+    days = g.integers(-100000, 50000, n).astype(np.int32)
+    ts = g.integers(-2 * 10 ** 15, 2 * 10 ** 15, n)
+    return pa.table({
+        'd': pa.array(days, type=pa.date32(), mask=_mask(g, n, 0.05)),
+        'ts': pa.array(ts, type=pa.timestamp('us'), mask=_mask(g, n, 0.05)),
+        'num': pa.array(g.standard_normal(n)),
+    })
+
+
+def corr_table(n, seed=5):
+    g = rng(seed)
+    a = g.standard_normal(n)
+    b = a + 0.1 * g.standard_normal(n)             # rho ~ 0.995 -> CORR
+    c = -a + g.standard_normal(n)
+    d = g.random(n).astype(np.float32)
+    e = (100 * a).astype(np.int64)
+    return pa.table({'a': pa.array(a, mask=_mask(g, n, 0.03)), 'b': pa.array(b), 'c': pa.array(c),
+                     'd': pa.array(d, mask=_mask(g, n, 0.03)), 'e': pa.array(e)})
+
+
+def demo_like_table(n, seed=20261015):
+    """Config-1 column mix: Demo.ipynb-style meteorites."""
+    g = rng(seed)
+    labels = np.array(['L%03d' % i for i in range(466)], dtype=object)
+    reclat = g.uniform(-90, 90, n)
+    reclat[_mask(g, n, 0.14)] = 0.0
+    rmask = _mask(g, n, 0.19)
+    days = (g.integers(1688, 2102, n) - 1970) * 365
+    return pa.table({
+        'name': pa.array(['name%d' % i for i in range(n)]),
+        'id': pa.array(np.arange(n, dtype=np.int64)),
+        'nametype': pa.array(np.where(g.random(n) < 0.998, 'Valid', 'Relict').astype(object)),
+        'recclass': pa.array(labels[np.minimum(g.zipf(1.3, n), 466) - 1]),
+        'mass_g': pa.array(g.lognormal(3, 2, n), mask=_mask(g, n, 0.003)),
+        'fall': pa.array(np.where(g.random(n) < 0.976, 'Found', 'Fell').astype(object)),
+        'reclat': pa.array(reclat, mask=rmask),
+        'reclat_city': pa.array(reclat + g.standard_normal(n), mask=rmask),
+        'source': pa.array(['NASA'] * n),
+        'year': pa.array(days.astype(np.int32), type=pa.date32(), mask=_mask(g, n, 0.007)),
+    })
