@@ -784,7 +784,7 @@ extern "C" int sdp_compact_candidates(const uint64_t *d_cand, const uint32_t *d_
 
 extern "C" int sdp_radix_hist(const uint64_t *d_keys, const uint64_t *d_n, uint64_t prefix, int32_t shift,
                               uint64_t *d_hist, void *stream) {
-    if (shift < 0 || shift > 53) return set_error(SDP_EINVAL, "sdp_radix_hist: shift %d", shift);
+    if (shift < 0 || shift > 63) return set_error(SDP_EINVAL, "sdp_radix_hist: shift %d", shift);
     hipLaunchKernelGGL(radix_hist_kernel, dim3(512), dim3(256), 0, (hipStream_t)stream, d_keys, d_n, prefix, shift,
                        d_hist);
     return check_launch("radix_hist_kernel");

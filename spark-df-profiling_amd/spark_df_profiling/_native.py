@@ -106,7 +106,9 @@ _SIGNATURES = {
     'sdp_gram': (ctypes.c_int, [_COL, _I32, _P, _P, _P, _I64, _P, _P, _P, _P]),
 }
 
-_STATUS_FUNCS = {k for k, (r, _) in _SIGNATURES.items() if r is ctypes.c_int}
+_VALUE_FUNCS = {'sdp_last_error', 'sdp_version', 'sdp_pass1_workspace_bytes', 'sdp_pass2_workspace_bytes',
+                'sdp_pass1_grid', 'sdp_gram_workspace_bytes'}
+_STATUS_FUNCS = set(_SIGNATURES) - _VALUE_FUNCS
 
 _lib = None
 

@@ -22,6 +22,7 @@ from __future__ import annotations
 
 import ctypes
 import math
+from fractions import Fraction
 from dataclasses import dataclass, field
 from typing import Dict, List, Optional
 
@@ -176,7 +177,12 @@ class Engine:
                 frac = 1.0 if plan.n_sample < 64 else min(1.0, (plan.in_sample[w] + 2.0) / plan.n_sample)
                 exp = frac * rows_pb
                 cap = max(cap, int(2.0 * exp + 6.0 * math.sqrt(exp) + 64))
-            cap = min(cap, int(math.ceil(rows_pb)) + 64 + 4 * 256)
+            # a block's rows come from whole grid-strided tiles; at small n a window
+            # can sit inside one tile (sorted data), so give every block room for
+            # all its rows (<= 2^24 rows: at most 5 x 128 MiB of slots)
+            tile_rows = 256 * 4 * (16 // nat.ELEM_SIZE[col.dtype])
+            full = int(math.ceil(n / max(grid, 1) / tile_rows + 1)) * tile_rows
+            cap = full if n <= (1 << 24) else min(cap, full)
         cand = self._u64(max(nw, 1) * grid * max(cap, 1))
         cand_counts = torch.zeros(max(nw, 1) * grid, dtype=torch.int32, device=self.device)
         res_dev = self._bytes(ctypes.sizeof(nat.SdpPass1Result))
@@ -570,7 +576,8 @@ class Engine:
                 bits.append(b)
             byts = vb[torch.tensor([b // 8 for b in bits], dtype=torch.int64, device=self.device)].cpu().tolist()
             return [bool((x >> (b % 8)) & 1) for x, b in zip(byts, bits)]
-        v = col.values[torch.tensor(rows, dtype=torch.int64, device=self.device)].cpu().numpy()
+        tv = typed_values(col)
+        v = tv[torch.tensor(rows, dtype=torch.int64, device=self.device)].cpu().numpy()
         if col.dtype == nat.U64:
             v = v.view(np.uint64)
         elif col.dtype == nat.U32:
@@ -656,6 +663,7 @@ def merge_pass1_results(parts):
         'dmin': min(p.dmin for p in parts), 'dmax': max(p.dmax for p in parts),
         'shift': parts[0].shift,
         's1': math.fsum([x for p in parts for x in (p.s1_hi, p.s1_lo)]),
+        's1_hi': 0.0, 's1_lo': 0.0,
         's2': math.fsum([p.s2 for p in parts]),
         's3': math.fsum([x for p in parts for x in (p.s3_hi, p.s3_lo)]),
         's4': math.fsum([p.s4 for p in parts]),
@@ -665,6 +673,10 @@ def merge_pass1_results(parts):
         'w_in': [sum(p.w_in[w] for p in parts) for w in range(W)],
         'w_overflow': 0,
     }
+    # s1 as an unevaluated pair (hi + lo) exact to ~2^-106 for the mean
+    hi = math.fsum([x for p in parts for x in (p.s1_hi, p.s1_lo)])
+    lo = float(sum((Fraction(x) for p in parts for x in (p.s1_hi, p.s1_lo)), Fraction(0)) - Fraction(hi))
+    out['s1_hi'], out['s1_lo'] = hi, lo
     isum = 0
     for p in parts:
         isum = (isum + p.isum) & U64
@@ -680,7 +692,9 @@ def moments(p1, is_int):
     n = p1['count']
     K = p1['shift']
     s1, s2, s3, s4 = p1['s1'], p1['s2'], p1['s3'], p1['s4']
-    dsum = math.fsum([K * n, s1]) if n else 0.0
+    # Spark Average = (double sum) / count: the sum is rounded once, from the
+    # exact K*n + s1 (Fraction arithmetic on the host, a handful of operations)
+    dsum = float(Fraction(K) * n + Fraction(p1['s1_hi']) + Fraction(p1['s1_lo'])) if n else 0.0
     mean = dsum / n if n else float('nan')
     m = s1 / n if n else 0.0
     M2 = s2 - s1 * s1 / n if n else 0.0
@@ -706,6 +720,21 @@ def moments(p1, is_int):
 # ----------------------------------------------------------------------------
 # key / value conversions for host assembly
 # ----------------------------------------------------------------------------
+
+_TORCH_DT = {nat.I8: torch.int8, nat.I16: torch.int16, nat.I32: torch.int32, nat.I64: torch.int64,
+             nat.U8: torch.uint8, nat.U16: torch.int16, nat.U32: torch.int32, nat.U64: torch.int64,
+             nat.F32: torch.float32, nat.F64: torch.float64}
+
+
+def typed_values(col: DeviceColumn):
+    """The column's value bytes viewed as its element type (length rows)."""
+    t = _TORCH_DT[col.dtype]
+    es = nat.ELEM_SIZE[col.dtype]
+    v = col.values
+    if v.dtype == torch.uint8:
+        v = v[:col.length * es].view(t)
+    return v[:col.length]
+
 
 def host_value(x, col: DeviceColumn):
     """A raw element as the driver sees it after toPandas (numpy scalar)."""

@@ -84,6 +84,11 @@ def assert_describe_equal(got, want):
             if k not in gv.columns:
                 continue
             a, b = gv.loc[name, k], wv.loc[name, k]
+            if k == 'mad' and not _isnan(b) and b is not None:
+                # mad inherits the mean's last-ulp rounding: |d mad / d mean| <= 1
+                m = float(wv.loc[name, 'mean'])
+                if abs(float(a) - float(b)) <= REL * abs(float(b)) + 4 * np.spacing(abs(m)):
+                    continue
             if not same_value(k, a, b):
                 problems.append('%s.%s: %r vs %r' % (name, k, a, b))
     if set(got['freq']) != set(want['freq']):
