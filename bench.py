@@ -1,0 +1,342 @@
+#!/usr/bin/env python3
+"""bench.py -- profile rows/s of describe() on MI355X (BASELINE.json metric).
+
+Workload: a synthetic table of `--rows` rows (default
+1e9) x 16 columns with 5 % nulls per cell (Arrow validity, no NaN), generated
+directly in HBM by torch from fixed seeds, row-sharded in contiguous ranges
+across ranks (strong scaling: the whole table is fixed, each of N ranks holds
+rows/N):
+  6 x fp64   N(0,1), N(1e9,1), lognormal(0,1), U(-1e6,1e6), exp(1), Student-t(3)
+  4 x int64  U[0,1e6), U[-2^31,2^31), zipf(1.2), sequential id
+  2 x fp32   N(0,1), U[0,1)
+  3 x utf8   zipf(1.1) over 100 / 1e5 / 1e8 labels, 4-16 bytes (large_string)
+  1 x date32 U[1688-01-01, 2101-12-31]
+
+One step = one full describe() (every column's statistics, the Pearson matrix
+with CORR rejection, the histogram PNGs) over the resident table.  Inputs are in
+HBM when the timed region starts; H2D is not timed.
+
+    python bench.py [--gpus N --steps K --warmup W --rows R]
+    torchrun --nproc-per-node N bench.py --gpus N ...     (one rank per GPU, RCCL)
+
+Rank 0 prints one JSON line.  `roofline` is for the dominant kernel, timed with
+HIP events on the launch stream; `cpu_baseline` is the oracle (CPU restatement)
+on a bounded sample of the same workload, rank 0 at N=1 only.
+"""
+
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, 'spark-df-profiling_amd'))
+
+METRIC = 'profile rows/sec (whole node) + % HBM roofline, 1B-row x16 col at 1/2/4/8 GPUs'
+HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md:36 (spec)
+NULL_P = 0.05
+SEED = 20261015
+
+
+# ----------------------------------------------------------------------------
+# synthetic C3 shard in HBM
+# ----------------------------------------------------------------------------
+
+def _gen(seed, device):
+    g = torch.Generator(device=device)
+    g.manual_seed(seed)
+    return g
+
+
+def _validity(n, g, device):
+    """Arrow LSB-first bitmap with P(null) = NULL_P, padded by 8 bytes."""
+    nb = (n + 7) // 8
+    bits = torch.rand(nb * 8, generator=g, device=device) >= NULL_P
+    w = torch.tensor([1, 2, 4, 8, 16, 32, 64, 128], dtype=torch.int32, device=device)
+    packed = (bits.view(nb, 8).to(torch.int32) * w).sum(1).to(torch.uint8)
+    out = torch.zeros(nb + 8, dtype=torch.uint8, device=device)
+    out[:nb] = packed
+    return out
+
+
+def _bounded_zipf(n, s, card, g, device):
+    """Continuous power-law inverse CDF on [1, card+1) -> labels 0..card-1."""
+    u = torch.rand(n, generator=g, device=device, dtype=torch.float64)
+    a = 1.0 - s
+    x = torch.pow(1.0 - u * (1.0 - (card + 1.0) ** a), 1.0 / a)
+    return torch.clamp(x.floor().to(torch.int64) - 1, 0, card - 1)
+
+
+def _mix(x):
+    x = x ^ (x >> 31)
+    x = x * 0x7FB5D329728EA185
+    x = x ^ (x >> 27)
+    x = x * 0x3C79AC492BA7B653
+    return x ^ (x >> 33)
+
+
+_HEX = torch.tensor(list(b'0123456789abcdef'), dtype=torch.uint8)
+_FILL = torch.tensor(list(b'ghijklmnopqrstuvwxyzGHIJ'), dtype=torch.uint8)
+
+
+def _string_column(labels, card, device, chunk=1 << 25):
+    """utf8 (int64 offsets): label l -> hex digits of l then filler, 4-16 bytes."""
+    ndig = max(1, math.ceil(math.log(card, 16))) if card > 1 else 1
+    h = _mix(labels.clone())
+    lens = torch.clamp(4 + (h & 0x7FFFFFFF) % 13, min=ndig).to(torch.int64)
+    offsets = torch.zeros(labels.numel() + 1, dtype=torch.int64, device=device)
+    torch.cumsum(lens, 0, out=offsets[1:])
+    total = int(offsets[-1].item())
+    data = torch.zeros(total + 16, dtype=torch.uint8, device=device)
+    hexd, fill = _HEX.to(device), _FILL.to(device)
+    n = labels.numel()
+    for s in range(0, n, chunk):
+        e = min(n, s + chunk)
+        L = lens[s:e]
+        rows = torch.repeat_interleave(torch.arange(s, e, device=device), L)
+        pos = torch.arange(rows.numel(), device=device) - (offsets[rows] - offsets[s])
+        lab = labels[rows]
+        shift = (ndig - 1 - pos).clamp(min=0) * 4
+        digit = hexd[((lab >> shift) & 15)]
+        filler = fill[(_mix(lab + pos) & 0xFFFF) % fill.numel()]
+        data[int(offsets[s].item()):int(offsets[e].item())] = torch.where(pos < ndig, digit, filler)
+    return offsets, data
+
+
+def make_c3_shard(rows_total, rank, world, device):
+    from spark_df_profiling import _native as nat
+    from spark_df_profiling.columns import DeviceColumn, DeviceTable
+    per = rows_total // world
+    start = rank * per
+    n = per if rank < world - 1 else rows_total - start
+    cols = []
+
+    def fixed(name, spark_t, dtype, values, seed):
+        g = _gen(seed * 131 + rank, device)
+        c = DeviceColumn(name, spark_t, n, 'fixed', dtype)
+        c.values = values
+        c.validity = _validity(n, g, device)
+        cols.append(c)
+
+    k = 0
+    f64 = [('f64_norm', lambda g: torch.randn(n, generator=g, device=device, dtype=torch.float64)),
+           ('f64_shifted', lambda g: 1e9 + torch.randn(n, generator=g, device=device, dtype=torch.float64)),
+           ('f64_lognormal', lambda g: torch.exp(torch.randn(n, generator=g, device=device, dtype=torch.float64))),
+           ('f64_uniform', lambda g: (torch.rand(n, generator=g, device=device, dtype=torch.float64) * 2 - 1) * 1e6),
+           ('f64_exp', lambda g: -torch.log1p(-torch.rand(n, generator=g, device=device, dtype=torch.float64))),
+           ('f64_student_t3', lambda g: torch.randn(n, generator=g, device=device, dtype=torch.float64) / torch.sqrt(
+               (torch.randn(n, generator=g, device=device, dtype=torch.float64) ** 2
+                + torch.randn(n, generator=g, device=device, dtype=torch.float64) ** 2
+                + torch.randn(n, generator=g, device=device, dtype=torch.float64) ** 2) / 3.0))]
+    for name, fn in f64:
+        k += 1
+        fixed(name, 'double', nat.F64, fn(_gen(SEED + k * 1000 + rank, device)), SEED + k)
+    i64 = [('i64_uniform_1e6', lambda g: torch.randint(0, 10 ** 6, (n,), generator=g, device=device)),
+           ('i64_uniform_2p31', lambda g: torch.randint(-2 ** 31, 2 ** 31, (n,), generator=g, device=device)),
+           ('i64_zipf', lambda g: _bounded_zipf(n, 1.2, 2 ** 40, g, device) + 1),
+           ('i64_id', lambda g: torch.arange(start, start + n, dtype=torch.int64, device=device))]
+    for name, fn in i64:
+        k += 1
+        fixed(name, 'bigint', nat.I64, fn(_gen(SEED + k * 1000 + rank, device)), SEED + k)
+    f32 = [('f32_norm', lambda g: torch.randn(n, generator=g, device=device, dtype=torch.float32)),
+           ('f32_uniform', lambda g: torch.rand(n, generator=g, device=device, dtype=torch.float32))]
+    for name, fn in f32:
+        k += 1
+        fixed(name, 'float', nat.F32, fn(_gen(SEED + k * 1000 + rank, device)), SEED + k)
+    for name, card in (('str_card100', 100), ('str_card1e5', 10 ** 5), ('str_card1e8', 10 ** 8)):
+        k += 1
+        g = _gen(SEED + k * 1000 + rank, device)
+        labels = _bounded_zipf(n, 1.1, card, g, device)
+        offsets, data = _string_column(labels, card, device)
+        del labels
+        c = DeviceColumn(name, 'string', n, 'bytes')
+        c.offsets, c.data, c.offset_width = offsets, data, 8
+        c.validity = _validity(n, _gen(SEED + k * 131 + rank, device), device)
+        cols.append(c)
+    k += 1
+    lo = (np.datetime64('1688-01-01') - np.datetime64('1970-01-01')).astype(int)
+    hi = (np.datetime64('2101-12-31') - np.datetime64('1970-01-01')).astype(int)
+    days = torch.randint(int(lo), int(hi) + 1, (n,), generator=_gen(SEED + k * 1000 + rank, device),
+                         device=device, dtype=torch.int32)
+    fixed('date', 'date', nat.I32, days, SEED + k)
+    torch.cuda.synchronize()
+    return DeviceTable(cols, n)
+
+
+def table_bytes(table):
+    """Resident bytes of the shard (values, offsets, string bytes, validity)."""
+    b = 0
+    for c in table.columns:
+        for t in (c.values, c.validity, c.offsets, c.data):
+            if t is not None:
+                b += t.numel() * t.element_size()
+    return b
+
+
+# ----------------------------------------------------------------------------
+# algorithmic bytes per kernel launch, for the roofline object
+# ----------------------------------------------------------------------------
+
+def _col_bytes(c):
+    if c.kind == 'bytes':
+        return (c.offsets.numel() * c.offsets.element_size() + c.data.numel() - 16) / max(c.length, 1) + 0.125
+    return c.values.element_size() + 0.125
+
+
+def kernel_alg_bytes(table, raw):
+    """{entry point: [bytes per launch, in launch order]} for the row-streaming
+    kernels: each reads its column once (values + validity bit); hash kernels
+    also write/read their groups (16 B per group for sets, 32 B with counts)."""
+    out = {}
+    for c in table.columns:
+        b = raw['columns'][c.name]
+        n = c.length
+        w = _col_bytes(c)
+        if c.kind == 'bytes':
+            out.setdefault('sdp_hash_bytes', []).append(n * w + 32 * b['distinct_count'])
+        elif c.spark_type in ('double', 'float', 'bigint', 'int', 'smallint', 'tinyint', 'date'):
+            out.setdefault('sdp_pass1', []).append(n * w)
+            out.setdefault('sdp_hash_u64', []).append(n * w + 16 * b['distinct_count'])
+            if 'numeric' in b:
+                out.setdefault('sdp_pass2', []).append(n * w)
+    return out
+
+
+def roofline(rec, alg):
+    """Dominant entry point by total event time -> achieved GB/s vs HBM peak."""
+    torch.cuda.synchronize()
+    times = {k: [a.elapsed_time(b) for a, b in v] for k, v in rec.items()}
+    tot = {k: sum(v) for k, v in times.items()}
+    dom = max((k for k in tot if k in alg), key=lambda k: tot[k])
+    nl = len(times[dom])
+    steps = max(1, nl // max(1, len(alg[dom])))
+    per_launch_bytes = sum(alg[dom]) / len(alg[dom])
+    avg_ms = tot[dom] / nl
+    achieved = per_launch_bytes / (avg_ms * 1e-3) / 1e9
+    return {'bound': 'hbm', 'kernel': dom, 'achieved': round(achieved, 1), 'peak': HBM_PEAK_GBS,
+            'unit': 'GB/s', 'frac': round(achieved / HBM_PEAK_GBS, 4), 'traffic': None,
+            'launches_per_step': nl // steps, 'avg_launch_ms': round(avg_ms, 4),
+            'alg_bytes_per_launch': int(per_launch_bytes)}, {k: round(v / steps, 3) for k, v in tot.items()}
+
+
+# ----------------------------------------------------------------------------
+# CPU baseline: the oracle (CPU restatement, not reference Spark) on a sample
+# ----------------------------------------------------------------------------
+
+def cpu_baseline(sample_rows, device):
+    import pyarrow as pa
+    import oracle
+    sys.path.insert(0, ROOT)
+    shard = make_c3_shard(sample_rows, 0, 1, device)
+    arrays = {}
+    for c in shard.columns:
+        n = c.length
+        valid = np.unpackbits(c.validity[:(n + 7) // 8].cpu().numpy(), bitorder='little')[:n].astype(bool)
+        if c.kind == 'bytes':
+            offs = c.offsets.cpu().numpy()
+            data = c.data.cpu().numpy().tobytes()
+            arr = pa.LargeStringArray.from_buffers(n, pa.py_buffer(offs.tobytes()), pa.py_buffer(data),
+                                                   pa.py_buffer(np.packbits(valid, bitorder='little').tobytes()))
+        elif c.spark_type == 'date':
+            arr = pa.array(c.values.cpu().numpy(), type=pa.date32(), mask=~valid)
+        else:
+            arr = pa.array(c.values.cpu().numpy(), mask=~valid)
+        arrays[c.name] = arr
+    table = pa.table(arrays)
+    del shard
+    torch.cuda.empty_cache()
+    t0 = time.perf_counter()
+    oracle.describe(table)
+    dt = time.perf_counter() - t0
+    return {'value': round(sample_rows / dt, 1), 'unit': 'rows/s', 'cores': 1, 'kind': 'port',
+            'sample': '%d rows x 16 cols of the same C3 generator; oracle/ numpy restatement '
+                      '(CPU restatement, not reference Spark: no pyspark/JVM in the image), %.1f s' % (sample_rows, dt)}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument('--gpus', type=int, default=1)
+    ap.add_argument('--steps', type=int, default=3)
+    ap.add_argument('--warmup', type=int, default=1)
+    ap.add_argument('--rows', type=int, default=10 ** 9)
+    ap.add_argument('--cpu-sample-rows', type=int, default=1 << 20)
+    ap.add_argument('--no-cpu-baseline', action='store_true')
+    ap.add_argument('--no-plots', action='store_true')
+    args = ap.parse_args()
+
+    world = int(os.environ.get('WORLD_SIZE', '1'))
+    rank = int(os.environ.get('RANK', '0'))
+    local = int(os.environ.get('LOCAL_RANK', '0'))
+    torch.cuda.set_device(local)
+    device = torch.device('cuda', local)
+    comm = None
+    if world > 1:
+        import torch.distributed as dist
+        os.environ.setdefault('MASTER_ADDR', '127.0.0.1')
+        dist.init_process_group('nccl', device_id=device)
+        from spark_df_profiling.comm import TorchComm
+        comm = TorchComm()
+
+    from spark_df_profiling import describe
+    from spark_df_profiling import _native as nat
+
+    t_gen = time.perf_counter()
+    table = make_c3_shard(args.rows, rank, world, device)
+    t_gen = time.perf_counter() - t_gen
+
+    def step(raw=None):
+        return describe(table, comm=comm, plots=not args.no_plots, raw=raw)
+
+    for _ in range(args.warmup):
+        step()
+
+    def barrier():
+        if comm is not None:
+            comm.barrier()
+        torch.cuda.synchronize()
+
+    raw = {}
+    barrier()
+    rec = nat.start_recording()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        step(raw if i == 0 else None)
+    barrier()
+    t1 = time.perf_counter()
+    nat.stop_recording()
+    elapsed = t1 - t0
+    if comm is not None:
+        el = torch.tensor([elapsed], dtype=torch.float64, device=device)
+        elapsed = float(torch.stack(comm.allgather(el)).max().item())
+    rl, per_kernel_ms = roofline(rec, kernel_alg_bytes(table, raw))
+
+    if rank != 0:
+        return
+    out = {
+        'metric': METRIC, 'value': round(args.rows * args.steps / elapsed, 1), 'unit': 'rows/s',
+        'n_gpus': world, 'steps': args.steps, 'warmup': args.warmup,
+        'ms_per_step': round(1e3 * elapsed / args.steps, 2), 'higher_is_better': True, 'scaling': 'strong',
+        'vs_baseline': None, 'dtype': 'f64', 'data': 'synthetic (torch, seeded, generated in HBM)',
+        'config': {'workload': 'C3: %d rows x 16 mixed columns (6 f64, 4 i64, 2 f32, 3 utf8, 1 date32), '
+                               '5%% nulls, row-sharded' % args.rows,
+                   'rows': args.rows, 'columns': 16, 'parallelism': 'row-shard x%d' % world,
+                   'plots': not args.no_plots},
+        'roofline': rl,
+        'per_kernel_ms_per_step': per_kernel_ms,
+        'resident_gb_per_gpu': round(table_bytes(table) / 1e9, 2),
+        'gen_s': round(t_gen, 1),
+    }
+    if world == 1 and not args.no_cpu_baseline:
+        del table
+        torch.cuda.empty_cache()
+        out['cpu_baseline'] = cpu_baseline(args.cpu_sample_rows, device)
+    print(json.dumps(out))
+
+
+if __name__ == '__main__':
+    main()

@@ -143,7 +143,15 @@ class _Caller:
             return fn
 
         def call(*args):
+            rec = _recorder
+            if rec is not None:
+                ev0 = torch.cuda.Event(enable_timing=True)
+                ev0.record()
             rc = fn(*args)
+            if rec is not None:
+                ev1 = torch.cuda.Event(enable_timing=True)
+                ev1.record()
+                rec.setdefault(name, []).append((ev0, ev1))
             if rc != 0:
                 msg = lib.sdp_last_error().decode(errors='replace')
                 raise NativeError('%s failed (status %d): %s' % (name, rc, msg))
@@ -153,6 +161,23 @@ class _Caller:
 
 
 sdp = _Caller()
+
+# Optional per-entry-point HIP event timing (bench.py): {name: [(start, end)]}.
+# Events are recorded on the current torch stream, the stream every entry point
+# is launched on; nothing synchronises until the caller reads them.
+_recorder = None
+
+
+def start_recording():
+    global _recorder
+    _recorder = {}
+    return _recorder
+
+
+def stop_recording():
+    global _recorder
+    rec, _recorder = _recorder, None
+    return rec
 
 
 def ptr(t):

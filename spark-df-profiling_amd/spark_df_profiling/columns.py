@@ -63,6 +63,11 @@ _NUMERIC_DTYPE = {
 }
 
 
+_TORCH_OF = {nat.I8: torch.int8, nat.I16: torch.int16, nat.I32: torch.int32, nat.I64: torch.int64,
+             nat.U8: torch.uint8, nat.U16: torch.int16, nat.U32: torch.int32, nat.U64: torch.int64,
+             nat.F32: torch.float32, nat.F64: torch.float64}
+
+
 @dataclass
 class DeviceColumn:
     """One Arrow column in HBM.
@@ -260,7 +265,8 @@ def column_from_arrow(name, arr, device) -> DeviceColumn:
     else:
         raise NotImplementedError('Column {c} is of type {t} and cannot be analyzed'.format(c=name, t=spark_t))
     vals = np.frombuffer(bufs[1], dtype=tdt, count=n, offset=arr.offset * np.dtype(tdt).itemsize)
-    col.values = _to_device(vals, device, pad=16)
+    raw = _to_device(vals, device, pad=16)
+    col.values = raw[:n * vals.itemsize].view(_TORCH_OF[col.dtype])
     return col
 
 
