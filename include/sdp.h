@@ -129,10 +129,13 @@ int sdp_quantile_plan(uint64_t *d_sample, int32_t n_sample, const double *probs,
                       int32_t n_probs, int32_t is_float, sdp_qplan *d_plan,
                       void *stream);
 
+#define SDP_PASS1_WAVES 4     /* waves per pass-1 workgroup = candidate segments per block */
+
 /* Fused pass 1 over one numeric column (see sdp_pass1_result).  Candidates
- * (keys strictly inside window w) go to per-block slots
- * d_cand[(w*grid + b)*slot_capacity ...]; per-block counts (clamped to
- * slot_capacity; overflow flagged in w_overflow) to d_cand_counts[w*grid + b]. */
+ * (keys strictly inside window w) go to wave-private slot ranges: segment
+ * s = (w*grid + b)*SDP_PASS1_WAVES + wave holds d_cand[s*slot_capacity ...], its
+ * count (clamped to slot_capacity; overflow flagged in w_overflow) in
+ * d_cand_counts[s]. */
 int sdp_pass1(const sdp_column *col, const sdp_qplan *d_plan, void *d_work,
               int64_t work_bytes, uint64_t *d_cand, uint32_t *d_cand_counts,
               int64_t slot_capacity, sdp_pass1_result *d_result, void *stream);
@@ -140,10 +143,14 @@ int sdp_pass1(const sdp_column *col, const sdp_qplan *d_plan, void *d_work,
 /* Grid size sdp_pass1 uses for `length` rows (host-only). */
 int32_t sdp_pass1_grid(int64_t length, int32_t dtype);
 
-/* Gather the per-block candidate slots of window w into a dense array. */
+/* Gather `nseg` segments of `slot_capacity` u64 slots (segment s holds
+ * d_cand_counts[s] entries) into a dense array, in segment order;
+ * *d_out_count receives the total.  d_offsets_work: nseg u64 of workspace.
+ * Used for pass-1 candidates (nseg = windows' grid*SDP_PASS1_WAVES) and for the
+ * groups sdp_group_dedup leaves at the front of each bucket. */
 int sdp_compact_candidates(const uint64_t *d_cand, const uint32_t *d_cand_counts,
-                           int32_t grid, int64_t slot_capacity, uint64_t *d_out,
-                           uint64_t *d_out_count, void *stream);
+                           int32_t nseg, int64_t slot_capacity, uint64_t *d_offsets_work,
+                           uint64_t *d_out, uint64_t *d_out_count, void *stream);
 
 /* Radix-select support: 2048-bin histogram of key bits [shift, shift+11) over
  * keys whose bits above shift+11 equal `prefix` (prefix_bits = 64-shift-11). */
@@ -184,6 +191,8 @@ int sdp_hash_bytes(const sdp_bytes_column *col, uint64_t *d_slots, uint64_t *d_c
                    int64_t capacity, uint64_t *d_stats, void *stream);
 
 /* Top-k groups by (count desc, key asc) from a table built with counts.
+ * `bytes_keys` is a flag word: bit0 byte keys (EMPTY slot = 0), bit1 dense
+ * group arrays (every slot is a group, as compacted from sdp_group_dedup).
  * Histogram of floor(log2(count)) over occupied slots (64 bins). */
 int sdp_table_count_log2_hist(const uint64_t *d_slots, const uint64_t *d_counts,
                               int64_t capacity, int32_t bytes_keys, uint64_t *d_hist,
@@ -215,6 +224,37 @@ int sdp_select_by_value(const uint64_t *d_sel, const uint64_t *d_vals, const uin
 /* Number of set validity bits (non-null rows), accumulated into *d_out. */
 int sdp_count_valid(const uint8_t *d_validity, int64_t bit_offset, int64_t length,
                     uint64_t *d_out, void *stream);
+
+/* ---- radix-partitioned grouping (sdp_group.hip) ----------------------------
+ * Exact distinct / value counts without a global hash table: rows are
+ * de-duplicated per tile in LDS and appended to 2^b1 hash buckets, the buckets
+ * re-partitioned by the next b2 hash bits (again de-duplicated in LDS), and
+ * every final bucket de-duplicated by one workgroup in LDS.  Records are
+ * structure-of-arrays; byte keys carry their 64-bit hash in d_key and a
+ * representative row in d_row, and are compared byte for byte.
+ * d_stats (68 x u64, zeroed by the caller): [0] rows, [1] rows whose u64 key is
+ * UINT64_MAX (kept outside the buckets), [2] bucket overflow, [3] LDS table
+ * full, [4..67] group count spread over 64 counters. */
+typedef struct sdp_buckets {
+    uint64_t *d_key;        /* [nbuckets][capacity]                         */
+    uint64_t *d_row;        /* byte keys only                               */
+    uint64_t *d_cnt;        /* per-record row counts (NULL: distinct only)  */
+    uint32_t *d_fill;       /* [nbuckets] records appended (zeroed)         */
+    int64_t   capacity;
+} sdp_buckets;
+
+int sdp_group_part_rows_u64(const sdp_column *col, int32_t b1, int32_t with_counts,
+                            const sdp_buckets *out, uint64_t *d_stats, void *stream);
+int sdp_group_part_rows_bytes(const sdp_bytes_column *col, int32_t b1,
+                              const sdp_buckets *out, uint64_t *d_stats, void *stream);
+/* L1 buckets (nb1 of them) -> nb1 * 2^b2 L2 buckets by hash bits [64-b1-b2, 64-b1). */
+int sdp_group_part_recs(const sdp_buckets *in, int32_t nb1, const sdp_buckets *out,
+                        int32_t b1, int32_t b2, const sdp_bytes_column *bytes_col,
+                        int32_t with_counts, uint64_t *d_stats, void *stream);
+/* One workgroup per bucket: groups written back to the front of the bucket
+ * (u64: key; bytes: (tag << 40 | row + 1)), d_ngroups[b] = groups in bucket b. */
+int sdp_group_dedup(const sdp_buckets *in, int64_t nbuckets, const sdp_bytes_column *bytes_col,
+                    int32_t with_counts, uint32_t *d_ngroups, uint64_t *d_stats, void *stream);
 
 /* ---- first rows (describe.py:276 limit(1), :282 limit(50)) ---------------- */
 /* Indices of the first k rows that survive na.drop (null, and NaN for floats). */

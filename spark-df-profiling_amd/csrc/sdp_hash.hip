@@ -268,8 +268,10 @@ __global__ void __launch_bounds__(H_BLOCK) hash_bytes_kernel(sdp_bytes_column co
     }
 }
 
-__device__ __forceinline__ bool occupied(const uint64_t *slots, int64_t i, int bytes_keys) {
-    return bytes_keys ? (slots[i] != 0) : (slots[i] != EMPTY64);
+// flags: bit0 = byte keys (EMPTY = 0), bit1 = dense group arrays (every slot a group)
+__device__ __forceinline__ bool occupied(const uint64_t *slots, int64_t i, int flags) {
+    if (flags & 2) return true;
+    return (flags & 1) ? (slots[i] != 0) : (slots[i] != EMPTY64);
 }
 
 __global__ void count_log2_hist_kernel(const uint64_t *slots, const uint64_t *counts, int64_t cap, int bytes_keys,

@@ -179,17 +179,19 @@ struct P1Thread {
     double dmin, dmax;
     double s1, s1c, s2, s3, s3c, s4;
     uint32_t gt[SDP_MAX_WINDOWS], eqlo[SDP_MAX_WINDOWS], eqhi[SDP_MAX_WINDOWS];
+    uint32_t wcur[SDP_MAX_WINDOWS];   // wave-uniform candidate cursors (wave-private slots)
 };
+
+constexpr int P1_WPB = 4;            // waves per pass-1 block (P1_BLOCK / WAVE)
 
 struct P1Ctx {
     uint64_t lo[SDP_MAX_WINDOWS], hi[SDP_MAX_WINDOWS];
     int nw;
     double K;
-    uint64_t *cand;           // [nw][grid][cap]
+    uint64_t *cand;           // [nw][grid][P1_WPB][cap]: one slot range per wave
     int64_t cap;
     int grid;
-    uint32_t *cursor;         // LDS [SDP_MAX_WINDOWS]
-    uint32_t *overflow;       // LDS
+    bool hne[SDP_MAX_WINDOWS]; // hi != lo
 };
 
 // One element; every lane of the wave calls this in lockstep (ballots inside).
@@ -227,19 +229,18 @@ __device__ __forceinline__ void p1_elem(P1Thread &st, const P1Ctx &cx, T x, bool
             const uint64_t lo = cx.lo[w], hi = cx.hi[w];
             st.gt[w] += (ok && key > hi);
             st.eqlo[w] += (ok && key == lo);
-            st.eqhi[w] += (ok && key == hi && hi != lo);
+            st.eqhi[w] += (ok && key == hi && cx.hne[w]);
             const bool inside = ok && key > lo && key < hi;
             const uint64_t m = __ballot(inside);
-            if (m) {
-                const int leader = __ffsll((long long)m) - 1;
-                uint32_t base = 0;
-                if (lane_id() == leader) base = atomicAdd(&cx.cursor[w], (uint32_t)__popcll(m));
-                base = __shfl(base, leader, WAVE);
+            if (m) {   // wave-uniform; no atomics: this wave owns its slot range
                 if (inside) {
-                    const uint32_t pos = base + (uint32_t)lane_rank(m);
-                    if ((int64_t)pos < cx.cap)
-                        cx.cand[((int64_t)w * cx.grid + blockIdx.x) * cx.cap + pos] = key;
+                    const uint32_t pos = st.wcur[w] + (uint32_t)lane_rank(m);
+                    if ((int64_t)pos < cx.cap) {
+                        const int64_t seg = ((int64_t)w * cx.grid + blockIdx.x) * P1_WPB + (threadIdx.x / WAVE);
+                        cx.cand[seg * cx.cap + pos] = key;
+                    }
                 }
+                st.wcur[w] += (uint32_t)__popcll(m);
             }
         }
     }
@@ -250,23 +251,19 @@ __global__ void __launch_bounds__(P1_BLOCK, 4) pass1_kernel(sdp_column col, cons
                                                          P1Partial *partials, uint64_t *cand,
                                                          uint32_t *cand_counts, int64_t cap) {
     constexpr int VPT = Vec16<T>::N;
-    __shared__ uint32_t s_cursor[SDP_MAX_WINDOWS];
-    __shared__ uint32_t s_overflow;
-
-    if (threadIdx.x < SDP_MAX_WINDOWS) s_cursor[threadIdx.x] = 0;
-    if (threadIdx.x == 0) s_overflow = 0;
 
     P1Ctx cx;
     cx.nw = plan->n_windows;
 #pragma unroll
-    for (int w = 0; w < SDP_MAX_WINDOWS; ++w) { cx.lo[w] = plan->lo[w]; cx.hi[w] = plan->hi[w]; }
+    for (int w = 0; w < SDP_MAX_WINDOWS; ++w) {
+        cx.lo[w] = plan->lo[w];
+        cx.hi[w] = plan->hi[w];
+        cx.hne[w] = cx.hi[w] != cx.lo[w];
+    }
     cx.K = plan->shift;
     cx.cand = cand;
     cx.cap = cap;
     cx.grid = gridDim.x;
-    cx.cursor = s_cursor;
-    cx.overflow = &s_overflow;
-    __syncthreads();
 
     P1Thread st;
     st.count = st.n_valid = st.n_nan = st.n_zero = 0;
@@ -277,7 +274,7 @@ __global__ void __launch_bounds__(P1_BLOCK, 4) pass1_kernel(sdp_column col, cons
     st.dmax = -__builtin_inf();
     st.s1 = st.s1c = st.s2 = st.s3 = st.s3c = st.s4 = 0.0;
 #pragma unroll
-    for (int w = 0; w < SDP_MAX_WINDOWS; ++w) st.gt[w] = st.eqlo[w] = st.eqhi[w] = 0;
+    for (int w = 0; w < SDP_MAX_WINDOWS; ++w) st.gt[w] = st.eqlo[w] = st.eqhi[w] = st.wcur[w] = 0;
 
     const int64_t n = col.length;
     const int64_t nvec = n / VPT;
@@ -340,23 +337,23 @@ __global__ void __launch_bounds__(P1_BLOCK, 4) pass1_kernel(sdp_column col, cons
             const uint64_t g = wave_sum_u64(st.gt[w]);
             const uint64_t e1 = wave_sum_u64(st.eqlo[w]);
             const uint64_t e2 = wave_sum_u64(st.eqhi[w]);
-            if (lane == 0) { s_u[wid][4 + w] = g; s_u[wid][4 + W_ + w] = e1; s_u[wid][4 + 2 * W_ + w] = e2; }
+            if (lane == 0) {
+                s_u[wid][4 + w] = g; s_u[wid][4 + W_ + w] = e1; s_u[wid][4 + 2 * W_ + w] = e2;
+                s_u[wid][4 + 3 * W_ + w] = st.wcur[w];
+                if (w < cx.nw)
+                    cand_counts[((int64_t)w * gridDim.x + blockIdx.x) * P1_WPB + wid] =
+                        (int64_t)st.wcur[w] < cap ? st.wcur[w] : (uint32_t)cap;
+            }
         }
     }
     __syncthreads();
     P1Partial *out = partials + blockIdx.x;
     const int t = threadIdx.x;
     constexpr int NW = P1_BLOCK / WAVE;
-    if (t < 4 + 3 * W_) {
+    if (t < NU) {
         uint64_t a = 0;
         for (int w = 0; w < NW; ++w) a += s_u[w][t];
         out->u[t] = a;
-    } else if (t < 4 + 4 * W_) {
-        const int w = t - (4 + 3 * W_);
-        out->u[t] = s_cursor[w];
-        if (w < cx.nw)
-            cand_counts[(int64_t)w * gridDim.x + blockIdx.x] =
-                (int64_t)s_cursor[w] < cap ? s_cursor[w] : (uint32_t)cap;
     } else if (t == 64) {
         int64_t a = s_i[0][0], mn = s_i[0][1], mx = s_i[0][2];
         for (int w = 1; w < NW; ++w) {
@@ -378,7 +375,8 @@ __global__ void __launch_bounds__(P1_BLOCK, 4) pass1_kernel(sdp_column col, cons
     } else if (t == 68) {
         uint32_t ovf = 0;
         for (int w = 0; w < cx.nw; ++w)
-            if ((int64_t)s_cursor[w] > cap) ovf |= 1u << w;
+            for (int v = 0; v < NW; ++v)
+                if ((int64_t)s_u[v][4 + 3 * W_ + w] > cap) ovf |= 1u << w;
         out->overflow = ovf;
         out->_pad = 0;
     }
@@ -430,22 +428,42 @@ __global__ void pass1_merge_kernel(const P1Partial *partials, int grid, const sd
 // candidate compaction and radix select
 // ============================================================================
 
-// d_counts[grid] per-block counts -> dense copy.  One workgroup per source block;
-// the exclusive prefix is recomputed per workgroup (grid <= 1024).
-__global__ void compact_cand_kernel(const uint64_t *cand, const uint32_t *counts, int grid,
-                                    int64_t cap, uint64_t *out, uint64_t *out_n) {
-    const int b = blockIdx.x;
-    __shared__ uint64_t s_base;
-    if (threadIdx.x == 0) {
-        uint64_t base = 0;
-        for (int i = 0; i < b; ++i) base += counts[i];
-        s_base = base;
-        if (b == grid - 1) *out_n = base + counts[b];
-    }
+// counts[nseg] per-segment counts -> dense copy, in two kernels: a single
+// workgroup scans the counts into exclusive offsets (chunks of 1024, carried
+// sequentially), then one workgroup per segment copies it.
+__global__ void __launch_bounds__(1024) scan_counts_kernel(const uint32_t *counts, int nseg, uint64_t *offs,
+                                                           uint64_t *total) {
+    __shared__ uint64_t s[1024];
+    __shared__ uint64_t carry;
+    if (threadIdx.x == 0) carry = 0;
     __syncthreads();
-    const uint32_t c = counts[b];
-    const uint64_t *src = cand + (int64_t)b * cap;
-    for (uint32_t i = threadIdx.x; i < c; i += blockDim.x) out[s_base + i] = src[i];
+    for (int base = 0; base < nseg; base += 1024) {
+        const int i = base + threadIdx.x;
+        const uint64_t v = i < nseg ? counts[i] : 0;
+        s[threadIdx.x] = v;
+        __syncthreads();
+        for (int o = 1; o < 1024; o <<= 1) {     // Hillis-Steele inclusive scan
+            const uint64_t t = threadIdx.x >= o ? s[threadIdx.x - o] : 0;
+            __syncthreads();
+            s[threadIdx.x] += t;
+            __syncthreads();
+        }
+        if (i < nseg) offs[i] = carry + s[threadIdx.x] - v;
+        __syncthreads();
+        if (threadIdx.x == 1023) carry += s[1023];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) *total = carry;
+}
+
+__global__ void copy_segments_kernel(const uint64_t *cand, const uint32_t *counts, const uint64_t *offs,
+                                     int nseg, int64_t cap, uint64_t *out) {
+    for (int b = blockIdx.x; b < nseg; b += gridDim.x) {
+        const uint32_t c = counts[b];
+        const uint64_t base = offs[b];
+        const uint64_t *src = cand + (int64_t)b * cap;
+        for (uint32_t i = threadIdx.x; i < c; i += blockDim.x) out[base + i] = src[i];
+    }
 }
 
 __global__ void radix_hist_kernel(const uint64_t *keys, const uint64_t *n_ptr, uint64_t prefix,
@@ -466,8 +484,48 @@ __global__ void radix_hist_kernel(const uint64_t *keys, const uint64_t *n_ptr, u
         if (h[i]) atomicAdd((unsigned long long *)&hist[i], (unsigned long long)h[i]);
 }
 
+// Block-staged compaction: matches gather in an LDS buffer and leave with one
+// global atomic per flush (not one per wave per iteration).
+constexpr int STAGE = 4096;
+
+struct Stager {
+    uint64_t *buf;      // LDS [STAGE]
+    uint32_t *cnt;      // LDS
+    uint64_t *gbase;    // LDS
+};
+
+// every thread calls with its candidate (keep) -- all threads of the block
+__device__ __forceinline__ void stage_push(Stager &sg, bool keep, uint64_t v, uint64_t *out,
+                                           unsigned long long *out_n, bool last) {
+    const uint64_t m = __ballot(keep);
+    if (m) {
+        uint32_t base = 0;
+        const int leader = __ffsll((long long)m) - 1;
+        if (lane_id() == leader) base = atomicAdd(sg.cnt, (uint32_t)__popcll(m));
+        base = __shfl(base, leader, WAVE);
+        if (keep) sg.buf[base + lane_rank(m)] = v;
+    }
+    __syncthreads();
+    const uint32_t c = *sg.cnt;
+    if (c > STAGE - blockDim.x || (last && c > 0)) {
+        if (threadIdx.x == 0) *sg.gbase = atomicAdd(out_n, (unsigned long long)c);
+        __syncthreads();
+        const uint64_t b = *sg.gbase;
+        for (uint32_t i = threadIdx.x; i < c; i += blockDim.x) out[b + i] = sg.buf[i];
+        __syncthreads();
+        if (threadIdx.x == 0) *sg.cnt = 0;
+    }
+    __syncthreads();
+}
+
 __global__ void radix_filter_kernel(const uint64_t *keys, const uint64_t *n_ptr, uint64_t prefix,
                                     int shift, uint64_t *out, uint64_t *out_n) {
+    __shared__ uint64_t s_buf[STAGE];
+    __shared__ uint32_t s_cnt;
+    __shared__ uint64_t s_gbase;
+    if (threadIdx.x == 0) s_cnt = 0;
+    __syncthreads();
+    Stager sg{s_buf, &s_cnt, &s_gbase};
     const uint64_t n = *n_ptr;
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
     const uint64_t iters = (n + stride - 1) / stride;
@@ -479,14 +537,7 @@ __global__ void radix_filter_kernel(const uint64_t *keys, const uint64_t *n_ptr,
             k = keys[i];
             keep = shift >= 64 ? true : ((k >> shift) == prefix);
         }
-        const uint64_t m = __ballot(keep);
-        if (m) {
-            const int leader = __ffsll((long long)m) - 1;
-            unsigned long long base = 0;
-            if (lane_id() == leader) base = atomicAdd((unsigned long long *)out_n, (unsigned long long)__popcll(m));
-            base = __shfl(base, leader, WAVE);
-            if (keep) out[base + lane_rank(m)] = k;
-        }
+        stage_push(sg, keep, k, out, (unsigned long long *)out_n, it + 1 == iters);
     }
 }
 
@@ -501,6 +552,12 @@ __global__ void __launch_bounds__(1024) sort_small_kernel(uint64_t *keys, const 
 
 template <typename T>
 __global__ void column_keys_kernel(sdp_column col, uint64_t *out, uint64_t *out_n) {
+    __shared__ uint64_t s_buf[STAGE];
+    __shared__ uint32_t s_cnt;
+    __shared__ uint64_t s_gbase;
+    if (threadIdx.x == 0) s_cnt = 0;
+    __syncthreads();
+    Stager sg{s_buf, &s_cnt, &s_gbase};
     const int64_t n = col.length;
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
     const int64_t iters = (n + stride - 1) / stride;
@@ -514,14 +571,7 @@ __global__ void column_keys_kernel(sdp_column col, uint64_t *out, uint64_t *out_
             keep = xd == xd;
             k = Elem<T>::key(x);
         }
-        const uint64_t m = __ballot(keep);
-        if (m) {
-            const int leader = __ffsll((long long)m) - 1;
-            unsigned long long base = 0;
-            if (lane_id() == leader) base = atomicAdd((unsigned long long *)out_n, (unsigned long long)__popcll(m));
-            base = __shfl(base, leader, WAVE);
-            if (keep) out[base + lane_rank(m)] = k;
-        }
+        stage_push(sg, keep, k, out, (unsigned long long *)out_n, it + 1 == iters);
     }
 }
 
@@ -531,7 +581,6 @@ __global__ void column_keys_kernel(sdp_column col, uint64_t *out, uint64_t *out_
 
 constexpr int P2_BLOCK = 256;
 constexpr int P2_UNROLL = 2;
-constexpr int P2_MAX_BALLOT_BINS = 256;   // lane-owned counters: 4 per lane
 
 struct P2Ctx {
     double mean, hi_t, lo_t, e0, inv_w;
@@ -559,12 +608,15 @@ __device__ __forceinline__ int case_bin(const P2Ctx &c, double x) {
     return -1;
 }
 
+constexpr int P2_SMALL_BINS = 16;
+
 struct P2Thread {
     double mad;
     uint32_t high, low, unbinned;
+    uint32_t bc[P2_SMALL_BINS];       // wave-uniform bin counts (SGPRs) for bins <= 16
 };
 
-template <typename T, bool BALLOT>
+template <typename T, bool SMALL>
 __device__ __forceinline__ void p2_elem(P2Thread &st, const P2Ctx &c, uint32_t *lds_hist, T x,
                                         bool valid) {
     const double xd = Elem<T>::d(x);
@@ -580,29 +632,17 @@ __device__ __forceinline__ void p2_elem(P2Thread &st, const P2Ctx &c, uint32_t *
         bin = case_bin(c, xd);
         st.unbinned += (bin < 0);
     }
-    if (BALLOT) {
-        // conflict-free counting: one ballot per bin, one single-lane LDS add
-        int jlo = 0, jhi = c.bins - 1;
-        if (c.bins > 32) {   // scan only the bins present in this wave
-            int bmin = bin < 0 ? 0x7fffffff : bin, bmax = bin;
+    if (SMALL) {
+        // one compare + ballot per bin; counts stay wave-uniform (scalar unit)
 #pragma unroll
-            for (int o = 32; o > 0; o >>= 1) {
-                bmin = min(bmin, __shfl_xor(bmin, o, WAVE));
-                bmax = max(bmax, __shfl_xor(bmax, o, WAVE));
-            }
-            jlo = bmin;
-            jhi = bmax;
-        }
-        for (int j = jlo; j <= jhi; ++j) {
-            const uint64_t m = __ballot(bin == j);
-            if (m && lane_id() == 0) atomicAdd(&lds_hist[j], (uint32_t)__popcll(m));
-        }
+        for (int j = 0; j < P2_SMALL_BINS; ++j)
+            if (j < c.bins) st.bc[j] += (uint32_t)__popcll(__ballot(bin == j));
     } else {
         if (bin >= 0) atomicAdd(&lds_hist[bin], 1u);
     }
 }
 
-template <typename T, bool BALLOT>
+template <typename T, bool SMALL>
 __global__ void __launch_bounds__(P2_BLOCK, 4) pass2_kernel(sdp_column col, double mean, const double *edges,
                                                          int bins, int monotone, double hi_t, double lo_t,
                                                          double *part_mad, uint64_t *part_cnt) {
@@ -622,6 +662,8 @@ __global__ void __launch_bounds__(P2_BLOCK, 4) pass2_kernel(sdp_column col, doub
     }
     P2Thread st;
     st.mad = 0.0; st.high = st.low = st.unbinned = 0;
+#pragma unroll
+    for (int j = 0; j < P2_SMALL_BINS; ++j) st.bc[j] = 0;
 
     const int64_t n = col.length;
     const int64_t nvec = n / VPT;
@@ -646,14 +688,14 @@ __global__ void __launch_bounds__(P2_BLOCK, 4) pass2_kernel(sdp_column col, doub
 #pragma unroll
         for (int u = 0; u < P2_UNROLL; ++u)
 #pragma unroll
-            for (int e = 0; e < VPT; ++e) p2_elem<T, BALLOT>(st, c, s_hist, v[u].v[e], (vb[u] >> e) & 1u);
+            for (int e = 0; e < VPT; ++e) p2_elem<T, SMALL>(st, c, s_hist, v[u].v[e], (vb[u] >> e) & 1u);
     }
     if (blockIdx.x == 0 && threadIdx.x < WAVE) {
         const int64_t i = nvec * VPT + threadIdx.x;
         const bool inb = i < n;
         T x = inb ? ((const T *)col.d_values)[i] : (T)0;
         const bool valid = inb && valid_bit(col.d_validity, col.validity_bit_offset, i);
-        p2_elem<T, BALLOT>(st, c, s_hist, x, valid);
+        p2_elem<T, SMALL>(st, c, s_hist, x, valid);
     }
     // ---- block reduction (fixed order) ----
     __shared__ double s_mad[P2_BLOCK / WAVE];
@@ -662,6 +704,11 @@ __global__ void __launch_bounds__(P2_BLOCK, 4) pass2_kernel(sdp_column col, doub
     const double mad = wave_sum_f64(st.mad);
     const uint64_t hi = wave_sum_u64(st.high), lo = wave_sum_u64(st.low), ub = wave_sum_u64(st.unbinned);
     if (lane == 0) { s_mad[wid] = mad; s_u[wid][0] = hi; s_u[wid][1] = lo; s_u[wid][2] = ub; }
+    if (SMALL && lane == 0) {
+#pragma unroll
+        for (int j = 0; j < P2_SMALL_BINS; ++j)
+            if (j < bins && st.bc[j]) atomicAdd(&s_hist[j], st.bc[j]);
+    }
     __syncthreads();
     const int stride = 3 + bins;
     if (threadIdx.x == 0) {
@@ -773,13 +820,19 @@ extern "C" int sdp_pass1(const sdp_column *col, const sdp_qplan *d_plan, void *d
     return check_launch("pass1_merge_kernel");
 }
 
-extern "C" int sdp_compact_candidates(const uint64_t *d_cand, const uint32_t *d_cand_counts, int32_t grid,
-                                      int64_t slot_capacity, uint64_t *d_out, uint64_t *d_out_count,
-                                      void *stream) {
-    if (grid < 1) return set_error(SDP_EINVAL, "sdp_compact_candidates: grid %d", grid);
-    hipLaunchKernelGGL(compact_cand_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream, d_cand, d_cand_counts,
-                       grid, slot_capacity, d_out, d_out_count);
-    return check_launch("compact_cand_kernel");
+extern "C" int sdp_compact_candidates(const uint64_t *d_cand, const uint32_t *d_cand_counts, int32_t nseg,
+                                      int64_t slot_capacity, uint64_t *d_offsets_work, uint64_t *d_out,
+                                      uint64_t *d_out_count, void *stream) {
+    if (nseg < 1 || d_offsets_work == nullptr) return set_error(SDP_EINVAL, "sdp_compact_candidates: nseg %d", nseg);
+    hipStream_t s = (hipStream_t)stream;
+    hipLaunchKernelGGL(scan_counts_kernel, dim3(1), dim3(1024), 0, s, d_cand_counts, nseg, d_offsets_work,
+                       d_out_count);
+    int rc = check_launch("scan_counts_kernel");
+    if (rc) return rc;
+    const int grid = nseg < 65536 ? nseg : 65536;
+    hipLaunchKernelGGL(copy_segments_kernel, dim3(grid), dim3(256), 0, s, d_cand, d_cand_counts, d_offsets_work,
+                       nseg, slot_capacity, d_out);
+    return check_launch("copy_segments_kernel");
 }
 
 extern "C" int sdp_radix_hist(const uint64_t *d_keys, const uint64_t *d_n, uint64_t prefix, int32_t shift,
@@ -826,7 +879,7 @@ extern "C" int sdp_pass2(const sdp_column *col, double mean, const double *d_edg
     uint64_t *pc = (uint64_t *)((char *)d_work + (int64_t)grid * sizeof(double));
     const size_t lds = (size_t)bins * (sizeof(double) + sizeof(uint32_t)) + 16;
     hipStream_t s = (hipStream_t)stream;
-    if (bins <= P2_MAX_BALLOT_BINS) {
+    if (bins <= P2_SMALL_BINS) {
         SDP_DISPATCH_NUMERIC(col->dtype,
             hipLaunchKernelGGL((pass2_kernel<T, true>), dim3(grid), dim3(P2_BLOCK), lds, s, *col, mean, d_edges,
                                bins, edges_monotone, hi_t, lo_t, pm, pc));

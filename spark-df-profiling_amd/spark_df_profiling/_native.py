@@ -20,6 +20,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get('SDP_LIBRARY', os.path.join(_HERE, 'lib', 'libsdp.so'))
 
 MAX_WINDOWS = 5
+PASS1_WAVES = 4          # SDP_PASS1_WAVES
 
 # enum sdp_dtype
 I8, I16, I32, I64, F32, F64, U8, U16, U32, U64, BOOL = 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11
@@ -41,6 +42,11 @@ class SdpBytesColumn(ctypes.Structure):
     _fields_ = [('d_data', ctypes.c_void_p), ('d_offsets', ctypes.c_void_p), ('d_validity', ctypes.c_void_p),
                 ('validity_bit_offset', ctypes.c_int64), ('length', ctypes.c_int64),
                 ('offset_width', ctypes.c_int32), ('fixed_width', ctypes.c_int32)]
+
+
+class SdpBuckets(ctypes.Structure):
+    _fields_ = [('d_key', ctypes.c_void_p), ('d_row', ctypes.c_void_p), ('d_cnt', ctypes.c_void_p),
+                ('d_fill', ctypes.c_void_p), ('capacity', ctypes.c_int64)]
 
 
 class SdpQPlan(ctypes.Structure):
@@ -73,6 +79,7 @@ _U64 = ctypes.c_uint64
 _D = ctypes.c_double
 _COL = ctypes.POINTER(SdpColumn)
 _BCOL = ctypes.POINTER(SdpBytesColumn)
+_BKT = ctypes.POINTER(SdpBuckets)
 
 # name -> (restype, argtypes); every status-returning entry is checked
 _SIGNATURES = {
@@ -84,7 +91,7 @@ _SIGNATURES = {
     'sdp_sample_keys': (ctypes.c_int, [_COL, _I32, _P, _P]),
     'sdp_quantile_plan': (ctypes.c_int, [_P, _I32, _P, _I32, _I32, _P, _P]),
     'sdp_pass1': (ctypes.c_int, [_COL, _P, _P, _I64, _P, _P, _I64, _P, _P]),
-    'sdp_compact_candidates': (ctypes.c_int, [_P, _P, _I32, _I64, _P, _P, _P]),
+    'sdp_compact_candidates': (ctypes.c_int, [_P, _P, _I32, _I64, _P, _P, _P, _P]),
     'sdp_radix_hist': (ctypes.c_int, [_P, _P, _U64, _I32, _P, _P]),
     'sdp_radix_filter': (ctypes.c_int, [_P, _P, _U64, _I32, _P, _P, _P]),
     'sdp_sort_small': (ctypes.c_int, [_P, _P, _P]),
@@ -101,6 +108,10 @@ _SIGNATURES = {
     'sdp_select_by_value': (ctypes.c_int, [_P, _P, _P, _U64, _U64, _P, _P, _P, _P]),
     'sdp_count_valid': (ctypes.c_int, [_P, _I64, _I64, _P, _P]),
     'sdp_first_valid': (ctypes.c_int, [_COL, _I32, _P, _P, _P]),
+    'sdp_group_part_rows_u64': (ctypes.c_int, [_COL, _I32, _I32, _BKT, _P, _P]),
+    'sdp_group_part_rows_bytes': (ctypes.c_int, [_BCOL, _I32, _BKT, _P, _P]),
+    'sdp_group_part_recs': (ctypes.c_int, [_BKT, _I32, _BKT, _I32, _I32, _BCOL, _I32, _P, _P]),
+    'sdp_group_dedup': (ctypes.c_int, [_BKT, _I64, _BCOL, _I32, _P, _P, _P]),
     'sdp_rowmask': (ctypes.c_int, [_COL, ctypes.POINTER(_I32), _I32, _P, _I64, _P, _P]),
     'sdp_gram_workspace_bytes': (_I64, [_I64, _I32]),
     'sdp_gram': (ctypes.c_int, [_COL, _I32, _P, _P, _P, _I64, _P, _P, _P, _P]),

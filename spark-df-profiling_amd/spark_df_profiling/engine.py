@@ -183,14 +183,16 @@ class Engine:
             tile_rows = 256 * 4 * (16 // nat.ELEM_SIZE[col.dtype])
             full = int(math.ceil(n / max(grid, 1) / tile_rows + 1)) * tile_rows
             cap = full if n <= (1 << 24) else min(cap, full)
-        cand = self._u64(max(nw, 1) * grid * max(cap, 1))
-        cand_counts = torch.zeros(max(nw, 1) * grid, dtype=torch.int32, device=self.device)
+        nseg = grid * nat.PASS1_WAVES                    # wave-private candidate segments per window
+        cap = -(-cap // nat.PASS1_WAVES) + 64 if cap else 0
+        cand = self._u64(max(nw, 1) * nseg * max(cap, 1))
+        cand_counts = torch.zeros(max(nw, 1) * nseg, dtype=torch.int32, device=self.device)
         res_dev = self._bytes(ctypes.sizeof(nat.SdpPass1Result))
         cs = col.sdp()
         sdp.sdp_pass1(ctypes.byref(cs), ptr(plan_dev), ptr(work), work.numel(), ptr(cand), ptr(cand_counts), cap,
                       ptr(res_dev), self._s())
         local = self._read(res_dev, nat.SdpPass1Result)
-        return local, {'cand': cand, 'counts': cand_counts, 'grid': grid, 'cap': cap}
+        return local, {'cand': cand, 'counts': cand_counts, 'nseg': nseg, 'cap': cap}
 
     def merge_pass1(self, local: nat.SdpPass1Result):
         """All-gather the per-rank pass-1 states and merge them in rank order."""
@@ -298,12 +300,12 @@ class Engine:
         return out, fallback is not None
 
     def _compact(self, cand_info, w):
-        grid, cap = cand_info['grid'], cand_info['cap']
-        out = self._u64(max(1, int(cand_info['counts'][w * grid:(w + 1) * grid].sum().item())))
+        nseg, cap = cand_info['nseg'], cand_info['cap']
+        out = self._u64(max(1, int(cand_info['counts'][w * nseg:(w + 1) * nseg].sum().item())))
         out_n = self._u64(1, zero=True)
-        base = cand_info['cand'][w * grid * cap:]
-        sdp.sdp_compact_candidates(ptr(base), ptr(cand_info['counts'][w * grid:]), grid, cap, ptr(out),
-                                   ptr(out_n), self._s())
+        base = cand_info['cand'][w * nseg * cap:]
+        sdp.sdp_compact_candidates(ptr(base), ptr(cand_info['counts'][w * nseg:]), nseg, cap,
+                                   ptr(self._u64(nseg)), ptr(out), ptr(out_n), self._s())
         return out, out_n
 
     def _all_keys(self, col):
@@ -380,8 +382,84 @@ class Engine:
         sdp.sdp_table_clear(ptr(slots), ptr(counts), capacity, int(bytes_keys), self._s())
         return slots, counts
 
+    # -- radix-partitioned grouping (sdp_group.hip) ------------------------------
+    def _alloc_buckets(self, nb, cap, isb, with_counts):
+        b = nat.SdpBuckets()
+        keep = {'key': self._u64(nb * cap)}
+        keep['row'] = self._u64(nb * cap) if isb else None
+        keep['cnt'] = self._u64(nb * cap) if with_counts else None
+        keep['fill'] = torch.zeros(nb, dtype=torch.int32, device=self.device)
+        b.d_key = keep['key'].data_ptr()
+        b.d_row = keep['row'].data_ptr() if isb else None
+        b.d_cnt = keep['cnt'].data_ptr() if with_counts else None
+        b.d_fill = keep['fill'].data_ptr()
+        b.capacity = cap
+        return b, keep
+
+    def group(self, col, with_counts, dense=True):
+        """Exact groups of a column by radix-partitioned LDS aggregation.
+        Returns a tab dict; `dense` adds compacted (key, count) group arrays.
+        Falls back to the global hash table if a bucket overflows."""
+        isb = col.kind == 'bytes'
+        with_counts = with_counts or isb
+        n = max(col.length, 1)
+        total_bits = max(0, math.ceil(math.log2(max(1.0, n / 2048.0))))
+        b1 = min(9, total_bits)
+        b2 = total_bits - b1
+        nb1 = 1 << b1
+        cap1 = -(-115 * n // (100 * nb1)) + 2 * (-(-n // 2048)) + 4096
+        stats = self._u64(68, zero=True)
+        s = self._s()
+        bk1, keep1 = self._alloc_buckets(nb1, cap1, isb, with_counts)
+        bc = col.sdp_bytes() if isb else None
+        if isb:
+            sdp.sdp_group_part_rows_bytes(ctypes.byref(bc), b1, ctypes.byref(bk1), ptr(stats), s)
+        else:
+            cs = col.sdp()
+            sdp.sdp_group_part_rows_u64(ctypes.byref(cs), b1, int(with_counts), ctypes.byref(bk1), ptr(stats), s)
+        final, keep, nfinal, capf = bk1, keep1, nb1, cap1
+        if b2 > 0:
+            mf = min(int(keep1['fill'].max().item()), cap1)
+            nb2 = 1 << b2
+            cap2 = -(-125 * mf // (100 * nb2)) + 2 * (-(-mf // 2048)) + 512
+            bk2, keep2 = self._alloc_buckets(nb1 * nb2, cap2, isb, with_counts)
+            sdp.sdp_group_part_recs(ctypes.byref(bk1), nb1, ctypes.byref(bk2), b1, b2,
+                                    ctypes.byref(bc) if isb else None, int(with_counts), ptr(stats), s)
+            del keep1, bk1
+            final, keep, nfinal, capf = bk2, keep2, nb1 * nb2, cap2
+        ngroups = torch.zeros(nfinal, dtype=torch.int32, device=self.device)
+        sdp.sdp_group_dedup(ctypes.byref(final), nfinal, ctypes.byref(bc) if isb else None, int(with_counts),
+                            ptr(ngroups), ptr(stats), s)
+        st = self._host_u64(stats)
+        if st[2] or st[3]:                          # overflow: exact global-table path
+            return None
+        groups_local = sum(st[4:68])
+        tab = {'bytes': isb, 'dense': True, 'rows': st[0], 'max_key_rows': st[1], 'col': col,
+               'groups': groups_local + (1 if st[1] else 0), 'groups_local': groups_local}
+        if dense:
+            keys = self._u64(max(groups_local, 1))
+            kn = self._u64(1, zero=True)
+            offs = self._u64(nfinal)
+            sdp.sdp_compact_candidates(ptr(keep['key']), ptr(ngroups), nfinal, capf, ptr(offs), ptr(keys), ptr(kn), s)
+            counts = None
+            if with_counts:
+                counts = self._u64(max(groups_local, 1))
+                cn = self._u64(1, zero=True)
+                sdp.sdp_compact_candidates(ptr(keep['cnt']), ptr(ngroups), nfinal, capf, ptr(offs), ptr(counts),
+                                           ptr(cn), s)
+            tab.update({'slots': keys, 'counts': counts, 'capacity': max(groups_local, 1)})
+        return tab
+
     def distinct_fixed(self, col, with_counts=False, capacity_hint=None):
         """countDistinct over a fixed-width column (describe.py:143)."""
+        if self.comm.world == 1:
+            tab = self.group(col, with_counts, dense=with_counts)
+            if tab is not None:
+                return tab
+        return self._distinct_fixed_table(col, with_counts, capacity_hint)
+
+    def _distinct_fixed_table(self, col, with_counts=False, capacity_hint=None):
+        """Global open-addressing table (fallback / multi-rank path)."""
         cap = _next_pow2(2 * max(capacity_hint if capacity_hint is not None else col.length, 1))
         slots, counts = self._table(cap, False, with_counts)
         stats = self._u64(4, zero=True)
@@ -396,6 +474,14 @@ class Engine:
         return tab
 
     def value_counts_bytes(self, col):
+        if self.comm.world == 1:
+            tab = self.group(col, True, dense=True)
+            if tab is not None:
+                return tab
+        return self.value_counts_bytes_table(col)
+
+    def value_counts_bytes_table(self, col):
+        """Global open-addressing byte-key table (fallback / multi-rank path)."""
         cap = _next_pow2(2 * max(col.length, 1))
         slots, counts = self._table(cap, True, True)
         stats = self._u64(4, zero=True)
@@ -413,6 +499,7 @@ class Engine:
         """Returns [(slot, count)] of the k first groups; bytes keys compared
         bytewise, fixed keys by their order-preserving u64 value."""
         slots, counts, cap, isb = tab['slots'], tab['counts'], tab['capacity'], tab['bytes']
+        flags = int(isb) | (2 if tab.get('dense') else 0)
         groups = tab['groups_local'] if 'groups_local' in tab else tab['groups']
         special = (not isb) and tab.get('max_key_rows', 0)
         bcol = tab['col'].sdp_bytes() if isb else None
@@ -422,7 +509,7 @@ class Engine:
         def select(cmin, cmax, limit):
             out = self._u64(max(limit, 1))
             on = self._u64(1, zero=True)
-            sdp.sdp_table_select(ptr(slots), ptr(counts), cap, int(isb), cmin, cmax, ptr(out), ptr(on), limit, s)
+            sdp.sdp_table_select(ptr(slots), ptr(counts), cap, flags, cmin, cmax, ptr(out), ptr(on), limit, s)
             return out, on
 
         def sort_take(sel, n_dev, take):
@@ -440,7 +527,7 @@ class Engine:
             res = sort_take(sel, n_dev, k)
             return _merge_special(res, extra, k, tab)
         hist = self._u64(64, zero=True)
-        sdp.sdp_table_count_log2_hist(ptr(slots), ptr(counts), cap, int(isb), ptr(hist), s)
+        sdp.sdp_table_count_log2_hist(ptr(slots), ptr(counts), cap, flags, ptr(hist), s)
         h = np.array(self._host_u64(hist), dtype=np.int64)
         cum = 0
         b = 63
@@ -461,7 +548,7 @@ class Engine:
         while True:
             step = max(1, -(-width // 2048))
             ch = self._u64(2048, zero=True)
-            sdp.sdp_table_count_hist(ptr(slots), ptr(counts), cap, int(isb), lo, step, ptr(ch), s)
+            sdp.sdp_table_count_hist(ptr(slots), ptr(counts), cap, flags, lo, step, ptr(ch), s)
             c = np.array(self._host_u64(ch), dtype=np.int64)
             nb = min(2048, -(-width // step))
             acc = 0

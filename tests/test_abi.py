@@ -1,0 +1,73 @@
+"""libsdp.so loads, exports every entry point include/sdp.h declares, and the
+ctypes mirrors have the C layout (CPU only: no kernel is launched)."""
+
+import ctypes
+import os
+import re
+import subprocess
+import tempfile
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, 'include', 'sdp.h')
+
+
+def declared_functions():
+    text = open(HEADER).read()
+    text = re.sub(r'/\*.*?\*/', '', text, flags=re.S)
+    return sorted(set(re.findall(r'\b(sdp_[a-z0-9_]+)\s*\(', text)))
+
+
+def test_header_declares_entry_points():
+    names = declared_functions()
+    for must in ('sdp_pass1', 'sdp_pass2', 'sdp_quantile_plan', 'sdp_hash_u64', 'sdp_hash_bytes',
+                 'sdp_group_part_rows_u64', 'sdp_group_dedup', 'sdp_gram', 'sdp_rowmask', 'sdp_first_valid',
+                 'sdp_last_error'):
+        assert must in names
+
+
+def test_library_exports_every_declared_symbol():
+    from spark_df_profiling import _native
+    lib = ctypes.CDLL(_native.LIB_PATH)
+    missing = [n for n in declared_functions() if not hasattr(lib, n)]
+    assert not missing, missing
+    # and the binding knows every one of them
+    assert set(declared_functions()) <= set(_native._SIGNATURES), \
+        set(declared_functions()) - set(_native._SIGNATURES)
+    assert _native.version().startswith('sdp-mi355x')
+
+
+def test_error_reporting_without_gpu():
+    """Argument validation fails before any device work, with a message."""
+    from spark_df_profiling import _native
+    with pytest.raises(_native.NativeError, match='n_sample'):
+        _native.sdp.sdp_quantile_plan(None, 0, None, 5, 1, None, None)
+    with pytest.raises(_native.NativeError, match='capacity'):
+        _native.sdp.sdp_table_clear(None, None, 1000, 0, None)
+
+
+STRUCTS = {'sdp_column': 'SdpColumn', 'sdp_bytes_column': 'SdpBytesColumn', 'sdp_qplan': 'SdpQPlan',
+           'sdp_pass1_result': 'SdpPass1Result', 'sdp_pass2_result': 'SdpPass2Result',
+           'sdp_buckets': 'SdpBuckets'}
+
+
+def test_struct_layouts_match_c():
+    from spark_df_profiling import _native
+    src = ['#include <stdio.h>', '#include <stddef.h>', '#include "%s"' % HEADER, 'int main(void){']
+    for c, py in STRUCTS.items():
+        src.append('printf("%s %%zu\\n", sizeof(%s));' % (c, c))
+        for f, _ in getattr(_native, py)._fields_:
+            src.append('printf("%s.%s %%zu\\n", offsetof(%s, %s));' % (c, f, c, f))
+    src.append('return 0;}')
+    with tempfile.TemporaryDirectory() as d:
+        cfile, exe = os.path.join(d, 'l.c'), os.path.join(d, 'l')
+        open(cfile, 'w').write('\n'.join(src))
+        subprocess.run(['gcc', '-o', exe, cfile], check=True)
+        out = subprocess.run([exe], check=True, capture_output=True, text=True).stdout.split('\n')
+    got = dict(line.split() for line in out if line)
+    for c, py in STRUCTS.items():
+        cls = getattr(_native, py)
+        assert int(got[c]) == ctypes.sizeof(cls), c
+        for f, _ in cls._fields_:
+            assert int(got['%s.%s' % (c, f)]) == getattr(cls, f).offset, (c, f)

@@ -1,0 +1,119 @@
+"""Host-side arithmetic of the engine vs the oracle (CPU only, no kernels)."""
+
+import math
+import random
+
+import numpy as np
+import pytest
+
+import oracle.spark_describe as osd
+from spark_df_profiling import engine as eng
+from spark_df_profiling import _native as nat
+from spark_df_profiling.utils import corr_from_gram, pretty_name
+
+
+def test_pretty_name():
+    assert [pretty_name(p) for p in (0.05, 0.25, 0.5, 0.75, 0.95)] == ['5%', '25%', '50%', '75%', '95%']
+    assert pretty_name(0.125) == '12.5%'
+
+
+@pytest.mark.parametrize('seed', range(20))
+def test_hist_edges_match_oracle(seed):
+    r = random.Random(seed)
+    lo = r.uniform(-1e6, 1e6)
+    hi = lo + abs(r.gauss(0, 10 ** r.randint(-3, 8)))
+    bins = r.choice([2, 3, 7, 10, 33, 100])
+    assert eng.hist_edges(lo, hi, bins) == osd.hist_edges(lo, hi, bins)
+
+
+def test_hist_edges_bins_one():
+    with pytest.raises(IndexError):
+        eng.hist_edges(0.0, 1.0, 1)
+
+
+@pytest.mark.parametrize('n', [1, 2, 3, 8, 9, 100, 9999, 10000, 10001, 123457])
+def test_percentile_approx_rank(n):
+    for p in (0.05, 0.25, 0.5, 0.75, 0.95, 1e-5, 0.99999):
+        assert eng.spark_percentile_approx_rank(n, p) == osd.spark_percentile_approx_rank(n, p)
+
+
+def _f64_key(x):
+    b = np.array([0.0 if x == 0 else x], dtype=np.float64).view(np.uint64)[0]
+    if x != x:
+        b = np.uint64(0x7FF8000000000000)
+    b = int(b)
+    return (~b & ((1 << 64) - 1)) if b >> 63 else b | (1 << 63)
+
+
+def test_key_roundtrip_and_order():
+    vals = [-np.inf, -1e300, -2.5, -1.0, -5e-324, 0.0, 5e-324, 1.0, 3.5, 1e300, np.inf]
+    keys = [_f64_key(v) for v in vals]
+    assert keys == sorted(keys)
+    assert _f64_key(float('nan')) > _f64_key(np.inf)
+    assert _f64_key(-0.0) == _f64_key(0.0)
+    for v, k in zip(vals, keys):
+        assert eng.key_to_float(k) == v
+    for i in (-2 ** 63, -1, 0, 1, 2 ** 63 - 1):
+        assert eng.key_to_int((i & ((1 << 64) - 1)) ^ (1 << 63)) == i
+
+
+def _p1_from(x, K, is_int):
+    """What pass 1 accumulates, restated exactly (Fractions) for a data chunk."""
+    from fractions import Fraction
+    r = nat.SdpPass1Result()
+    d = [Fraction(float(v)) - Fraction(K) for v in x]
+    s1 = sum(d, Fraction(0))
+    r.count = len(x)
+    r.n_valid = len(x)
+    r.shift = K
+    r.s1_hi = float(s1)
+    r.s1_lo = float(s1 - Fraction(r.s1_hi))
+    r.s2 = float(sum((t * t for t in d), Fraction(0)))
+    s3 = sum((t * t * t for t in d), Fraction(0))
+    r.s3_hi = float(s3)
+    r.s3_lo = float(s3 - Fraction(r.s3_hi))
+    r.s4 = float(sum((t ** 4 for t in d), Fraction(0)))
+    if is_int:
+        r.isum = int(np.sum(np.asarray(x, dtype=np.int64)))
+        r.imin, r.imax = int(min(x)), int(max(x))
+    else:
+        r.dmin, r.dmax = float(min(x)), float(max(x))
+    return r
+
+
+@pytest.mark.parametrize('kind', ['norm', 'shifted', 'lognormal', 'int'])
+def test_moments_from_power_sums_match_oracle(kind):
+    g = np.random.default_rng(3)
+    if kind == 'norm':
+        x = g.standard_normal(4000)
+    elif kind == 'shifted':
+        x = 1e9 + g.standard_normal(4000)
+    elif kind == 'lognormal':
+        x = g.lognormal(3, 2, 4000)
+    else:
+        x = g.integers(-10 ** 6, 10 ** 6, 4000)
+    is_int = kind == 'int'
+    K = float(np.median(x))
+    parts = [_p1_from(c, K, is_int) for c in np.array_split(x, 3)]
+    p1 = eng.merge_pass1_results(parts)
+    got = eng.moments(p1, is_int)
+    want = osd.numeric_stats(np.asarray(x), np.ones(len(x), bool), is_int, len(x), 10, 2)
+    for k in ('mean', 'variance', 'std', 'skewness', 'kurtosis', 'sum', 'min', 'max'):
+        assert math.isclose(got[k], want[k], rel_tol=1e-12, abs_tol=1e-12), (k, got[k], want[k])
+
+
+def test_int_sum_wraps():
+    parts = [_p1_from([2 ** 62, 2 ** 62], 0.0, True), _p1_from([2 ** 62, 5], 0.0, True)]
+    p1 = eng.merge_pass1_results(parts)
+    assert p1['isum'] == (3 * 2 ** 62 + 5) - 2 ** 64
+
+
+def test_corr_from_gram():
+    g = np.random.default_rng(1)
+    X = g.standard_normal((500, 4))
+    X[:, 1] += X[:, 0]
+    K = X.mean(0) + 0.3
+    Xc = X - K
+    rho = corr_from_gram(Xc.T @ Xc, Xc.sum(0), len(X))
+    assert np.allclose(rho, np.corrcoef(X.T), rtol=1e-12, atol=1e-12)
+    assert np.isnan(corr_from_gram(np.zeros((2, 2)), np.zeros(2), 0)).all()
