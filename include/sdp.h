@@ -180,15 +180,18 @@ int sdp_table_clear(uint64_t *d_slots, uint64_t *d_counts, int64_t capacity,
 
 /* countDistinct over a fixed-width column: NaN one value, -0.0 == 0.0, nulls
  * ignored.  with_counts != 0 also accumulates per-key row counts (CAT path).
+ * d_row_counts (nullable): row i stands for d_row_counts[i] rows (re-aggregating
+ * groups received from other ranks).
  * d_stats: [0] groups, [1] rows inserted, [2] rows with key UINT64_MAX. */
-int sdp_hash_u64(const sdp_column *col, uint64_t *d_slots, uint64_t *d_counts,
-                 int64_t capacity, int32_t with_counts, uint64_t *d_stats,
-                 void *stream);
+int sdp_hash_u64(const sdp_column *col, const uint64_t *d_row_counts, uint64_t *d_slots,
+                 uint64_t *d_counts, int64_t capacity, int32_t with_counts,
+                 uint64_t *d_stats, void *stream);
 
 /* Same for byte keys; slots hold (24-bit hash tag << 40 | row+1), equal keys
  * are confirmed by byte comparison. d_stats: [0] groups, [1] rows inserted. */
-int sdp_hash_bytes(const sdp_bytes_column *col, uint64_t *d_slots, uint64_t *d_counts,
-                   int64_t capacity, uint64_t *d_stats, void *stream);
+int sdp_hash_bytes(const sdp_bytes_column *col, const uint64_t *d_row_counts,
+                   uint64_t *d_slots, uint64_t *d_counts, int64_t capacity,
+                   uint64_t *d_stats, void *stream);
 
 /* Top-k groups by (count desc, key asc) from a table built with counts.
  * `bytes_keys` is a flag word: bit0 byte keys (EMPTY slot = 0), bit1 dense
@@ -201,7 +204,8 @@ int sdp_table_count_log2_hist(const uint64_t *d_slots, const uint64_t *d_counts,
 int sdp_table_count_hist(const uint64_t *d_slots, const uint64_t *d_counts,
                          int64_t capacity, int32_t bytes_keys, uint64_t lo,
                          uint64_t step, uint64_t *d_hist, void *stream);
-/* Slot indices with count >= min_count (and <= max_count), appended. */
+/* Slot indices with count >= min_count (and <= max_count), appended; with
+ * d_counts == NULL (distinct-only table) every group counts as 1. */
 int sdp_table_select(const uint64_t *d_slots, const uint64_t *d_counts, int64_t capacity,
                      int32_t bytes_keys, uint64_t min_count, uint64_t max_count,
                      uint64_t *d_out, uint64_t *d_out_n, uint64_t out_capacity,

@@ -168,10 +168,11 @@ __global__ void table_clear_kernel(uint64_t *slots, uint64_t *counts, int64_t ca
     }
 }
 
-__global__ void __launch_bounds__(H_BLOCK) hash_u64_kernel(sdp_column col, uint64_t *slots, uint64_t *counts,
+__global__ void __launch_bounds__(H_BLOCK) hash_u64_kernel(sdp_column col, const uint64_t *row_counts,
+                                                           uint64_t *slots, uint64_t *counts,
                                                            uint64_t mask, uint64_t *stats) {
     __shared__ uint64_t l_key[H_LSLOTS];
-    __shared__ uint32_t l_cnt[H_LSLOTS];
+    __shared__ uint64_t l_cnt[H_LSLOTS];
     __shared__ uint64_t s_red[H_BLOCK / WAVE][3];
     const int64_t n = col.length;
     const int64_t ntiles = (n + H_TILE - 1) / H_TILE;
@@ -185,13 +186,17 @@ __global__ void __launch_bounds__(H_BLOCK) hash_u64_kernel(sdp_column col, uint6
             if (i >= n) break;
             uint64_t key;
             if (!fetch_key(col, i, key)) continue;
-            ++n_rows;
-            if (key == EMPTY64) { ++n_max; continue; }
+            const uint64_t rc = row_counts ? row_counts[i] : 1ull;
+            n_rows += rc;
+            if (key == EMPTY64) { n_max += rc; continue; }
             uint32_t pos = (uint32_t)(mix64(key) & (H_LSLOTS - 1));
             while (true) {
                 const uint64_t old = atomicCAS((unsigned long long *)&l_key[pos], (unsigned long long)EMPTY64,
                                                (unsigned long long)key);
-                if (old == EMPTY64 || old == key) { atomicAdd(&l_cnt[pos], 1u); break; }
+                if (old == EMPTY64 || old == key) {
+                    atomicAdd((unsigned long long *)&l_cnt[pos], (unsigned long long)rc);
+                    break;
+                }
                 pos = (pos + 1) & (H_LSLOTS - 1);
             }
         }
@@ -213,11 +218,12 @@ __global__ void __launch_bounds__(H_BLOCK) hash_u64_kernel(sdp_column col, uint6
     }
 }
 
-__global__ void __launch_bounds__(H_BLOCK) hash_bytes_kernel(sdp_bytes_column col, uint64_t *slots,
-                                                             uint64_t *counts, uint64_t mask, uint64_t *stats) {
+__global__ void __launch_bounds__(H_BLOCK) hash_bytes_kernel(sdp_bytes_column col, const uint64_t *row_counts,
+                                                             uint64_t *slots, uint64_t *counts, uint64_t mask,
+                                                             uint64_t *stats) {
     __shared__ uint64_t l_slot[H_LSLOTS];     // (tag << 40) | (row + 1), 0 = empty
     __shared__ uint64_t l_hash[H_LSLOTS];
-    __shared__ uint32_t l_cnt[H_LSLOTS];
+    __shared__ uint64_t l_cnt[H_LSLOTS];
     __shared__ uint64_t s_red[H_BLOCK / WAVE][2];
     const int64_t n = col.length;
     const int64_t ntiles = (n + H_TILE - 1) / H_TILE;
@@ -230,7 +236,8 @@ __global__ void __launch_bounds__(H_BLOCK) hash_bytes_kernel(sdp_bytes_column co
             const int64_t row = base + k;
             if (row >= n) break;
             if (!valid_bit(col.d_validity, col.validity_bit_offset, row)) continue;
-            ++n_rows;
+            const uint64_t rc = row_counts ? row_counts[row] : 1ull;
+            n_rows += rc;
             const BytesRef me = bytes_at(col, row);
             const uint64_t h = hash_bytes(me);
             const uint64_t tag = h >> 40;
@@ -240,11 +247,15 @@ __global__ void __launch_bounds__(H_BLOCK) hash_bytes_kernel(sdp_bytes_column co
                 uint64_t cur = l_slot[pos];
                 if (cur == 0) {
                     const uint64_t old = atomicCAS((unsigned long long *)&l_slot[pos], 0ull, (unsigned long long)mine);
-                    if (old == 0) { l_hash[pos] = h; atomicAdd(&l_cnt[pos], 1u); break; }
+                    if (old == 0) {
+                        l_hash[pos] = h;
+                        atomicAdd((unsigned long long *)&l_cnt[pos], (unsigned long long)rc);
+                        break;
+                    }
                     cur = old;
                 }
                 if ((cur >> 40) == tag && bytes_equal(me, bytes_at(col, (int64_t)(cur & ROW_MASK) - 1))) {
-                    atomicAdd(&l_cnt[pos], 1u);
+                    atomicAdd((unsigned long long *)&l_cnt[pos], (unsigned long long)rc);
                     break;
                 }
                 pos = (pos + 1) & (H_LSLOTS - 1);
@@ -317,7 +328,7 @@ __global__ void table_select_kernel(const uint64_t *slots, const uint64_t *count
         const int64_t i = it * stride + (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
         bool keep = false;
         if (i < cap && occupied(slots, i, bytes_keys)) {
-            const uint64_t c = counts[i];
+            const uint64_t c = counts ? counts[i] : 1ull;   // distinct-only tables carry no counts
             keep = c >= cmin && c <= cmax;
         }
         const uint64_t m = __ballot(keep);
@@ -478,31 +489,35 @@ extern "C" int sdp_table_clear(uint64_t *d_slots, uint64_t *d_counts, int64_t ca
     return check_launch("table_clear_kernel");
 }
 
-extern "C" int sdp_hash_u64(const sdp_column *col, uint64_t *d_slots, uint64_t *d_counts, int64_t capacity,
-                            int32_t with_counts, uint64_t *d_stats, void *stream) {
+extern "C" int sdp_hash_u64(const sdp_column *col, const uint64_t *d_row_counts, uint64_t *d_slots,
+                            uint64_t *d_counts, int64_t capacity, int32_t with_counts, uint64_t *d_stats,
+                            void *stream) {
     if (col == nullptr || col->length < 0) return set_error(SDP_EINVAL, "sdp_hash_u64: column");
     if (!pow2(capacity)) return set_error(SDP_EINVAL, "sdp_hash_u64: capacity");
     if (col->dtype < SDP_I8 || col->dtype > SDP_BOOL) return set_error(SDP_EINVAL, "sdp_hash_u64: dtype %d", col->dtype);
     hipLaunchKernelGGL(hash_u64_kernel, dim3(grid_for(col->length, H_TILE, 2048)), dim3(H_BLOCK), 0,
-                       (hipStream_t)stream, *col, d_slots, with_counts ? d_counts : nullptr,
+                       (hipStream_t)stream, *col, d_row_counts, d_slots, with_counts ? d_counts : nullptr,
                        (uint64_t)(capacity - 1), d_stats);
     return check_launch("hash_u64_kernel");
 }
 
-extern "C" int sdp_hash_bytes(const sdp_bytes_column *col, uint64_t *d_slots, uint64_t *d_counts, int64_t capacity,
-                              uint64_t *d_stats, void *stream) {
+extern "C" int sdp_hash_bytes(const sdp_bytes_column *col, const uint64_t *d_row_counts, uint64_t *d_slots,
+                              uint64_t *d_counts, int64_t capacity, uint64_t *d_stats, void *stream) {
     if (col == nullptr || col->length < 0) return set_error(SDP_EINVAL, "sdp_hash_bytes: column");
     if (col->length >= (int64_t)ROW_MASK) return set_error(SDP_EINVAL, "sdp_hash_bytes: more than 2^40 rows");
     if (!pow2(capacity)) return set_error(SDP_EINVAL, "sdp_hash_bytes: capacity");
     if (col->fixed_width <= 0 && col->offset_width != 4 && col->offset_width != 8)
         return set_error(SDP_EINVAL, "sdp_hash_bytes: offset_width %d", col->offset_width);
     hipLaunchKernelGGL(hash_bytes_kernel, dim3(grid_for(col->length, H_TILE, 2048)), dim3(H_BLOCK), 0,
-                       (hipStream_t)stream, *col, d_slots, d_counts, (uint64_t)(capacity - 1), d_stats);
+                       (hipStream_t)stream, *col, d_row_counts, d_slots, d_counts, (uint64_t)(capacity - 1),
+                       d_stats);
     return check_launch("hash_bytes_kernel");
 }
 
 extern "C" int sdp_table_count_log2_hist(const uint64_t *d_slots, const uint64_t *d_counts, int64_t capacity,
                                          int32_t bytes_keys, uint64_t *d_hist, void *stream) {
+    if (d_slots == nullptr || d_counts == nullptr || d_hist == nullptr)
+        return set_error(SDP_EINVAL, "sdp_table_count_log2_hist: null pointer");
     hipLaunchKernelGGL(count_log2_hist_kernel, dim3(grid_for(capacity, 256 * 16, 2048)), dim3(256), 0,
                        (hipStream_t)stream, d_slots, d_counts, capacity, bytes_keys, d_hist);
     return check_launch("count_log2_hist_kernel");
@@ -511,6 +526,8 @@ extern "C" int sdp_table_count_log2_hist(const uint64_t *d_slots, const uint64_t
 extern "C" int sdp_table_count_hist(const uint64_t *d_slots, const uint64_t *d_counts, int64_t capacity,
                                     int32_t bytes_keys, uint64_t lo, uint64_t step, uint64_t *d_hist, void *stream) {
     if (step == 0) return set_error(SDP_EINVAL, "sdp_table_count_hist: step 0");
+    if (d_slots == nullptr || d_counts == nullptr || d_hist == nullptr)
+        return set_error(SDP_EINVAL, "sdp_table_count_hist: null pointer");
     hipLaunchKernelGGL(count_hist_kernel, dim3(grid_for(capacity, 256 * 16, 2048)), dim3(256), 0,
                        (hipStream_t)stream, d_slots, d_counts, capacity, bytes_keys, lo, step, d_hist);
     return check_launch("count_hist_kernel");
@@ -519,6 +536,8 @@ extern "C" int sdp_table_count_hist(const uint64_t *d_slots, const uint64_t *d_c
 extern "C" int sdp_table_select(const uint64_t *d_slots, const uint64_t *d_counts, int64_t capacity,
                                 int32_t bytes_keys, uint64_t min_count, uint64_t max_count, uint64_t *d_out,
                                 uint64_t *d_out_n, uint64_t out_capacity, void *stream) {
+    if (d_slots == nullptr || d_out == nullptr || d_out_n == nullptr)
+        return set_error(SDP_EINVAL, "sdp_table_select: null pointer");
     hipLaunchKernelGGL(table_select_kernel, dim3(grid_for(capacity, 256 * 16, 2048)), dim3(256), 0,
                        (hipStream_t)stream, d_slots, d_counts, capacity, bytes_keys, min_count, max_count, d_out,
                        d_out_n, out_capacity);
@@ -527,6 +546,8 @@ extern "C" int sdp_table_select(const uint64_t *d_slots, const uint64_t *d_count
 
 extern "C" int sdp_sort_groups(uint64_t *d_sel, const uint64_t *d_n, const uint64_t *d_slots,
                                const uint64_t *d_counts, const sdp_bytes_column *bytes_col, void *stream) {
+    if (d_sel == nullptr || d_n == nullptr || d_slots == nullptr || d_counts == nullptr)
+        return set_error(SDP_EINVAL, "sdp_sort_groups: null pointer");
     sdp_bytes_column bc;
     memset(&bc, 0, sizeof(bc));
     if (bytes_col) bc = *bytes_col;

@@ -98,8 +98,8 @@ _SIGNATURES = {
     'sdp_column_keys': (ctypes.c_int, [_COL, _P, _P, _P]),
     'sdp_pass2': (ctypes.c_int, [_COL, _D, _P, _I32, _I32, _D, _D, _P, _I64, _P, _P, _P]),
     'sdp_table_clear': (ctypes.c_int, [_P, _P, _I64, _I32, _P]),
-    'sdp_hash_u64': (ctypes.c_int, [_COL, _P, _P, _I64, _I32, _P, _P]),
-    'sdp_hash_bytes': (ctypes.c_int, [_BCOL, _P, _P, _I64, _P, _P]),
+    'sdp_hash_u64': (ctypes.c_int, [_COL, _P, _P, _P, _I64, _I32, _P, _P]),
+    'sdp_hash_bytes': (ctypes.c_int, [_BCOL, _P, _P, _P, _I64, _P, _P]),
     'sdp_table_count_log2_hist': (ctypes.c_int, [_P, _P, _I64, _I32, _P, _P]),
     'sdp_table_count_hist': (ctypes.c_int, [_P, _P, _I64, _I32, _U64, _U64, _P, _P]),
     'sdp_table_select': (ctypes.c_int, [_P, _P, _I64, _I32, _U64, _U64, _P, _P, _U64, _P]),

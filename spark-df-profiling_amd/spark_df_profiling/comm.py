@@ -39,6 +39,9 @@ class LocalComm:
         assert len(send_counts) == 1
         return send
 
+    def allgather_object(self, obj):
+        return [obj]
+
     def barrier(self):
         pass
 
@@ -98,6 +101,11 @@ class TorchComm:
         out = torch.empty(sum(rc), dtype=send.dtype, device=dev)
         self.dist.all_to_all_single(out, send, output_split_sizes=rc, input_split_sizes=list(send_counts),
                                     group=self.group)
+        return out
+
+    def allgather_object(self, obj):
+        out = [None] * self.world
+        self.dist.all_gather_object(out, obj, group=self.group)
         return out
 
     def barrier(self):

@@ -193,10 +193,10 @@ def _date_series(engine, col, p1, distinct, freq):
 def _categorical_series(engine, col, tab, count, bundle):
     """describe_categorical_1d (describe.py:250-271).  Groups ordered by count
     desc then key asc (the reference's orderBy leaves ties unspecified)."""
-    top = engine.topk(tab, TOPK)
-    values = engine.group_values(tab, [s for s, _ in top], col)
-    counts = [int(c) for _, c in top]
-    bundle['topk'] = list(zip(values, counts))
+    pairs = engine.global_topk(tab, col, TOPK)
+    values = [v for v, _ in pairs]
+    counts = [int(c) for _, c in pairs]
+    bundle['topk'] = pairs
     groups = tab['groups']
     s = OrderedDict()
     s['top'] = values[0]

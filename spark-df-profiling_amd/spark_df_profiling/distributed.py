@@ -1,13 +1,171 @@
-"""Multi-GPU exchanges for distinct counts and value counts.
+"""Row-sharded grouping across ranks.
 
-Placeholder until the hash-partitioned all-to-all lands: the row-sharded path
-currently supports world == 1 for grouping statistics.
+Each rank aggregates its own rows on its GPU (libsdp hash tables), then the
+groups are repartitioned by key hash so that every key has exactly one owner
+rank (all-to-all), and the owner re-aggregates what it received:
+
+* distinct count  = sum over owners of their group counts (all-reduce);
+* value counts    = each owner's top-k by (count desc, key asc), all-gathered
+                    and merged on every rank in the same order;
+* first rows      = every rank's first k na.drop rows, concatenated in rank order
+                    (rank r holds the r-th contiguous row range).
+
+The exchange itself is data movement (gather by owner, all_to_all_single);
+aggregation runs in the same HIP kernels as the single-GPU path.
 """
+
+from __future__ import annotations
+
+import ctypes
+
+import numpy as np
+import torch
+
+from . import _native as nat
+from ._native import sdp, ptr
+
+MASK40 = (1 << 40) - 1
+
+
+def _owner_u64(keys: torch.Tensor, world: int) -> torch.Tensor:
+    """Owner rank of each u64 key (stored as int64): a multiplicative hash."""
+    h = keys * -7046029254386353131            # 0x9E3779B97F4A7C15 as int64; wraps
+    return ((h >> 40) & 0xFFFFFF) % world
+
+
+def _table_groups(engine, tab):
+    """Dense (keys, counts) of a local table (all occupied slots)."""
+    slots, counts, cap = tab['slots'], tab['counts'], tab['capacity']
+    flags = int(tab['bytes']) | (2 if tab.get('dense') else 0)
+    n_local = tab['groups_local'] if 'groups_local' in tab else tab['groups']
+    sel = engine._u64(max(n_local, 1))
+    nsel = engine._u64(1, zero=True)
+    sdp.sdp_table_select(ptr(slots), ptr(counts), cap, flags, 1 if counts is not None else 0,
+                         (1 << 64) - 1, ptr(sel), ptr(nsel), max(n_local, 1), engine._s())
+    m = int(nsel.item())
+    sel = sel[:m]
+    keys = slots[sel]
+    cnt = counts[sel] if counts is not None else None
+    return keys, cnt
 
 
 def exchange_fixed_groups(engine, tab, with_counts):
-    raise NotImplementedError('multi-rank distinct counts: not built yet')
+    comm = engine.comm
+    world = comm.world
+    keys, cnt = _table_groups(engine, tab)
+    owner = _owner_u64(keys, world)
+    order = torch.argsort(owner, stable=True)
+    keys = keys[order]
+    send = torch.bincount(owner, minlength=world).tolist()
+    rkeys = comm.alltoallv(keys.contiguous(), send)
+    rcnt = None
+    if with_counts:
+        rcnt = comm.alltoallv(cnt[order].contiguous(), send)
+    # owner table over the received keys (they are already order-preserving
+    # u64 keys: a U64 column hashes them unchanged)
+    from .columns import DeviceColumn
+    col = DeviceColumn('_exchange', 'bigint', int(rkeys.numel()), 'fixed', nat.U64)
+    col.values = rkeys if rkeys.numel() else torch.zeros(2, dtype=torch.int64, device=engine.device)
+    local = engine._distinct_fixed_table(col, with_counts=with_counts, row_counts=rcnt, exchanged=True)
+    side = torch.tensor([tab['max_key_rows'], tab['rows'], local['groups'] - (1 if local['max_key_rows'] else 0)],
+                        dtype=torch.int64, device=engine.device)
+    tot = comm.allreduce_sum(side).tolist()
+    max_rows, rows, owner_groups = int(tot[0]), int(tot[1]), int(tot[2])
+    local['groups_local'] = local['groups'] - (1 if local['max_key_rows'] else 0)
+    local['max_key_rows'] = max_rows if comm.rank == 0 else 0
+    local['groups'] = owner_groups + (1 if max_rows else 0)
+    local['rows'] = rows
+    local['sharded'] = True
+    return local
 
 
 def exchange_bytes_groups(engine, tab):
-    raise NotImplementedError('multi-rank value counts: not built yet')
+    comm = engine.comm
+    world = comm.world
+    col = tab['col']
+    slots, cnt = _table_groups(engine, tab)
+    rows = (slots & MASK40) - 1
+    owner = ((slots >> 40) & 0xFFFFFF) % world
+    order = torch.argsort(owner, stable=True)
+    rows, cnt, owner = rows[order], cnt[order], owner[order]
+    send = torch.bincount(owner, minlength=world).tolist()
+    if col.fixed_width:
+        starts = rows * col.fixed_width
+        lens = torch.full_like(rows, col.fixed_width)
+    else:
+        o = col.offsets.to(torch.int64)
+        starts = o[rows]
+        lens = o[rows + 1] - starts
+    # byte gather: index of every byte of every group key, owner-major
+    tot = int(lens.sum().item())
+    if tot:
+        first = torch.repeat_interleave(starts - torch.cumsum(lens, 0) + lens, lens)
+        idx = first + torch.arange(tot, device=engine.device)
+        payload = col.data[idx]
+    else:
+        payload = torch.zeros(0, dtype=torch.uint8, device=engine.device)
+    byte_send = []
+    csum = 0
+    lens_list = lens.tolist() if lens.numel() else []
+    pos = 0
+    for r in range(world):
+        b = sum(lens_list[pos:pos + send[r]])
+        byte_send.append(b)
+        pos += send[r]
+        csum += b
+    rlens = comm.alltoallv(lens.contiguous(), send)
+    rcnt = comm.alltoallv(cnt.contiguous(), send)
+    rbytes = comm.alltoallv(payload.contiguous(), byte_send)
+    from .columns import DeviceColumn
+    n = int(rlens.numel())
+    rc = DeviceColumn('_exchange', col.spark_type, n, 'bytes', decimal_scale=col.decimal_scale)
+    offs = torch.zeros(n + 1, dtype=torch.int64, device=engine.device)
+    if n:
+        torch.cumsum(rlens, 0, out=offs[1:])
+    rc.offsets = offs
+    rc.offset_width = 8
+    data = torch.zeros(int(rbytes.numel()) + 16, dtype=torch.uint8, device=engine.device)
+    data[:rbytes.numel()] = rbytes
+    rc.data = data
+    local = engine.value_counts_bytes_table(rc, row_counts=rcnt, exchanged=True)
+    local['src_col'] = rc
+    local['col'] = rc
+    side = torch.tensor([tab['rows'], local['groups']], dtype=torch.int64, device=engine.device)
+    t = comm.allreduce_sum(side).tolist()
+    local['groups_local'] = local['groups']
+    local['groups'] = int(t[1])
+    local['rows'] = int(t[0])
+    local['sharded'] = True
+    return local
+
+
+def merge_topk(comm, pairs, k):
+    """Global top-k from every rank's local top-k list of (value, count)."""
+    if comm.world == 1:
+        return pairs[:k]
+    allp = comm.allgather_object(pairs)
+    merged = [p for part in allp for p in part]
+    merged.sort(key=lambda vc: (-vc[1], _sortable(vc[0])))
+    return merged[:k]
+
+
+def _sortable(v):
+    if isinstance(v, (bytes, bytearray)):
+        return bytes(v)
+    if isinstance(v, (np.integer,)):
+        return int(v)
+    if isinstance(v, (np.floating,)):
+        return float(v)
+    return v
+
+
+def merge_first_rows(comm, values, k):
+    if comm.world == 1:
+        return values[:k]
+    allv = comm.allgather_object(values)
+    out = []
+    for part in allv:
+        out.extend(part)
+        if len(out) >= k:
+            break
+    return out[:k]

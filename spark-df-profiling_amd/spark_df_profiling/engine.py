@@ -451,46 +451,54 @@ class Engine:
         return tab
 
     def distinct_fixed(self, col, with_counts=False, capacity_hint=None):
-        """countDistinct over a fixed-width column (describe.py:143)."""
-        if self.comm.world == 1:
+        """countDistinct over a fixed-width column (describe.py:143).
+
+        Path choice (measured on MI355X at 1e9 rows, tools/bench_group.py):
+        the radix-partitioned LDS grouping wins for near-unique keys (50 vs 80
+        ms); a global table sized by a small key range (<= rows / 4) stays
+        cache-resident and wins there (23 vs 44 ms)."""
+        small_range = capacity_hint is not None and capacity_hint * 4 <= max(col.length, 1)
+        if self.comm.world == 1 and not small_range and col.length >= (1 << 16):
             tab = self.group(col, with_counts, dense=with_counts)
             if tab is not None:
                 return tab
         return self._distinct_fixed_table(col, with_counts, capacity_hint)
 
-    def _distinct_fixed_table(self, col, with_counts=False, capacity_hint=None):
-        """Global open-addressing table (fallback / multi-rank path)."""
-        cap = _next_pow2(2 * max(capacity_hint if capacity_hint is not None else col.length, 1))
+    def _distinct_fixed_table(self, col, with_counts=False, capacity_hint=None, row_counts=None, exchanged=False):
+        """Global open-addressing table (fallback / small key ranges / multi-rank)."""
+        bound = col.length if capacity_hint is None else min(capacity_hint, col.length)
+        cap = _next_pow2(2 * max(bound, 1))
         slots, counts = self._table(cap, False, with_counts)
         stats = self._u64(4, zero=True)
         cs = col.sdp()
-        sdp.sdp_hash_u64(ctypes.byref(cs), ptr(slots), ptr(counts), cap, int(with_counts), ptr(stats), self._s())
+        sdp.sdp_hash_u64(ctypes.byref(cs), ptr(row_counts), ptr(slots), ptr(counts), cap, int(with_counts),
+                         ptr(stats), self._s())
         st = self._host_u64(stats)
         groups = st[0] + (1 if st[2] else 0)
         tab = {'slots': slots, 'counts': counts, 'capacity': cap, 'bytes': False, 'max_key_rows': st[2],
-               'rows': st[1], 'groups': groups}
-        if self.comm.world > 1:
+               'rows': st[1], 'groups': groups, 'groups_local': st[0], 'col': col}
+        if self.comm.world > 1 and not exchanged:
             tab = self._exchange_fixed(tab, with_counts)
         return tab
 
     def value_counts_bytes(self, col):
-        if self.comm.world == 1:
+        if self.comm.world == 1 and col.length >= (1 << 16):
             tab = self.group(col, True, dense=True)
             if tab is not None:
                 return tab
         return self.value_counts_bytes_table(col)
 
-    def value_counts_bytes_table(self, col):
+    def value_counts_bytes_table(self, col, row_counts=None, exchanged=False):
         """Global open-addressing byte-key table (fallback / multi-rank path)."""
         cap = _next_pow2(2 * max(col.length, 1))
         slots, counts = self._table(cap, True, True)
         stats = self._u64(4, zero=True)
         bc = col.sdp_bytes()
-        sdp.sdp_hash_bytes(ctypes.byref(bc), ptr(slots), ptr(counts), cap, ptr(stats), self._s())
+        sdp.sdp_hash_bytes(ctypes.byref(bc), ptr(row_counts), ptr(slots), ptr(counts), cap, ptr(stats), self._s())
         st = self._host_u64(stats)
         tab = {'slots': slots, 'counts': counts, 'capacity': cap, 'bytes': True, 'rows': st[1], 'groups': st[0],
-               'col': col}
-        if self.comm.world > 1:
+               'groups_local': st[0], 'col': col}
+        if self.comm.world > 1 and not exchanged:
             tab = self._exchange_bytes(tab)
         return tab
 
@@ -614,6 +622,15 @@ class Engine:
             sel, n_dev, n = eq, en, ne
             offset += 8
 
+    def global_topk(self, tab, col, k=TOPK):
+        """[(value, count)] of the first k groups by (count desc, key asc) over
+        every rank (each rank owns a hash partition of the groups)."""
+        top = self.topk(tab, k)
+        values = self.group_values(tab, [sl for sl, _ in top], col)
+        pairs = [(v, int(c)) for v, (_, c) in zip(values, top)]
+        from .distributed import merge_topk
+        return merge_topk(self.comm, pairs, k)
+
     def group_values(self, tab, slot_list, col: DeviceColumn):
         """Host values of the groups at `slot_list` (None = the EMPTY64 key)."""
         if not tab['bytes']:
@@ -634,7 +651,8 @@ class Engine:
     def first_rows(self, col: DeviceColumn, k):
         """Values of the first k rows that survive na.drop, in row order."""
         if col.kind == 'null' or col.length == 0:
-            return []
+            from .distributed import merge_first_rows
+            return merge_first_rows(self.comm, [], k)
         c = nat.SdpColumn()
         c.d_values = None
         c.d_validity = col.validity.data_ptr() if col.validity is not None else None
@@ -649,8 +667,11 @@ class Engine:
         f = int(found.item())
         rows = [int(x) for x in idx[:f].cpu().tolist()]
         if col.kind == 'bytes':
-            return self.row_bytes_values(col, rows, col)
-        return self.fixed_row_values(col, rows)
+            vals = self.row_bytes_values(col, rows, col)
+        else:
+            vals = self.fixed_row_values(col, rows)
+        from .distributed import merge_first_rows
+        return merge_first_rows(self.comm, vals, k)
 
     def fixed_row_values(self, col, rows):
         if not rows:

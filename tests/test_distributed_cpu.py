@@ -1,0 +1,89 @@
+"""world_size-2 gloo tests of the rank-merge logic (CPU only, no kernels)."""
+
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(('127.0.0.1', 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, q):
+    os.environ['MASTER_ADDR'] = '127.0.0.1'
+    os.environ['MASTER_PORT'] = str(port)
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+    try:
+        from spark_df_profiling.comm import TorchComm
+        from spark_df_profiling.distributed import merge_topk, merge_first_rows, _owner_u64
+        from spark_df_profiling import engine as eng
+        from spark_df_profiling import _native as nat
+        comm = TorchComm()
+        out = {}
+        # allgather / allgatherv / allreduce
+        t = torch.tensor([rank + 1.0, 10.0 * rank], dtype=torch.float64)
+        out['allgather'] = [x.tolist() for x in comm.allgather(t)]
+        v = torch.arange(rank + 2, dtype=torch.int64)
+        out['allgatherv'] = [x.tolist() for x in comm.allgatherv(v)]
+        out['allreduce'] = comm.allreduce_sum(torch.tensor([rank + 1], dtype=torch.int64)).tolist()
+        # alltoallv (gloo emulation): rank r sends (r*10 + d) repeated d+1 times to rank d
+        send = torch.cat([torch.full((d + 1,), rank * 10 + d, dtype=torch.int64) for d in range(world)])
+        out['alltoallv'] = comm.alltoallv(send, [d + 1 for d in range(world)]).tolist()
+        # top-k merge: (count desc, key asc), deterministic on every rank
+        local = [('b%d' % rank, 5), ('a', 3 + rank), ('z%d' % rank, 1)]
+        out['topk'] = merge_topk(comm, local, 4)
+        out['first'] = merge_first_rows(comm, ['r%d_%d' % (rank, i) for i in range(3)], 4)
+        # pass-1 states merged in rank order on every rank
+        e = eng.Engine(device='cpu', comm=comm)
+        p = nat.SdpPass1Result()
+        p.count = 10 + rank
+        p.n_valid = 11 + rank
+        p.isum = 2 ** 62
+        p.imin, p.imax = -rank, rank
+        p.dmin, p.dmax = float(-rank), float(rank)
+        p.s1_hi, p.s2 = 1.0 + rank, 2.0
+        p.w_gt[0] = rank
+        m = e.merge_pass1(p)
+        out['p1'] = (m['count'], m['n_valid'], m['isum'], m['imin'], m['imax'], m['s1'], m['w_gt'][0])
+        out['owner'] = _owner_u64(torch.arange(1000, dtype=torch.int64), world).bincount(minlength=world).tolist()
+        q.put((rank, out))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_two_rank_merges():
+    world = 2
+    port = _free_port()
+    ctx = mp.get_context('spawn')
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=120) for _ in range(world))
+    for p in procs:
+        p.join(60)
+        assert p.exitcode == 0
+    for r in range(world):
+        o = res[r]
+        assert o['allgather'] == [[1.0, 0.0], [2.0, 10.0]]
+        assert o['allgatherv'] == [[0, 1], [0, 1, 2]]
+        assert o['allreduce'] == [3]
+        want = []
+        for src in range(world):
+            want += [src * 10 + r] * (r + 1)
+        assert o['alltoallv'] == want
+        assert o['topk'] == [('b0', 5), ('b1', 5), ('a', 4), ('a', 3)]
+        assert o['first'] == ['r0_0', 'r0_1', 'r0_2', 'r1_0']
+        assert o['p1'] == (21, 23, 2 ** 63 - 2 ** 64, -1, 1, 3.0, 1)
+        assert sum(o['owner']) == 1000 and min(o['owner']) > 350
+    same = {k: v for k, v in res[0].items() if k != 'alltoallv'}
+    assert same == {k: v for k, v in res[1].items() if k != 'alltoallv'}

@@ -1,0 +1,71 @@
+"""Row-sharded describe() on N ranks vs the oracle on the whole table.
+
+Run with one GPU per rank over RCCL, or several ranks sharing one GPU over gloo:
+    python -m torch.distributed.run --nproc-per-node 2 --master-addr 127.0.0.1 \\
+        --master-port 29511 tools/multirank_check.py [nccl|gloo]
+"""
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+for p in (ROOT, os.path.join(ROOT, 'spark-df-profiling_amd'), os.path.join(ROOT, 'tests')):
+    sys.path.insert(0, p)
+
+import pyarrow as pa
+import torch
+import torch.distributed as dist
+
+import datagen
+from compare import assert_describe_equal
+
+
+def main():
+    backend = sys.argv[1] if len(sys.argv) > 1 else 'gloo'
+    rank = int(os.environ['RANK'])
+    world = int(os.environ['WORLD_SIZE'])
+    local = int(os.environ.get('LOCAL_RANK', '0'))
+    ngpu = torch.cuda.device_count()
+    dev = torch.device('cuda', local % ngpu)
+    torch.cuda.set_device(dev)
+    if backend == 'nccl':
+        dist.init_process_group('nccl', device_id=dev)
+    else:
+        dist.init_process_group('gloo')
+    from spark_df_profiling import describe
+    from spark_df_profiling.columns import DeviceTable
+    from spark_df_profiling.comm import TorchComm
+    comm = TorchComm()
+    tables = {
+        'demo': datagen.demo_like_table(60_000),
+        'numeric': datagen.numeric_table(40_000),
+        'categorical': datagen.categorical_table(30_000),
+        'dates': datagen.date_table(20_000),
+        'corr': datagen.corr_table(20_000),
+        'legacy': datagen.legacy_table(),
+    }
+    failures = 0
+    for name, t in tables.items():
+        full = DeviceTable.from_arrow(t, dev)
+        n = t.num_rows
+        per = (n // world) // 16 * 16
+        start = rank * per
+        stop = n if rank == world - 1 else start + per
+        shard = full.slice_rows(start, stop)
+        got = describe(shard, comm=comm, plots=False)
+        if rank == 0:
+            import oracle
+            want = oracle.describe(t)
+            try:
+                assert_describe_equal(got, want)
+                print('[%s] OK world=%d' % (name, world), flush=True)
+            except AssertionError as e:
+                failures += 1
+                print('[%s] MISMATCH world=%d\n%s' % (name, world, e), flush=True)
+    dist.barrier()
+    dist.destroy_process_group()
+    if rank == 0 and failures:
+        sys.exit(1)
+
+
+if __name__ == '__main__':
+    main()
