@@ -229,36 +229,75 @@ int sdp_select_by_value(const uint64_t *d_sel, const uint64_t *d_vals, const uin
 int sdp_count_valid(const uint8_t *d_validity, int64_t bit_offset, int64_t length,
                     uint64_t *d_out, void *stream);
 
-/* ---- radix-partitioned grouping (sdp_group.hip) ----------------------------
- * Exact distinct / value counts without a global hash table: rows are
- * de-duplicated per tile in LDS and appended to 2^b1 hash buckets, the buckets
- * re-partitioned by the next b2 hash bits (again de-duplicated in LDS), and
- * every final bucket de-duplicated by one workgroup in LDS.  Records are
- * structure-of-arrays; byte keys carry their 64-bit hash in d_key and a
- * representative row in d_row, and are compared byte for byte.
- * d_stats (68 x u64, zeroed by the caller): [0] rows, [1] rows whose u64 key is
- * UINT64_MAX (kept outside the buckets), [2] bucket overflow, [3] LDS table
- * full, [4..67] group count spread over 64 counters. */
-typedef struct sdp_buckets {
-    uint64_t *d_key;        /* [nbuckets][capacity]                         */
-    uint64_t *d_row;        /* byte keys only                               */
-    uint64_t *d_cnt;        /* per-record row counts (NULL: distinct only)  */
-    uint32_t *d_fill;       /* [nbuckets] records appended (zeroed)         */
-    int64_t   capacity;
-} sdp_buckets;
+/* ---- two-level hash partitioning with exact offsets (sdp_part.hip) ---------
+ * Replaces countDistinct (describe.py:143) and groupBy(c).count()
+ * (describe.py:251).  Records are structure-of-arrays: fixed-width keys are one
+ * u64 h = mix64(key) in d_k0; byte keys are (k0, k1) = first 16 bytes, zero
+ * padded, and meta = len << 40 | row + 1 (strings > 16 bytes: k0 = 64-bit hash,
+ * compared byte for byte against the column).
+ * Flow: sdp_part_rows phase 0 (per-block histogram of the top b1 hash bits,
+ * H1[bucket][block]) -> sdp_scan_u32 -> phase 1 (scatter at exact offsets) ->
+ * sdp_part_recs phase 0/1 per chunk with the next b2 bits -> sdp_scan_u32 ->
+ * sdp_part_dedup (one workgroup per final bucket, LDS table).
+ * d_stats (68 x u64, zeroed): [0] valid rows, [1] fixed-key records whose
+ * h == UINT64_MAX (kept outside the tables), [2] 64-bit hash collision between
+ * different byte strings, [3] LDS table full, [4..67] groups (64 counters). */
+#define SDP_PART_MAX_GRID 1024
+typedef struct sdp_records {
+    uint64_t *d_k0;
+    uint64_t *d_k1;     /* byte keys only */
+    uint64_t *d_meta;   /* byte keys only */
+} sdp_records;
+/* Keys counted outside the partitions (n <= 256): hashes, and for byte keys
+ * the (k0, k1, meta) of one representative row; counts go to d_heavy_counts. */
+typedef struct sdp_heavy {
+    const uint64_t *d_h;
+    const uint64_t *d_k0;
+    const uint64_t *d_k1;
+    const uint64_t *d_meta;
+    int32_t n;
+    int32_t _pad;
+} sdp_heavy;
+/* One L1-bucket chunk of records [start, end); its phase-0 histogram entry for
+ * sub-bucket s is written at hbase + s * hstride. */
+typedef struct sdp_chunk {
+    int64_t start, end, hbase, hstride;
+} sdp_chunk;
 
-int sdp_group_part_rows_u64(const sdp_column *col, int32_t b1, int32_t with_counts,
-                            const sdp_buckets *out, uint64_t *d_stats, void *stream);
-int sdp_group_part_rows_bytes(const sdp_bytes_column *col, int32_t b1,
-                              const sdp_buckets *out, uint64_t *d_stats, void *stream);
-/* L1 buckets (nb1 of them) -> nb1 * 2^b2 L2 buckets by hash bits [64-b1-b2, 64-b1). */
-int sdp_group_part_recs(const sdp_buckets *in, int32_t nb1, const sdp_buckets *out,
-                        int32_t b1, int32_t b2, const sdp_bytes_column *bytes_col,
-                        int32_t with_counts, uint64_t *d_stats, void *stream);
-/* One workgroup per bucket: groups written back to the front of the bucket
- * (u64: key; bytes: (tag << 40 | row + 1)), d_ngroups[b] = groups in bucket b. */
-int sdp_group_dedup(const sdp_buckets *in, int64_t nbuckets, const sdp_bytes_column *bytes_col,
-                    int32_t with_counts, uint32_t *d_ngroups, uint64_t *d_stats, void *stream);
+/* Rows per partition workgroup (grid = ceil(length / this)). */
+int64_t sdp_part_rows_per_block(int64_t length, int32_t is_bytes);
+/* Mean records per final bucket the dedup tables are sized for. */
+int64_t sdp_part_bucket_target(int32_t is_bytes, int32_t with_counts);
+/* Evenly spaced sample: hashes (UINT64_MAX for nulls) and, for byte keys, the
+ * records.  Exactly one of col / bcol is non-NULL (as for every sdp_part_*). */
+int sdp_part_sample(const sdp_column *col, const sdp_bytes_column *bcol, int32_t n_sample,
+                    uint64_t *d_h, const sdp_records *d_out, void *stream);
+/* phase 0: d_hist[b * grid + block] (u32) + heavy counts + d_stats[0];
+ * phase 1: records scattered to d_out at d_offsets (exclusive scan of d_hist). */
+int sdp_part_rows(const sdp_column *col, const sdp_bytes_column *bcol, const sdp_heavy *heavy,
+                  int32_t b1, int32_t phase, uint32_t *d_hist, const uint64_t *d_offsets,
+                  const sdp_records *d_out, uint64_t *d_heavy_counts, uint64_t *d_stats,
+                  void *stream);
+/* L1 records -> sub-buckets by hash bits [64-b1-b2, 64-b1). */
+int sdp_part_recs(const sdp_records *in, int32_t is_bytes, const sdp_chunk *d_chunks,
+                  int64_t nchunks, int32_t b1, int32_t b2, int32_t phase, uint32_t *d_hist,
+                  const uint64_t *d_offsets, const sdp_records *out, void *stream);
+/* Final bucket f = records [d_starts[f], d_starts[f+1]).  Distinct only (fixed
+ * keys, !with_counts): group totals in d_stats.  Otherwise the groups of f go to
+ * d_out_key/d_out_cnt at [d_starts[f], + d_ngroups[f]): fixed keys as the
+ * order-preserving u64 key, byte keys as (hash tag << 40 | row + 1). */
+int sdp_part_dedup(const sdp_records *in, int32_t is_bytes, const sdp_bytes_column *bcol,
+                   const uint64_t *d_starts, int64_t nbuckets, int32_t with_counts,
+                   uint64_t *d_out_key, uint64_t *d_out_cnt, uint32_t *d_ngroups,
+                   uint64_t *d_stats, void *stream);
+/* Pack the per-bucket groups: src[d_starts[f] ..+ngroups[f]) -> dst[d_out_offsets[f] ..). */
+int sdp_part_compact(const uint64_t *d_src_a, const uint64_t *d_src_b, const uint64_t *d_starts,
+                     const uint32_t *d_ngroups, const uint64_t *d_out_offsets, int64_t nbuckets,
+                     uint64_t *d_dst_a, uint64_t *d_dst_b, void *stream);
+/* Exclusive scan of n u32 counts into n + 1 u64 offsets (d_out[n] = total). */
+int64_t sdp_scan_workspace_bytes(int64_t n);
+int sdp_scan_u32(const uint32_t *d_in, int64_t n, uint64_t *d_out, void *d_work,
+                 int64_t work_bytes, void *stream);
 
 /* ---- first rows (describe.py:276 limit(1), :282 limit(50)) ---------------- */
 /* Indices of the first k rows that survive na.drop (null, and NaN for floats). */

@@ -382,45 +382,95 @@ __global__ void __launch_bounds__(P1_BLOCK, 4) pass1_kernel(sdp_column col, cons
     }
 }
 
-__global__ void pass1_merge_kernel(const P1Partial *partials, int grid, const sdp_qplan *plan,
-                                   sdp_pass1_result *out) {
-    // one thread per field, partials visited in block order (deterministic)
+// Deterministic merge of the block partials: every field is reduced by the
+// whole workgroup (strided partial sums, then a fixed-order tree in LDS).
+constexpr int MERGE_T = 256;
+
+__device__ __forceinline__ void block_reduce_dd(double &h, double &l, double *sh, double *sl) {
+    sh[threadIdx.x] = h; sl[threadIdx.x] = l;
+    __syncthreads();
+    for (int o = MERGE_T / 2; o > 0; o >>= 1) {
+        if ((int)threadIdx.x < o) dd_add(sh[threadIdx.x], sl[threadIdx.x], sh[threadIdx.x + o], sl[threadIdx.x + o]);
+        __syncthreads();
+    }
+    h = sh[0]; l = sl[0];
+    __syncthreads();
+}
+
+template <typename V, typename Op>
+__device__ __forceinline__ V block_reduce(V v, V *sm, Op op) {
+    sm[threadIdx.x] = v;
+    __syncthreads();
+    for (int o = MERGE_T / 2; o > 0; o >>= 1) {
+        if ((int)threadIdx.x < o) sm[threadIdx.x] = op(sm[threadIdx.x], sm[threadIdx.x + o]);
+        __syncthreads();
+    }
+    v = sm[0];
+    __syncthreads();
+    return v;
+}
+
+__global__ void __launch_bounds__(MERGE_T) pass1_merge_kernel(const P1Partial *partials, int grid,
+                                                              const sdp_qplan *plan, sdp_pass1_result *out) {
+    __shared__ double sh[MERGE_T], sl[MERGE_T];
+    __shared__ uint64_t su[MERGE_T];
+    __shared__ int64_t si[MERGE_T];
     const int t = threadIdx.x;
-    if (t < NU) {
+    auto addu = [](uint64_t a, uint64_t b) { return a + b; };
+    for (int f = 0; f < NU; ++f) {
         uint64_t a = 0;
-        for (int b = 0; b < grid; ++b) a += partials[b].u[t];
-        uint64_t *dst;
-        if (t < 4) dst = (&out->count) + t;                 // count, n_valid, n_nan, n_zero
-        else if (t < 4 + W_) dst = out->w_gt + (t - 4);
-        else if (t < 4 + 2 * W_) dst = out->w_eq_lo + (t - 4 - W_);
-        else if (t < 4 + 3 * W_) dst = out->w_eq_hi + (t - 4 - 2 * W_);
-        else dst = out->w_in + (t - 4 - 3 * W_);
-        *dst = a;
-    } else if (t == 32) {
+        for (int b = t; b < grid; b += MERGE_T) a += partials[b].u[f];
+        a = block_reduce(a, su, addu);
+        if (t == 0) {
+            uint64_t *dst;
+            if (f < 4) dst = (&out->count) + f;
+            else if (f < 4 + W_) dst = out->w_gt + (f - 4);
+            else if (f < 4 + 2 * W_) dst = out->w_eq_lo + (f - 4 - W_);
+            else if (f < 4 + 3 * W_) dst = out->w_eq_hi + (f - 4 - 2 * W_);
+            else dst = out->w_in + (f - 4 - 3 * W_);
+            *dst = a;
+        }
+    }
+    {
         int64_t a = 0, mn = INT64_MAX, mx = INT64_MIN;
-        for (int b = 0; b < grid; ++b) {
+        for (int b = t; b < grid; b += MERGE_T) {
             a = (int64_t)((uint64_t)a + (uint64_t)partials[b].i[0]);
             mn = partials[b].i[1] < mn ? partials[b].i[1] : mn;
             mx = partials[b].i[2] > mx ? partials[b].i[2] : mx;
         }
-        out->isum = a; out->imin = mn; out->imax = mx;
-    } else if (t == 33 || t == 34) {
-        const int o = (t == 33) ? 0 : 3;
+        a = block_reduce(a, si, [](int64_t x, int64_t y) { return (int64_t)((uint64_t)x + (uint64_t)y); });
+        mn = block_reduce(mn, si, [](int64_t x, int64_t y) { return x < y ? x : y; });
+        mx = block_reduce(mx, si, [](int64_t x, int64_t y) { return x > y ? x : y; });
+        if (t == 0) { out->isum = a; out->imin = mn; out->imax = mx; }
+    }
+    for (int o = 0; o <= 3; o += 3) {
         double h = 0.0, l = 0.0;
-        for (int b = 0; b < grid; ++b) dd_add(h, l, partials[b].d[o], partials[b].d[o + 1]);
-        if (o == 0) { out->s1_hi = h; out->s1_lo = l; } else { out->s3_hi = h; out->s3_lo = l; }
-    } else if (t == 35) {
+        for (int b = t; b < grid; b += MERGE_T) dd_add(h, l, partials[b].d[o], partials[b].d[o + 1]);
+        block_reduce_dd(h, l, sh, sl);
+        if (t == 0) {
+            if (o == 0) { out->s1_hi = h; out->s1_lo = l; } else { out->s3_hi = h; out->s3_lo = l; }
+        }
+    }
+    {
         double a = 0.0, c = 0.0, mn = __builtin_inf(), mx = -__builtin_inf();
-        uint32_t ovf = 0;
-        for (int b = 0; b < grid; ++b) {
+        uint64_t ovf = 0;
+        for (int b = t; b < grid; b += MERGE_T) {
             a += partials[b].d[2]; c += partials[b].d[5];
             mn = fmin(mn, partials[b].d[6]); mx = fmax(mx, partials[b].d[7]);
             ovf |= partials[b].overflow;
         }
-        out->s2 = a; out->s4 = c; out->dmin = mn; out->dmax = mx;
-        out->w_overflow = ovf;
-        out->_pad = 0;
-        out->shift = plan->shift;
+        auto addd = [](double x, double y) { return x + y; };
+        a = block_reduce(a, sh, addd);
+        c = block_reduce(c, sh, addd);
+        mn = block_reduce(mn, sh, [](double x, double y) { return fmin(x, y); });
+        mx = block_reduce(mx, sh, [](double x, double y) { return fmax(x, y); });
+        ovf = block_reduce(ovf, su, [](uint64_t x, uint64_t y) { return x | y; });
+        if (t == 0) {
+            out->s2 = a; out->s4 = c; out->dmin = mn; out->dmax = mx;
+            out->w_overflow = (uint32_t)ovf;
+            out->_pad = 0;
+            out->shift = plan->shift;
+        }
     }
 }
 
@@ -724,26 +774,29 @@ __global__ void __launch_bounds__(P2_BLOCK, 4) pass2_kernel(sdp_column col, doub
         part_cnt[(int64_t)blockIdx.x * stride + 3 + i] = s_hist[i];
 }
 
-__global__ void pass2_merge_kernel(const double *part_mad, const uint64_t *part_cnt, int grid, int bins,
-                                   sdp_pass2_result *out, uint64_t *hist) {
+__global__ void __launch_bounds__(MERGE_T) pass2_merge_kernel(const double *part_mad, const uint64_t *part_cnt,
+                                                              int grid, int bins, sdp_pass2_result *out,
+                                                              uint64_t *hist) {
+    __shared__ double sh[MERGE_T];
+    __shared__ uint64_t su[MERGE_T];
     const int stride = 3 + bins;
-    for (int i = threadIdx.x; i < bins; i += blockDim.x) {
-        uint64_t s = 0;
-        for (int b = 0; b < grid; ++b) s += part_cnt[(int64_t)b * stride + 3 + i];
-        hist[i] = s;
-    }
-    if (threadIdx.x == 0) {
-        sdp_pass2_result r;
-        r.abs_dev_sum = 0.0;
-        r.n_high = r.n_low = r.n_unbinned = 0;
-        for (int b = 0; b < grid; ++b) {
-            r.abs_dev_sum += part_mad[b];
-            r.n_high += part_cnt[(int64_t)b * stride + 0];
-            r.n_low += part_cnt[(int64_t)b * stride + 1];
-            r.n_unbinned += part_cnt[(int64_t)b * stride + 2];
+    const int t = threadIdx.x;
+    auto addu = [](uint64_t a, uint64_t b) { return a + b; };
+    for (int f = 0; f < 3 + bins; ++f) {
+        uint64_t a = 0;
+        for (int b = t; b < grid; b += MERGE_T) a += part_cnt[(int64_t)b * stride + f];
+        a = block_reduce(a, su, addu);
+        if (t == 0) {
+            if (f == 0) out->n_high = a;
+            else if (f == 1) out->n_low = a;
+            else if (f == 2) out->n_unbinned = a;
+            else hist[f - 3] = a;
         }
-        *out = r;
     }
+    double m = 0.0;
+    for (int b = t; b < grid; b += MERGE_T) m += part_mad[b];
+    m = block_reduce(m, sh, [](double x, double y) { return x + y; });
+    if (t == 0) out->abs_dev_sum = m;
 }
 
 static int p2_grid(int64_t n, int dt) {
@@ -815,8 +868,7 @@ extern "C" int sdp_pass1(const sdp_column *col, const sdp_qplan *d_plan, void *d
                            d_cand_counts, slot_capacity));
     rc = check_launch("pass1_kernel");
     if (rc) return rc;
-    hipLaunchKernelGGL(pass1_merge_kernel, dim3(1), dim3(64), 0, s, parts, grid, d_plan, d_result);
-    static_assert(NU <= 32, "merge thread map");
+    hipLaunchKernelGGL(pass1_merge_kernel, dim3(1), dim3(MERGE_T), 0, s, parts, grid, d_plan, d_result);
     return check_launch("pass1_merge_kernel");
 }
 
@@ -890,6 +942,6 @@ extern "C" int sdp_pass2(const sdp_column *col, double mean, const double *d_edg
     }
     rc = check_launch("pass2_kernel");
     if (rc) return rc;
-    hipLaunchKernelGGL(pass2_merge_kernel, dim3(1), dim3(256), 0, s, pm, pc, grid, bins, d_result, d_hist);
+    hipLaunchKernelGGL(pass2_merge_kernel, dim3(1), dim3(MERGE_T), 0, s, pm, pc, grid, bins, d_result, d_hist);
     return check_launch("pass2_merge_kernel");
 }

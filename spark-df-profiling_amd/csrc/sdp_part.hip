@@ -1,0 +1,1122 @@
+// sdp_part.hip -- exact distinct counts and value counts by two-level hash
+// partitioning with exact offsets (gfx950).
+//
+// Replaces countDistinct (describe.py:143) and the groupBy(c).count() of
+// describe_categorical_1d (describe.py:251) for columns of any cardinality.
+//
+// Every valid row becomes one record.  Fixed-width keys: the record is
+// h = mix64(key) (a bijection, so distinct h == distinct keys and the key is
+// recovered by inv_mix64).  Byte keys: (k0, k1, meta) with k0/k1 the first 16
+// bytes (zero padded) and meta = len << 40 | row + 1; strings longer than 16
+// bytes carry their 64-bit hash in k0 and are compared byte for byte against
+// the column.  Pipeline (each step a kernel, every probe in LDS):
+//
+//   rows  phase 0  per-block histogram of the top b1 hash bits -> H1[b][block]
+//   scan           exclusive scan of H1 (bucket-major) -> exact record offsets
+//   rows  phase 1  re-read; per 4096-row tile an LDS counting sort by bucket,
+//                  then each bucket's run is written contiguously at its offset
+//   recs  phase 0  per L1 chunk histogram of the next b2 bits -> H2
+//   scan           -> exact offsets of every (L1 bucket, sub-bucket, chunk)
+//   recs  phase 1  LDS counting sort + contiguous runs, as above
+//   dedup          one workgroup per final bucket (~2-8 K records) groups its
+//                  records in an LDS hash table; distinct counts, or groups +
+//                  counts written in place and compacted
+//
+// Keys seen >= 3 times in a 16 K-row sample ("heavy" keys, at most 256) are
+// counted per block in LDS during phase 0 and never become records, so skewed
+// columns do not pile up in one bucket.  Offsets come from the scans, so the
+// output is packed exactly and nothing can overflow; every stage except the
+// LDS atomics inside a tile is deterministic.
+#include <type_traits>
+#include "sdp_common.h"
+
+namespace sdp {
+
+constexpr int PT = 256;                 // threads per partition workgroup
+constexpr int U_RPT = 16;               // fixed-width rows per thread per tile
+constexpr int U_TILE = PT * U_RPT;      // 4096
+constexpr int B_RPT = 8;                // byte rows per thread per tile
+constexpr int B_TILE = PT * B_RPT;      // 2048
+constexpr int B_STAGE = 32768;          // LDS bytes of string data per tile
+constexpr int MAXB = 1024;              // buckets per level (b <= 10)
+constexpr int HEAVY_MAX = 256;
+constexpr int HEAVY_SLOTS = 512;
+constexpr int SHORT_MAX = 16;
+constexpr uint64_t RMASK40 = (1ull << 40) - 1ull;
+constexpr uint64_t LEN_MAX = (1ull << 24) - 1ull;
+
+// ---- hashing ------------------------------------------------------------------
+__host__ __device__ __forceinline__ uint64_t inv_mix64(uint64_t x) {
+    x ^= (x >> 31) ^ (x >> 62);
+    x *= 0x319642B2D24D8EC3ull;
+    x ^= (x >> 27) ^ (x >> 54);
+    x *= 0x96DE1B173F119089ull;
+    x ^= (x >> 30) ^ (x >> 60);
+    return x;
+}
+__device__ __forceinline__ uint64_t bh_init(uint64_t len) {
+    return 0x9E3779B97F4A7C15ull ^ (len * 0xFF51AFD7ED558CCDull);
+}
+__device__ __forceinline__ uint64_t bh_step(uint64_t h, uint64_t w) {
+    h = (h ^ w) * 0x87C37B91114253D5ull;
+    return (h << 31) | (h >> 33);
+}
+// hash of a string of <= 16 bytes given as zero-padded little-endian words
+__device__ __forceinline__ uint64_t bh_short(uint64_t k0, uint64_t k1, uint64_t len) {
+    uint64_t h = bh_init(len);
+    if (len > 0) h = bh_step(h, k0);
+    if (len > 8) h = bh_step(h, k1);
+    return mix64(h);
+}
+// hash of a byte record (short: recomputed from the bytes; long: carried in k0)
+__device__ __forceinline__ uint64_t rec_hash(uint64_t k0, uint64_t k1, uint64_t meta) {
+    const uint64_t len = meta >> 40;
+    return len <= SHORT_MAX ? bh_short(k0, k1, len) : k0;
+}
+
+// ---- string access --------------------------------------------------------------
+__device__ __forceinline__ int64_t str_off(const sdp_bytes_column &c, int64_t row) {
+    if (c.fixed_width > 0) return row * (int64_t)c.fixed_width;
+    if (c.offset_width == 8) return ((const int64_t *)c.d_offsets)[row];
+    return (int64_t)((const int32_t *)c.d_offsets)[row];
+}
+// 8 bytes at an arbitrary global address (reads aligned dwords; the data
+// buffer is padded by 16 bytes), zero beyond `avail`
+__device__ __forceinline__ uint64_t gload8(const uint8_t *p, int64_t avail) {
+    if (avail <= 0) return 0ull;
+    const uintptr_t a = (uintptr_t)p;
+    const uint32_t *w = (const uint32_t *)(a & ~(uintptr_t)3);
+    const uint32_t sh = (uint32_t)(a & 3);
+    const uint32_t w0 = w[0], w1 = w[1], w2 = w[2];
+    const uint64_t v = (uint64_t)__builtin_amdgcn_alignbyte(w1, w0, sh) |
+                       ((uint64_t)__builtin_amdgcn_alignbyte(w2, w1, sh) << 32);
+    return avail >= 8 ? v : (v & ((1ull << (8 * avail)) - 1ull));
+}
+// 8 bytes at LDS byte offset `off` of a dword-staged buffer
+__device__ __forceinline__ uint64_t lload8(const uint32_t *s, int64_t off, int64_t avail) {
+    if (avail <= 0) return 0ull;
+    const int64_t w = off >> 2;
+    const uint32_t sh = (uint32_t)(off & 3);
+    const uint32_t w0 = s[w], w1 = s[w + 1], w2 = s[w + 2];
+    const uint64_t v = (uint64_t)__builtin_amdgcn_alignbyte(w1, w0, sh) |
+                       ((uint64_t)__builtin_amdgcn_alignbyte(w2, w1, sh) << 32);
+    return avail >= 8 ? v : (v & ((1ull << (8 * avail)) - 1ull));
+}
+__device__ uint64_t hash_long_global(const uint8_t *p, int64_t len) {
+    uint64_t h = bh_init((uint64_t)len);
+    for (int64_t i = 0; i < len; i += 8) h = bh_step(h, gload8(p + i, len - i));
+    return mix64(h);
+}
+__device__ uint64_t hash_long_lds(const uint32_t *s, int64_t off, int64_t len) {
+    uint64_t h = bh_init((uint64_t)len);
+    for (int64_t i = 0; i < len; i += 8) h = bh_step(h, lload8(s, off + i, len - i));
+    return mix64(h);
+}
+__device__ bool rows_equal_global(const sdp_bytes_column &c, int64_t ra, int64_t rb) {
+    const int64_t a0 = str_off(c, ra), a1 = str_off(c, ra + 1);
+    const int64_t b0 = str_off(c, rb), b1 = str_off(c, rb + 1);
+    const int64_t len = a1 - a0;
+    if (len != b1 - b0) return false;
+    for (int64_t i = 0; i < len; i += 8)
+        if (gload8(c.d_data + a0 + i, len - i) != gload8(c.d_data + b0 + i, len - i)) return false;
+    return true;
+}
+
+// ---- heavy keys ---------------------------------------------------------------
+struct HeavyArg {
+    const uint64_t *h;      // [n] hashes (fixed: h = mix64(key))
+    const uint64_t *k0;     // bytes only
+    const uint64_t *k1;
+    const uint64_t *meta;
+    int32_t n;
+};
+struct HeavyLds {
+    uint64_t h[HEAVY_SLOTS];
+    int16_t idx[HEAVY_SLOTS];
+    uint64_t k0[HEAVY_MAX];
+    uint64_t k1[HEAVY_MAX];
+    uint32_t len[HEAVY_MAX];
+    uint32_t cnt[HEAVY_MAX];
+};
+template <bool BYTES>
+__device__ void heavy_build(HeavyLds &s, const HeavyArg &a) {
+    for (int i = threadIdx.x; i < HEAVY_SLOTS; i += blockDim.x) s.h[i] = EMPTY64;
+    for (int i = threadIdx.x; i < HEAVY_MAX; i += blockDim.x) s.cnt[i] = 0;
+    __syncthreads();
+    for (int i = threadIdx.x; i < a.n; i += blockDim.x) {
+        const uint64_t h = a.h[i];
+        uint32_t pos = (uint32_t)h & (HEAVY_SLOTS - 1);
+        while (true) {
+            const uint64_t old = atomicCAS((unsigned long long *)&s.h[pos], (unsigned long long)EMPTY64,
+                                           (unsigned long long)h);
+            if (old == EMPTY64) { s.idx[pos] = (int16_t)i; break; }
+            pos = (pos + 1) & (HEAVY_SLOTS - 1);
+        }
+        if constexpr (BYTES) {
+            s.k0[i] = a.k0[i];
+            s.k1[i] = a.k1[i];
+            s.len[i] = (uint32_t)(a.meta[i] >> 40);
+        }
+    }
+    __syncthreads();
+}
+// index of the heavy key equal to this row, or -1
+__device__ __forceinline__ int heavy_find_u64(const HeavyLds &s, int n, uint64_t h) {
+    if (n == 0 || h == EMPTY64) return -1;
+    uint32_t pos = (uint32_t)h & (HEAVY_SLOTS - 1);
+    while (true) {
+        const uint64_t v = s.h[pos];
+        if (v == h) return s.idx[pos];
+        if (v == EMPTY64) return -1;
+        pos = (pos + 1) & (HEAVY_SLOTS - 1);
+    }
+}
+__device__ __forceinline__ int heavy_find_bytes(const HeavyLds &s, int n, uint64_t h, uint64_t k0, uint64_t k1,
+                                                uint32_t len) {
+    if (n == 0 || len > SHORT_MAX || h == EMPTY64) return -1;
+    uint32_t pos = (uint32_t)h & (HEAVY_SLOTS - 1);
+    while (true) {
+        const uint64_t v = s.h[pos];
+        if (v == EMPTY64) return -1;
+        if (v == h) {
+            const int i = s.idx[pos];
+            if (s.k0[i] == k0 && s.k1[i] == k1 && s.len[i] == len) return i;
+        }
+        pos = (pos + 1) & (HEAVY_SLOTS - 1);
+    }
+}
+__device__ void heavy_flush(HeavyLds &s, int n, uint64_t *counts) {
+    __syncthreads();
+    for (int i = threadIdx.x; i < n; i += blockDim.x)
+        if (s.cnt[i]) atomicAdd((unsigned long long *)&counts[i], (unsigned long long)s.cnt[i]);
+}
+
+// ---- block scan of nb <= MAXB LDS counters (exclusive) ------------------------
+__device__ void block_excl_scan(const uint32_t *in, uint32_t *out, int nb, uint32_t *s_wsum) {
+    constexpr int PER = MAXB / PT;      // 4 entries per thread
+    const int t = threadIdx.x;
+    uint32_t v[PER];
+    uint32_t sum = 0;
+#pragma unroll
+    for (int k = 0; k < PER; ++k) {
+        const int i = t * PER + k;
+        v[k] = i < nb ? in[i] : 0u;
+        sum += v[k];
+    }
+    // inclusive scan of `sum` across the wave
+    uint32_t x = sum;
+    const int lane = lane_id();
+#pragma unroll
+    for (int o = 1; o < WAVE; o <<= 1) {
+        const uint32_t y = __shfl_up(x, o, WAVE);
+        if (lane >= o) x += y;
+    }
+    const int w = t / WAVE;
+    if (lane == WAVE - 1) s_wsum[w] = x;
+    __syncthreads();
+    uint32_t wb = 0;
+    for (int k = 0; k < w; ++k) wb += s_wsum[k];
+    uint32_t run = wb + x - sum;
+#pragma unroll
+    for (int k = 0; k < PER; ++k) {
+        const int i = t * PER + k;
+        if (i < nb) out[i] = run;
+        run += v[k];
+    }
+    __syncthreads();
+}
+
+// ---- fixed-width row loading ----------------------------------------------------
+__device__ __forceinline__ uint64_t fetch_key(const sdp_column &c, int64_t i, bool &valid) {
+    valid = valid_bit(c.d_validity, c.validity_bit_offset, i);
+    switch (c.dtype) {
+    case SDP_I8: return Elem<int8_t>::key(((const int8_t *)c.d_values)[i]);
+    case SDP_I16: return Elem<int16_t>::key(((const int16_t *)c.d_values)[i]);
+    case SDP_I32: return Elem<int32_t>::key(((const int32_t *)c.d_values)[i]);
+    case SDP_I64: return Elem<int64_t>::key(((const int64_t *)c.d_values)[i]);
+    case SDP_U8: return ((const uint8_t *)c.d_values)[i];
+    case SDP_U16: return ((const uint16_t *)c.d_values)[i];
+    case SDP_U32: return ((const uint32_t *)c.d_values)[i];
+    case SDP_U64: return ((const uint64_t *)c.d_values)[i];
+    case SDP_F32: return Elem<float>::key(((const float *)c.d_values)[i]);
+    case SDP_F64: return Elem<double>::key(((const double *)c.d_values)[i]);
+    case SDP_BOOL: {
+        const int64_t b = c.validity_bit_offset + i;
+        return (((const uint8_t *)c.d_values)[b >> 3] >> (b & 7)) & 1u;
+    }
+    default: valid = false; return 0;
+    }
+}
+template <typename T> __device__ __forceinline__ uint64_t key_of(T v);
+template <> __device__ __forceinline__ uint64_t key_of<double>(double v) { return f64_key(v); }
+template <> __device__ __forceinline__ uint64_t key_of<float>(float v) { return f64_key((double)v); }
+template <> __device__ __forceinline__ uint64_t key_of<int64_t>(int64_t v) { return i64_key(v); }
+template <> __device__ __forceinline__ uint64_t key_of<int32_t>(int32_t v) { return i64_key(v); }
+template <> __device__ __forceinline__ uint64_t key_of<int16_t>(int16_t v) { return i64_key(v); }
+template <> __device__ __forceinline__ uint64_t key_of<int8_t>(int8_t v) { return i64_key(v); }
+template <> __device__ __forceinline__ uint64_t key_of<uint64_t>(uint64_t v) { return v; }
+template <> __device__ __forceinline__ uint64_t key_of<uint32_t>(uint32_t v) { return v; }
+template <> __device__ __forceinline__ uint64_t key_of<uint16_t>(uint16_t v) { return v; }
+template <> __device__ __forceinline__ uint64_t key_of<uint8_t>(uint8_t v) { return v; }
+
+// The U_RPT rows of thread t in the tile at `base`: slot q of thread t is row
+// base + ((q / VPT) * PT + t) * VPT + q % VPT (16-byte vector loads) for full
+// tiles of a vectorisable dtype, else row base + q * PT + t.
+template <typename T>
+__device__ __forceinline__ void load_tile_u64(const sdp_column &c, int64_t base, int64_t end, uint64_t (&h)[U_RPT],
+                                              uint32_t &vmask) {
+    vmask = 0;
+    const int t = threadIdx.x;
+    if constexpr (!std::is_same<T, bool>::value) {
+        constexpr int VPT = Vec16<T>::N;
+        if (base + U_TILE <= end && (base % VPT) == 0) {
+            const Vec16<T> *vals = (const Vec16<T> *)c.d_values;
+            Vec16<T> v[U_RPT / VPT];
+            uint32_t vb[U_RPT / VPT];
+#pragma unroll
+            for (int u = 0; u < U_RPT / VPT; ++u) {
+                const int64_t vi = base / VPT + (int64_t)u * PT + t;
+                v[u] = vals[vi];
+                vb[u] = valid_bits(c.d_validity, c.validity_bit_offset, vi * VPT, VPT);
+            }
+#pragma unroll
+            for (int u = 0; u < U_RPT / VPT; ++u)
+#pragma unroll
+                for (int e = 0; e < VPT; ++e) {
+                    const int q = u * VPT + e;
+                    h[q] = mix64(key_of<T>(v[u].v[e]));
+                    vmask |= ((vb[u] >> e) & 1u) << q;
+                }
+            return;
+        }
+    }
+#pragma unroll
+    for (int q = 0; q < U_RPT; ++q) {
+        const int64_t i = base + (int64_t)q * PT + t;
+        h[q] = 0;
+        if (i < end) {
+            bool ok;
+            const uint64_t k = fetch_key(c, i, ok);
+            h[q] = mix64(k);
+            vmask |= (uint32_t)ok << q;
+        }
+    }
+}
+
+// ---- rows -> L1 buckets (fixed width) ------------------------------------------
+struct RowsLds {
+    HeavyLds heavy;
+    uint32_t hist[MAXB];
+    uint32_t off[MAXB];
+    uint64_t cur[MAXB];
+    uint64_t stage[U_TILE];
+    uint16_t bkt[U_TILE];
+    uint32_t wsum[PT / WAVE];
+};
+
+template <typename T, bool SCATTER>
+__global__ void __launch_bounds__(PT) part_rows_u64_kernel(sdp_column col, HeavyArg heavy, int b1,
+                                                           int64_t rows_per_block, uint32_t *hist,
+                                                           const uint64_t *offs, uint64_t *out_h,
+                                                           uint64_t *heavy_counts, uint64_t *stats) {
+    __shared__ RowsLds s;
+    const int G = gridDim.x, g = blockIdx.x, t = threadIdx.x;
+    const int nb = 1 << b1;
+    const int shift = 64 - b1;
+    const int64_t r0 = (int64_t)g * rows_per_block;
+    const int64_t r1 = min(col.length, r0 + rows_per_block);
+    heavy_build<false>(s.heavy, heavy);
+    for (int b = t; b < nb; b += PT) {
+        s.hist[b] = 0;
+        if (SCATTER) s.cur[b] = offs[(int64_t)b * G + g];
+    }
+    __syncthreads();
+    uint64_t rows = 0;
+    for (int64_t base = r0; base < r1; base += U_TILE) {
+        uint64_t h[U_RPT];
+        uint32_t vmask;
+        load_tile_u64<T>(col, base, r1, h, vmask);
+        uint32_t rank[U_RPT];
+        uint32_t keep = 0;
+#pragma unroll
+        for (int q = 0; q < U_RPT; ++q) {
+            if ((vmask >> q) & 1u) {
+                ++rows;
+                const int hv = heavy_find_u64(s.heavy, heavy.n, h[q]);
+                if (hv >= 0) {
+                    if (!SCATTER) atomicAdd(&s.heavy.cnt[hv], 1u);
+                } else {
+                    keep |= 1u << q;
+                    const int b = b1 ? (int)(h[q] >> shift) : 0;
+                    rank[q] = atomicAdd(&s.hist[b], 1u);
+                }
+            }
+        }
+        if constexpr (SCATTER) {
+            __syncthreads();
+            block_excl_scan(s.hist, s.off, nb, s.wsum);
+#pragma unroll
+            for (int q = 0; q < U_RPT; ++q) {
+                if ((keep >> q) & 1u) {
+                    const int b = b1 ? (int)(h[q] >> shift) : 0;
+                    const uint32_t p = s.off[b] + rank[q];
+                    s.stage[p] = h[q];
+                    s.bkt[p] = (uint16_t)b;
+                }
+            }
+            __syncthreads();
+            const uint32_t total = s.off[nb - 1] + s.hist[nb - 1];
+            for (uint32_t j = t; j < total; j += PT) {
+                const int b = s.bkt[j];
+                out_h[s.cur[b] + (j - s.off[b])] = s.stage[j];
+            }
+            __syncthreads();
+            for (int b = t; b < nb; b += PT) {
+                s.cur[b] += s.hist[b];
+                s.hist[b] = 0;
+            }
+            __syncthreads();
+        }
+    }
+    if constexpr (!SCATTER) {
+        __syncthreads();
+        for (int b = t; b < nb; b += PT) hist[(int64_t)b * G + g] = s.hist[b];
+        heavy_flush(s.heavy, heavy.n, heavy_counts);
+        rows = wave_sum_u64(rows);
+        if (lane_id() == 0 && rows) atomicAdd((unsigned long long *)&stats[0], (unsigned long long)rows);
+    }
+}
+
+// ---- rows -> L1 buckets (byte keys) ---------------------------------------------
+struct BRowsLds {
+    HeavyLds heavy;
+    uint32_t hist[MAXB];
+    uint32_t off[MAXB];
+    uint64_t cur[MAXB];
+    union {
+        uint32_t bytes[B_STAGE / 4 + 8];
+        struct {
+            uint64_t k0[B_TILE];
+            uint64_t k1[B_TILE];
+            uint64_t meta[B_TILE];
+        } rec;
+    } u;
+    uint16_t bkt[B_TILE];
+    uint32_t wsum[PT / WAVE];
+    int64_t stage_base;
+    int staged;
+};
+
+template <bool SCATTER>
+__global__ void __launch_bounds__(PT) part_rows_bytes_kernel(sdp_bytes_column col, HeavyArg heavy, int b1,
+                                                             int64_t rows_per_block, uint32_t *hist,
+                                                             const uint64_t *offs, uint64_t *out_k0,
+                                                             uint64_t *out_k1, uint64_t *out_meta,
+                                                             uint64_t *heavy_counts, uint64_t *stats) {
+    __shared__ BRowsLds s;
+    const int G = gridDim.x, g = blockIdx.x, t = threadIdx.x;
+    const int nb = 1 << b1;
+    const int shift = 64 - b1;
+    const int64_t r0 = (int64_t)g * rows_per_block;
+    const int64_t r1 = min(col.length, r0 + rows_per_block);
+    heavy_build<true>(s.heavy, heavy);
+    for (int b = t; b < nb; b += PT) {
+        s.hist[b] = 0;
+        if (SCATTER) s.cur[b] = offs[(int64_t)b * G + g];
+    }
+    __syncthreads();
+    uint64_t rows = 0;
+    for (int64_t base = r0; base < r1; base += B_TILE) {
+        const int64_t tend = min(r1, base + B_TILE);
+        // stage the tile's bytes [o_lo & ~15, o_hi rounded up to 16) when they fit
+        if (t == 0) {
+            const int64_t lo = str_off(col, base) & ~(int64_t)15;
+            const int64_t hi = (str_off(col, tend) + 15) & ~(int64_t)15;
+            s.stage_base = lo;
+            s.staged = (hi - lo) <= B_STAGE ? 1 : 0;
+        }
+        __syncthreads();
+        const int64_t sbase = s.stage_base;
+        const bool staged = s.staged != 0;
+        if (staged) {
+            const int64_t hi = (str_off(col, tend) + 15) & ~(int64_t)15;
+            const int nvec = (int)((hi - sbase) >> 4);
+            const uint4 *src = (const uint4 *)(col.d_data + sbase);
+            uint4 *dst = (uint4 *)s.u.bytes;
+            for (int v = t; v < nvec; v += PT) dst[v] = src[v];
+        }
+        __syncthreads();
+        uint64_t k0[B_RPT], k1[B_RPT], meta[B_RPT], h[B_RPT];
+        uint32_t rank[B_RPT];
+        uint32_t keep = 0;
+#pragma unroll
+        for (int q = 0; q < B_RPT; ++q) {
+            const int64_t row = base + (int64_t)q * PT + t;
+            meta[q] = 0;
+            if (row < tend && valid_bit(col.d_validity, col.validity_bit_offset, row)) {
+                ++rows;
+                const int64_t o0 = str_off(col, row), o1 = str_off(col, row + 1);
+                const int64_t len = o1 - o0;
+                if (len <= SHORT_MAX) {
+                    if (staged) {
+                        k0[q] = lload8(s.u.bytes, o0 - sbase, len);
+                        k1[q] = lload8(s.u.bytes, o0 - sbase + 8, len - 8);
+                    } else {
+                        k0[q] = gload8(col.d_data + o0, len);
+                        k1[q] = gload8(col.d_data + o0 + 8, len - 8);
+                    }
+                    h[q] = bh_short(k0[q], k1[q], (uint64_t)len);
+                } else {
+                    h[q] = staged ? hash_long_lds(s.u.bytes, o0 - sbase, len)
+                                  : hash_long_global(col.d_data + o0, len);
+                    k0[q] = h[q];
+                    k1[q] = 0;
+                }
+                meta[q] = ((uint64_t)min((int64_t)LEN_MAX, len) << 40) | (uint64_t)(row + 1);
+                const int hv = heavy_find_bytes(s.heavy, heavy.n, h[q], k0[q], k1[q], (uint32_t)len);
+                if (hv >= 0) {
+                    if (!SCATTER) atomicAdd(&s.heavy.cnt[hv], 1u);
+                } else {
+                    keep |= 1u << q;
+                    const int b = b1 ? (int)(h[q] >> shift) : 0;
+                    rank[q] = atomicAdd(&s.hist[b], 1u);
+                }
+            }
+        }
+        __syncthreads();        // staged bytes consumed (the record stage aliases them)
+        if constexpr (SCATTER) {
+            block_excl_scan(s.hist, s.off, nb, s.wsum);
+#pragma unroll
+            for (int q = 0; q < B_RPT; ++q) {
+                if ((keep >> q) & 1u) {
+                    const int b = b1 ? (int)(h[q] >> shift) : 0;
+                    const uint32_t p = s.off[b] + rank[q];
+                    s.u.rec.k0[p] = k0[q];
+                    s.u.rec.k1[p] = k1[q];
+                    s.u.rec.meta[p] = meta[q];
+                    s.bkt[p] = (uint16_t)b;
+                }
+            }
+            __syncthreads();
+            const uint32_t total = s.off[nb - 1] + s.hist[nb - 1];
+            for (uint32_t j = t; j < total; j += PT) {
+                const int b = s.bkt[j];
+                const uint64_t o = s.cur[b] + (j - s.off[b]);
+                out_k0[o] = s.u.rec.k0[j];
+                out_k1[o] = s.u.rec.k1[j];
+                out_meta[o] = s.u.rec.meta[j];
+            }
+            __syncthreads();
+            for (int b = t; b < nb; b += PT) {
+                s.cur[b] += s.hist[b];
+                s.hist[b] = 0;
+            }
+            __syncthreads();
+        }
+    }
+    if constexpr (!SCATTER) {
+        __syncthreads();
+        for (int b = t; b < nb; b += PT) hist[(int64_t)b * G + g] = s.hist[b];
+        heavy_flush(s.heavy, heavy.n, heavy_counts);
+        rows = wave_sum_u64(rows);
+        if (lane_id() == 0 && rows) atomicAdd((unsigned long long *)&stats[0], (unsigned long long)rows);
+    }
+}
+
+// ---- L1 records -> L2 buckets ----------------------------------------------------
+// Chunk c = records [start, end) of one L1 bucket; its histogram entry for
+// sub-bucket s lives at hbase + s * hstride (so the flat exclusive scan orders
+// records by (L1 bucket, sub-bucket, chunk)).
+struct Chunk {
+    int64_t start, end, hbase, hstride;
+};
+
+template <bool BYTES>
+struct RecsLds {
+    uint32_t hist[MAXB];
+    uint32_t off[MAXB];
+    uint64_t cur[MAXB];
+    uint64_t k0[BYTES ? B_TILE : U_TILE];
+    uint64_t k1[BYTES ? B_TILE : 1];
+    uint64_t meta[BYTES ? B_TILE : 1];
+    uint16_t bkt[BYTES ? B_TILE : U_TILE];
+    uint32_t wsum[PT / WAVE];
+};
+
+template <bool BYTES, bool SCATTER>
+__global__ void __launch_bounds__(PT) part_recs_kernel(const uint64_t *in_k0, const uint64_t *in_k1,
+                                                       const uint64_t *in_meta, const Chunk *chunks,
+                                                       int64_t nchunks, int b1, int b2, uint32_t *hist,
+                                                       const uint64_t *offs, uint64_t *out_k0, uint64_t *out_k1,
+                                                       uint64_t *out_meta) {
+    constexpr int RPT = BYTES ? B_RPT : U_RPT;
+    constexpr int TILE = PT * RPT;
+    __shared__ RecsLds<BYTES> s;
+    const int t = threadIdx.x;
+    const int nb = 1 << b2;
+    const int shift = 64 - b1 - b2;
+    for (int64_t c = blockIdx.x; c < nchunks; c += gridDim.x) {
+        const Chunk ch = chunks[c];
+        for (int b = t; b < nb; b += PT) {
+            s.hist[b] = 0;
+            if (SCATTER) s.cur[b] = offs[ch.hbase + (int64_t)b * ch.hstride];
+        }
+        __syncthreads();
+        for (int64_t base = ch.start; base < ch.end; base += TILE) {
+            uint64_t k0[RPT], k1[RPT], meta[RPT];
+            uint32_t rank[RPT];
+            int bk[RPT];
+            uint32_t have = 0;
+#pragma unroll
+            for (int q = 0; q < RPT; ++q) {
+                const int64_t r = base + (int64_t)q * PT + t;
+                if (r < ch.end) {
+                    have |= 1u << q;
+                    k0[q] = in_k0[r];
+                    if (BYTES) { k1[q] = in_k1[r]; meta[q] = in_meta[r]; }
+                }
+            }
+#pragma unroll
+            for (int q = 0; q < RPT; ++q) {
+                if ((have >> q) & 1u) {
+                    const uint64_t h = BYTES ? rec_hash(k0[q], k1[q], meta[q]) : k0[q];
+                    bk[q] = (int)((h >> shift) & (uint64_t)(nb - 1));
+                    rank[q] = atomicAdd(&s.hist[bk[q]], 1u);
+                }
+            }
+            if constexpr (SCATTER) {
+                __syncthreads();
+                block_excl_scan(s.hist, s.off, nb, s.wsum);
+#pragma unroll
+                for (int q = 0; q < RPT; ++q) {
+                    if ((have >> q) & 1u) {
+                        const uint32_t p = s.off[bk[q]] + rank[q];
+                        s.k0[p] = k0[q];
+                        if (BYTES) { s.k1[p] = k1[q]; s.meta[p] = meta[q]; }
+                        s.bkt[p] = (uint16_t)bk[q];
+                    }
+                }
+                __syncthreads();
+                const uint32_t total = s.off[nb - 1] + s.hist[nb - 1];
+                for (uint32_t j = t; j < total; j += PT) {
+                    const int b = s.bkt[j];
+                    const uint64_t o = s.cur[b] + (j - s.off[b]);
+                    out_k0[o] = s.k0[j];
+                    if (BYTES) { out_k1[o] = s.k1[j]; out_meta[o] = s.meta[j]; }
+                }
+                __syncthreads();
+                for (int b = t; b < nb; b += PT) {
+                    s.cur[b] += s.hist[b];
+                    s.hist[b] = 0;
+                }
+                __syncthreads();
+            }
+        }
+        if constexpr (!SCATTER) {
+            __syncthreads();
+            for (int b = t; b < nb; b += PT) hist[ch.hbase + (int64_t)b * ch.hstride] = s.hist[b];
+            __syncthreads();
+        }
+    }
+}
+
+// ---- final buckets: LDS grouping -------------------------------------------------
+constexpr int DT = 1024;                // dedup threads per workgroup
+constexpr int D_U64 = 16384;            // table slots, fixed keys, distinct only (128 KB)
+constexpr int D_U64C = 8192;            // fixed keys with counts (96 KB)
+constexpr int D_B = 4096;               // byte keys (144 KB)
+
+// stats: [1] records whose h == UINT64_MAX (fixed keys; kept outside the table),
+// [2] hash collision between different byte strings, [3] table full,
+// [4 + (f & 63)] groups.
+template <bool COUNTS>
+__global__ void __launch_bounds__(DT) part_dedup_u64_kernel(const uint64_t *in_h, const uint64_t *starts,
+                                                            int64_t nbuckets, uint64_t *out_key,
+                                                            uint64_t *out_cnt, uint32_t *ngroups,
+                                                            uint64_t *stats) {
+    constexpr int S = COUNTS ? D_U64C : D_U64;
+    __shared__ uint64_t s_key[S];
+    __shared__ uint32_t s_cnt[COUNTS ? S : 1];
+    __shared__ uint32_t s_n, s_special, s_full;
+    const int t = threadIdx.x;
+    for (int64_t f = blockIdx.x; f < nbuckets; f += gridDim.x) {
+        const int64_t lo = starts[f], hi = starts[f + 1];
+        if (lo == hi) {
+            if (COUNTS && t == 0) ngroups[f] = 0;
+            continue;
+        }
+        for (int i = t; i < S; i += DT) {
+            s_key[i] = EMPTY64;
+            if (COUNTS) s_cnt[i] = 0;
+        }
+        if (t == 0) { s_n = 0; s_special = 0; s_full = 0; }
+        __syncthreads();
+        uint32_t fresh = 0, special = 0;
+        bool full = false;
+        for (int64_t r = lo + t; r < hi; r += DT) {
+            const uint64_t h = in_h[r];
+            if (h == EMPTY64) { ++special; continue; }
+            uint32_t pos = (uint32_t)h & (S - 1);
+            int probe = 0;
+            for (; probe < S; ++probe) {
+                uint64_t cur = s_key[pos];
+                if (cur == EMPTY64) {
+                    cur = atomicCAS((unsigned long long *)&s_key[pos], (unsigned long long)EMPTY64,
+                                    (unsigned long long)h);
+                    if (cur == EMPTY64) { ++fresh; break; }
+                }
+                if (cur == h) break;
+                pos = (pos + 1) & (S - 1);
+            }
+            if (probe == S) { full = true; continue; }
+            if (COUNTS) atomicAdd(&s_cnt[pos], 1u);
+        }
+        if (special) atomicAdd(&s_special, special);
+        if (full) s_full = 1;
+        if (!COUNTS) {
+            fresh = (uint32_t)wave_sum_u64(fresh);
+            if (lane_id() == 0 && fresh) atomicAdd(&s_n, fresh);
+        }
+        __syncthreads();
+        if constexpr (COUNTS) {
+            for (int i = t; i < S; i += DT) {
+                const uint64_t h = s_key[i];
+                if (h != EMPTY64) {
+                    const uint32_t p = atomicAdd(&s_n, 1u);
+                    out_key[lo + p] = inv_mix64(h);
+                    out_cnt[lo + p] = s_cnt[i];
+                }
+            }
+            __syncthreads();
+        }
+        if (t == 0) {
+            if (COUNTS) ngroups[f] = s_n;
+            if (s_n) atomicAdd((unsigned long long *)&stats[4 + (f & 63)], (unsigned long long)s_n);
+            if (s_special) atomicAdd((unsigned long long *)&stats[1], (unsigned long long)s_special);
+            if (s_full) atomicOr((unsigned long long *)&stats[3], 1ull);
+        }
+        __syncthreads();
+    }
+}
+
+// Byte keys, in rounds of DT * 4 records held in registers:
+//   1. claim a slot per distinct hash (CAS on h)        2. the claimant writes
+//   its record into the slot    3. everyone compares bytes and counts.
+// Different strings with equal 64-bit hashes raise stats[2] (the caller then
+// recounts the column on the exact global-table path).
+constexpr int D_RPT = 4;
+__global__ void __launch_bounds__(DT) part_dedup_bytes_kernel(const uint64_t *in_k0, const uint64_t *in_k1,
+                                                              const uint64_t *in_meta, const uint64_t *starts,
+                                                              int64_t nbuckets, sdp_bytes_column col,
+                                                              uint64_t *out_key, uint64_t *out_cnt,
+                                                              uint32_t *ngroups, uint64_t *stats) {
+    __shared__ uint64_t s_h[D_B];
+    __shared__ uint64_t s_k0[D_B];
+    __shared__ uint64_t s_k1[D_B];
+    __shared__ uint64_t s_meta[D_B];
+    __shared__ uint32_t s_cnt[D_B];
+    __shared__ uint32_t s_n, s_full, s_coll;
+    const int t = threadIdx.x;
+    for (int64_t f = blockIdx.x; f < nbuckets; f += gridDim.x) {
+        const int64_t lo = starts[f], hi = starts[f + 1];
+        if (lo == hi) {
+            if (t == 0) ngroups[f] = 0;
+            continue;
+        }
+        for (int i = t; i < D_B; i += DT) {
+            s_h[i] = EMPTY64;
+            s_cnt[i] = 0;
+        }
+        if (t == 0) { s_n = 0; s_full = 0; s_coll = 0; }
+        __syncthreads();
+        for (int64_t rb = lo; rb < hi; rb += (int64_t)DT * D_RPT) {
+            uint64_t k0[D_RPT], k1[D_RPT], meta[D_RPT], h[D_RPT];
+            int pos[D_RPT];
+            bool mine[D_RPT];
+#pragma unroll
+            for (int q = 0; q < D_RPT; ++q) {
+                const int64_t r = rb + (int64_t)q * DT + t;
+                pos[q] = -1;
+                mine[q] = false;
+                if (r < hi) {
+                    k0[q] = in_k0[r];
+                    k1[q] = in_k1[r];
+                    meta[q] = in_meta[r];
+                    h[q] = rec_hash(k0[q], k1[q], meta[q]);
+                }
+            }
+#pragma unroll
+            for (int q = 0; q < D_RPT; ++q) {
+                const int64_t r = rb + (int64_t)q * DT + t;
+                if (r >= hi) continue;
+                // EMPTY64 is the empty marker: remap that one hash value
+                const uint64_t hk = h[q] == EMPTY64 ? 0xFFFFFFFFFFFFFFFEull : h[q];
+                h[q] = hk;
+                uint32_t p = (uint32_t)hk & (D_B - 1);
+                for (int probe = 0; probe < D_B; ++probe) {
+                    uint64_t cur = s_h[p];
+                    if (cur == EMPTY64) {
+                        cur = atomicCAS((unsigned long long *)&s_h[p], (unsigned long long)EMPTY64,
+                                        (unsigned long long)hk);
+                        if (cur == EMPTY64) { pos[q] = (int)p; mine[q] = true; break; }
+                    }
+                    if (cur == hk) { pos[q] = (int)p; break; }
+                    p = (p + 1) & (D_B - 1);
+                }
+                if (pos[q] < 0) s_full = 1;
+            }
+            __syncthreads();
+#pragma unroll
+            for (int q = 0; q < D_RPT; ++q)
+                if (mine[q]) {
+                    s_k0[pos[q]] = k0[q];
+                    s_k1[pos[q]] = k1[q];
+                    s_meta[pos[q]] = meta[q];
+                }
+            __syncthreads();
+#pragma unroll
+            for (int q = 0; q < D_RPT; ++q) {
+                if (pos[q] < 0) continue;
+                const int p = pos[q];
+                bool eq;
+                if (mine[q]) {
+                    eq = true;
+                } else {
+                    const uint64_t om = s_meta[p];
+                    eq = (om >> 40) == (meta[q] >> 40) && s_k0[p] == k0[q] && s_k1[p] == k1[q];
+                    if (eq && (meta[q] >> 40) > SHORT_MAX)
+                        eq = rows_equal_global(col, (int64_t)(om & RMASK40) - 1, (int64_t)(meta[q] & RMASK40) - 1);
+                }
+                if (eq) atomicAdd(&s_cnt[p], 1u);
+                else s_coll = 1;
+            }
+            __syncthreads();
+        }
+        for (int i = t; i < D_B; i += DT) {
+            const uint64_t hk = s_h[i];
+            if (hk != EMPTY64) {
+                const uint32_t p = atomicAdd(&s_n, 1u);
+                out_key[lo + p] = ((hk >> 40) << 40) | (s_meta[i] & RMASK40);
+                out_cnt[lo + p] = s_cnt[i];
+            }
+        }
+        __syncthreads();
+        if (t == 0) {
+            ngroups[f] = s_n;
+            if (s_n) atomicAdd((unsigned long long *)&stats[4 + (f & 63)], (unsigned long long)s_n);
+            if (s_full) atomicOr((unsigned long long *)&stats[3], 1ull);
+            if (s_coll) atomicOr((unsigned long long *)&stats[2], 1ull);
+        }
+        __syncthreads();
+    }
+}
+
+// groups of bucket f: src[starts[f] .. +ngroups[f]) -> dst[out_off[f] ..)
+__global__ void __launch_bounds__(PT) part_compact_kernel(const uint64_t *src_a, const uint64_t *src_b,
+                                                          const uint64_t *starts, const uint32_t *ngroups,
+                                                          const uint64_t *out_off, int64_t nbuckets,
+                                                          uint64_t *dst_a, uint64_t *dst_b) {
+    for (int64_t f = blockIdx.x; f < nbuckets; f += gridDim.x) {
+        const int64_t lo = starts[f], o = out_off[f];
+        const uint32_t m = ngroups[f];
+        for (uint32_t i = threadIdx.x; i < m; i += PT) {
+            dst_a[o + i] = src_a[lo + i];
+            if (src_b) dst_b[o + i] = src_b[lo + i];
+        }
+    }
+}
+
+// ---- sample (heavy-key detection) ------------------------------------------------
+__global__ void part_sample_u64_kernel(sdp_column col, int32_t ns, uint64_t *out_h) {
+    const int j = blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= ns) return;
+    const int64_t n = col.length;
+    const int64_t i = (int64_t)(((double)j + 0.5) * (double)n / (double)ns);
+    uint64_t h = EMPTY64;
+    if (i < n) {
+        bool ok;
+        const uint64_t k = fetch_key(col, i, ok);
+        if (ok) h = mix64(k);
+    }
+    out_h[j] = h;
+}
+__global__ void part_sample_bytes_kernel(sdp_bytes_column col, int32_t ns, uint64_t *out_h, uint64_t *out_k0,
+                                         uint64_t *out_k1, uint64_t *out_meta) {
+    const int j = blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= ns) return;
+    const int64_t n = col.length;
+    const int64_t i = (int64_t)(((double)j + 0.5) * (double)n / (double)ns);
+    uint64_t h = EMPTY64, k0 = 0, k1 = 0, meta = 0;
+    if (i < n && valid_bit(col.d_validity, col.validity_bit_offset, i)) {
+        const int64_t o0 = str_off(col, i), len = str_off(col, i + 1) - o0;
+        if (len <= SHORT_MAX) {
+            k0 = gload8(col.d_data + o0, len);
+            k1 = gload8(col.d_data + o0 + 8, len - 8);
+            h = bh_short(k0, k1, (uint64_t)len);
+        } else {
+            h = hash_long_global(col.d_data + o0, len);
+            k0 = h;
+        }
+        meta = ((uint64_t)min((int64_t)LEN_MAX, len) << 40) | (uint64_t)(i + 1);
+    }
+    out_h[j] = h;
+    out_k0[j] = k0;
+    out_k1[j] = k1;
+    out_meta[j] = meta;
+}
+
+// ---- exclusive scan of u32 counts into u64 offsets (n + 1 entries) ---------------
+constexpr int SCAN_T = 256;
+constexpr int SCAN_PER = 16;
+constexpr int SCAN_B = SCAN_T * SCAN_PER;   // 4096 entries per block
+
+__device__ uint64_t block_scan_u64(uint64_t v, uint64_t *s_w, uint64_t &total) {
+    // exclusive scan of one value per thread (SCAN_T threads)
+    uint64_t x = v;
+    const int lane = lane_id();
+#pragma unroll
+    for (int o = 1; o < WAVE; o <<= 1) {
+        const uint64_t y = __shfl_up(x, o, WAVE);
+        if (lane >= o) x += y;
+    }
+    const int w = threadIdx.x / WAVE;
+    if (lane == WAVE - 1) s_w[w] = x;
+    __syncthreads();
+    uint64_t wb = 0, tot = 0;
+    for (int k = 0; k < SCAN_T / WAVE; ++k) {
+        if (k < w) wb += s_w[k];
+        tot += s_w[k];
+    }
+    __syncthreads();
+    total = tot;
+    return wb + x - v;
+}
+
+__global__ void __launch_bounds__(SCAN_T) scan_reduce_kernel(const uint32_t *in, int64_t n, uint64_t *part) {
+    __shared__ uint64_t s_w[SCAN_T / WAVE];
+    const int64_t b0 = (int64_t)blockIdx.x * SCAN_B;
+    uint64_t sum = 0;
+    for (int k = 0; k < SCAN_PER; ++k) {
+        const int64_t i = b0 + (int64_t)k * SCAN_T + threadIdx.x;
+        if (i < n) sum += in[i];
+    }
+    uint64_t total;
+    block_scan_u64(sum, s_w, total);
+    if (threadIdx.x == 0) part[blockIdx.x] = total;
+}
+__global__ void __launch_bounds__(SCAN_T) scan_partials_kernel(uint64_t *part, int64_t nparts) {
+    __shared__ uint64_t s_w[SCAN_T / WAVE];
+    uint64_t carry = 0;
+    for (int64_t c0 = 0; c0 < nparts; c0 += SCAN_T) {
+        const int64_t i = c0 + threadIdx.x;
+        const uint64_t v = i < nparts ? part[i] : 0;
+        uint64_t total;
+        const uint64_t ex = block_scan_u64(v, s_w, total);
+        if (i < nparts) part[i] = carry + ex;
+        carry += total;
+    }
+    if (threadIdx.x == 0) part[nparts] = carry;
+}
+__global__ void __launch_bounds__(SCAN_T) scan_apply_kernel(const uint32_t *in, int64_t n, const uint64_t *part,
+                                                            uint64_t *out, int64_t nparts) {
+    __shared__ uint64_t s_w[SCAN_T / WAVE];
+    const int64_t b0 = (int64_t)blockIdx.x * SCAN_B;
+    // thread t owns entries [b0 + t*SCAN_PER, +SCAN_PER) (contiguous)
+    uint32_t v[SCAN_PER];
+    uint64_t sum = 0;
+#pragma unroll
+    for (int k = 0; k < SCAN_PER; ++k) {
+        const int64_t i = b0 + (int64_t)threadIdx.x * SCAN_PER + k;
+        v[k] = i < n ? in[i] : 0u;
+        sum += v[k];
+    }
+    uint64_t total;
+    uint64_t run = part[blockIdx.x] + block_scan_u64(sum, s_w, total);
+#pragma unroll
+    for (int k = 0; k < SCAN_PER; ++k) {
+        const int64_t i = b0 + (int64_t)threadIdx.x * SCAN_PER + k;
+        if (i < n) out[i] = run;
+        run += v[k];
+    }
+    if (blockIdx.x == 0 && threadIdx.x == 0) out[n] = part[nparts];
+}
+
+static int grid_of(int64_t items, int64_t cap) {
+    if (items < 1) return 1;
+    return (int)(items < cap ? items : cap);
+}
+
+template <typename T>
+static void launch_rows_u64(int phase, int grid, hipStream_t s, const sdp_column &c, HeavyArg hv, int b1, int64_t rpb,
+                            uint32_t *hist, const uint64_t *offs, uint64_t *out, uint64_t *hc, uint64_t *st) {
+    if (phase == 0)
+        hipLaunchKernelGGL((part_rows_u64_kernel<T, false>), dim3(grid), dim3(PT), 0, s, c, hv, b1, rpb, hist, offs,
+                           out, hc, st);
+    else
+        hipLaunchKernelGGL((part_rows_u64_kernel<T, true>), dim3(grid), dim3(PT), 0, s, c, hv, b1, rpb, hist, offs, out,
+                           hc, st);
+}
+
+}  // namespace sdp
+
+using namespace sdp;
+
+extern "C" {
+
+int64_t sdp_part_rows_per_block(int64_t length, int32_t is_bytes) {
+    const int64_t tile = is_bytes ? B_TILE : U_TILE;
+    const int64_t tiles = (length + tile - 1) / tile;
+    const int64_t blocks = tiles < 1 ? 1 : (tiles < SDP_PART_MAX_GRID ? tiles : SDP_PART_MAX_GRID);
+    return ((tiles + blocks - 1) / blocks) * tile;
+}
+
+int sdp_part_sample(const sdp_column *col, const sdp_bytes_column *bcol, int32_t n_sample, uint64_t *d_h,
+                    const sdp_records *d_out, void *stream) {
+    if ((col == nullptr) == (bcol == nullptr) || n_sample < 1) return set_error(SDP_EINVAL, "part_sample: args");
+    const int blocks = (n_sample + 255) / 256;
+    hipStream_t s = (hipStream_t)stream;
+    if (col) {
+        hipLaunchKernelGGL(part_sample_u64_kernel, dim3(blocks), dim3(256), 0, s, *col, n_sample, d_h);
+    } else {
+        if (d_out == nullptr) return set_error(SDP_EINVAL, "part_sample: byte keys need record outputs");
+        hipLaunchKernelGGL(part_sample_bytes_kernel, dim3(blocks), dim3(256), 0, s, *bcol, n_sample, d_h, d_out->d_k0,
+                           d_out->d_k1, d_out->d_meta);
+    }
+    return check_launch("part_sample");
+}
+
+int sdp_part_rows(const sdp_column *col, const sdp_bytes_column *bcol, const sdp_heavy *heavy, int32_t b1,
+                  int32_t phase, uint32_t *d_hist, const uint64_t *d_offsets, const sdp_records *d_out,
+                  uint64_t *d_heavy_counts, uint64_t *d_stats, void *stream) {
+    if ((col == nullptr) == (bcol == nullptr) || b1 < 0 || b1 > 10 || (phase != 0 && phase != 1))
+        return set_error(SDP_EINVAL, "part_rows: args");
+    if (phase == 0 && d_hist == nullptr) return set_error(SDP_EINVAL, "part_rows: phase 0 needs d_hist");
+    if (phase == 1 && (d_offsets == nullptr || d_out == nullptr || d_out->d_k0 == nullptr))
+        return set_error(SDP_EINVAL, "part_rows: phase 1 needs offsets and outputs");
+    HeavyArg hv{nullptr, nullptr, nullptr, nullptr, 0};
+    if (heavy && heavy->n > 0) {
+        if (heavy->n > HEAVY_MAX) return set_error(SDP_EINVAL, "part_rows: %d heavy keys > %d", heavy->n, HEAVY_MAX);
+        hv = HeavyArg{heavy->d_h, heavy->d_k0, heavy->d_k1, heavy->d_meta, heavy->n};
+        if (bcol && (hv.k0 == nullptr || hv.k1 == nullptr || hv.meta == nullptr))
+            return set_error(SDP_EINVAL, "part_rows: byte heavy keys need k0/k1/meta");
+    }
+    if (phase == 0 && hv.n > 0 && d_heavy_counts == nullptr)
+        return set_error(SDP_EINVAL, "part_rows: heavy keys need d_heavy_counts");
+    const int64_t n = col ? col->length : bcol->length;
+    const int64_t rpb = sdp_part_rows_per_block(n, bcol != nullptr);
+    const int grid = (int)((n + rpb - 1) / rpb < 1 ? 1 : (n + rpb - 1) / rpb);
+    hipStream_t s = (hipStream_t)stream;
+    if (bcol) {
+        if (bcol->length >= (int64_t)RMASK40) return set_error(SDP_EINVAL, "part_rows: more than 2^40 rows");
+        if (phase == 0)
+            hipLaunchKernelGGL((part_rows_bytes_kernel<false>), dim3(grid), dim3(PT), 0, s, *bcol, hv, b1, rpb, d_hist,
+                               d_offsets, nullptr, nullptr, nullptr, d_heavy_counts, d_stats);
+        else
+            hipLaunchKernelGGL((part_rows_bytes_kernel<true>), dim3(grid), dim3(PT), 0, s, *bcol, hv, b1, rpb, d_hist,
+                               d_offsets, d_out->d_k0, d_out->d_k1, d_out->d_meta, d_heavy_counts, d_stats);
+        return check_launch("part_rows_bytes_kernel");
+    }
+    uint64_t *out = phase ? d_out->d_k0 : nullptr;
+    const sdp_column &c = *col;
+    if (c.dtype != SDP_BOOL && !aligned16(c.d_values)) return set_error(SDP_EALIGN, "part_rows: values not 16-byte aligned");
+    switch (c.dtype) {
+    case SDP_F64: launch_rows_u64<double>(phase, grid, s, c, hv, b1, rpb, d_hist, d_offsets, out, d_heavy_counts, d_stats); break;
+    case SDP_F32: launch_rows_u64<float>(phase, grid, s, c, hv, b1, rpb, d_hist, d_offsets, out, d_heavy_counts, d_stats); break;
+    case SDP_I64: launch_rows_u64<int64_t>(phase, grid, s, c, hv, b1, rpb, d_hist, d_offsets, out, d_heavy_counts, d_stats); break;
+    case SDP_I32: launch_rows_u64<int32_t>(phase, grid, s, c, hv, b1, rpb, d_hist, d_offsets, out, d_heavy_counts, d_stats); break;
+    case SDP_I16: launch_rows_u64<int16_t>(phase, grid, s, c, hv, b1, rpb, d_hist, d_offsets, out, d_heavy_counts, d_stats); break;
+    case SDP_I8: launch_rows_u64<int8_t>(phase, grid, s, c, hv, b1, rpb, d_hist, d_offsets, out, d_heavy_counts, d_stats); break;
+    case SDP_U64: launch_rows_u64<uint64_t>(phase, grid, s, c, hv, b1, rpb, d_hist, d_offsets, out, d_heavy_counts, d_stats); break;
+    case SDP_U32: launch_rows_u64<uint32_t>(phase, grid, s, c, hv, b1, rpb, d_hist, d_offsets, out, d_heavy_counts, d_stats); break;
+    case SDP_U16: launch_rows_u64<uint16_t>(phase, grid, s, c, hv, b1, rpb, d_hist, d_offsets, out, d_heavy_counts, d_stats); break;
+    case SDP_U8: launch_rows_u64<uint8_t>(phase, grid, s, c, hv, b1, rpb, d_hist, d_offsets, out, d_heavy_counts, d_stats); break;
+    case SDP_BOOL: launch_rows_u64<bool>(phase, grid, s, c, hv, b1, rpb, d_hist, d_offsets, out, d_heavy_counts, d_stats); break;
+    default: return set_error(SDP_EINVAL, "part_rows: dtype %d", c.dtype);
+    }
+    return check_launch("part_rows_u64_kernel");
+}
+
+int sdp_part_recs(const sdp_records *in, int32_t is_bytes, const sdp_chunk *d_chunks, int64_t nchunks, int32_t b1,
+                  int32_t b2, int32_t phase, uint32_t *d_hist, const uint64_t *d_offsets, const sdp_records *out,
+                  void *stream) {
+    if (in == nullptr || d_chunks == nullptr || nchunks < 1 || b2 < 1 || b2 > 10 || b1 < 0 || b1 + b2 > 63 ||
+        (phase != 0 && phase != 1))
+        return set_error(SDP_EINVAL, "part_recs: args");
+    if (phase == 1 && (out == nullptr || d_offsets == nullptr)) return set_error(SDP_EINVAL, "part_recs: outputs");
+    const int grid = grid_of(nchunks, 8192);
+    hipStream_t s = (hipStream_t)stream;
+    const Chunk *ch = (const Chunk *)d_chunks;
+    uint64_t *o0 = out ? out->d_k0 : nullptr, *o1 = out ? out->d_k1 : nullptr, *o2 = out ? out->d_meta : nullptr;
+    if (is_bytes) {
+        if (phase == 0)
+            hipLaunchKernelGGL((part_recs_kernel<true, false>), dim3(grid), dim3(PT), 0, s, in->d_k0, in->d_k1,
+                               in->d_meta, ch, nchunks, b1, b2, d_hist, d_offsets, o0, o1, o2);
+        else
+            hipLaunchKernelGGL((part_recs_kernel<true, true>), dim3(grid), dim3(PT), 0, s, in->d_k0, in->d_k1,
+                               in->d_meta, ch, nchunks, b1, b2, d_hist, d_offsets, o0, o1, o2);
+    } else {
+        if (phase == 0)
+            hipLaunchKernelGGL((part_recs_kernel<false, false>), dim3(grid), dim3(PT), 0, s, in->d_k0, nullptr,
+                               nullptr, ch, nchunks, b1, b2, d_hist, d_offsets, o0, nullptr, nullptr);
+        else
+            hipLaunchKernelGGL((part_recs_kernel<false, true>), dim3(grid), dim3(PT), 0, s, in->d_k0, nullptr, nullptr,
+                               ch, nchunks, b1, b2, d_hist, d_offsets, o0, nullptr, nullptr);
+    }
+    return check_launch("part_recs_kernel");
+}
+
+int64_t sdp_part_bucket_target(int32_t is_bytes, int32_t with_counts) {
+    return is_bytes ? D_B / 2 : (with_counts ? D_U64C / 2 : D_U64 / 2);
+}
+
+int sdp_part_dedup(const sdp_records *in, int32_t is_bytes, const sdp_bytes_column *bcol, const uint64_t *d_starts,
+                   int64_t nbuckets, int32_t with_counts, uint64_t *d_out_key, uint64_t *d_out_cnt,
+                   uint32_t *d_ngroups, uint64_t *d_stats, void *stream) {
+    if (in == nullptr || d_starts == nullptr || nbuckets < 1 || d_stats == nullptr)
+        return set_error(SDP_EINVAL, "part_dedup: args");
+    if ((with_counts || is_bytes) && (d_out_key == nullptr || d_out_cnt == nullptr || d_ngroups == nullptr))
+        return set_error(SDP_EINVAL, "part_dedup: group outputs");
+    const int grid = grid_of(nbuckets, 256 * 8);
+    hipStream_t s = (hipStream_t)stream;
+    if (is_bytes) {
+        if (bcol == nullptr) return set_error(SDP_EINVAL, "part_dedup: byte keys need the column");
+        hipLaunchKernelGGL(part_dedup_bytes_kernel, dim3(grid), dim3(DT), 0, s, in->d_k0, in->d_k1, in->d_meta,
+                           d_starts, nbuckets, *bcol, d_out_key, d_out_cnt, d_ngroups, d_stats);
+    } else if (with_counts) {
+        hipLaunchKernelGGL(part_dedup_u64_kernel<true>, dim3(grid), dim3(DT), 0, s, in->d_k0, d_starts, nbuckets,
+                           d_out_key, d_out_cnt, d_ngroups, d_stats);
+    } else {
+        hipLaunchKernelGGL(part_dedup_u64_kernel<false>, dim3(grid), dim3(DT), 0, s, in->d_k0, d_starts, nbuckets,
+                           nullptr, nullptr, nullptr, d_stats);
+    }
+    return check_launch("part_dedup");
+}
+
+int sdp_part_compact(const uint64_t *d_src_a, const uint64_t *d_src_b, const uint64_t *d_starts,
+                     const uint32_t *d_ngroups, const uint64_t *d_out_offsets, int64_t nbuckets, uint64_t *d_dst_a,
+                     uint64_t *d_dst_b, void *stream) {
+    if (d_src_a == nullptr || d_dst_a == nullptr || nbuckets < 1 || (d_src_b != nullptr) != (d_dst_b != nullptr))
+        return set_error(SDP_EINVAL, "part_compact: args");
+    hipLaunchKernelGGL(part_compact_kernel, dim3(grid_of(nbuckets, 8192)), dim3(PT), 0, (hipStream_t)stream, d_src_a,
+                       d_src_b, d_starts, d_ngroups, d_out_offsets, nbuckets, d_dst_a, d_dst_b);
+    return check_launch("part_compact_kernel");
+}
+
+int64_t sdp_scan_workspace_bytes(int64_t n) {
+    return (int64_t)(((n + SCAN_B - 1) / SCAN_B) + 1) * 8;
+}
+
+int sdp_scan_u32(const uint32_t *d_in, int64_t n, uint64_t *d_out, void *d_work, int64_t work_bytes, void *stream) {
+    if (d_in == nullptr || d_out == nullptr || n < 1) return set_error(SDP_EINVAL, "scan_u32: args");
+    if (work_bytes < sdp_scan_workspace_bytes(n)) return set_error(SDP_ECAP, "scan_u32: workspace too small");
+    const int64_t nparts = (n + SCAN_B - 1) / SCAN_B;
+    if (nparts > 0x7FFFFFFF) return set_error(SDP_EINVAL, "scan_u32: too long");
+    uint64_t *part = (uint64_t *)d_work;
+    hipStream_t s = (hipStream_t)stream;
+    hipLaunchKernelGGL(scan_reduce_kernel, dim3((unsigned)nparts), dim3(SCAN_T), 0, s, d_in, n, part);
+    hipLaunchKernelGGL(scan_partials_kernel, dim3(1), dim3(SCAN_T), 0, s, part, nparts);
+    hipLaunchKernelGGL(scan_apply_kernel, dim3((unsigned)nparts), dim3(SCAN_T), 0, s, d_in, n, part, d_out, nparts);
+    return check_launch("scan_u32");
+}
+
+}  // extern "C"

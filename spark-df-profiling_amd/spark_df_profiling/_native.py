@@ -21,6 +21,8 @@ LIB_PATH = os.environ.get('SDP_LIBRARY', os.path.join(_HERE, 'lib', 'libsdp.so')
 
 MAX_WINDOWS = 5
 PASS1_WAVES = 4          # SDP_PASS1_WAVES
+PART_MAX_GRID = 1024     # SDP_PART_MAX_GRID
+HEAVY_MAX = 256
 
 # enum sdp_dtype
 I8, I16, I32, I64, F32, F64, U8, U16, U32, U64, BOOL = 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11
@@ -44,9 +46,18 @@ class SdpBytesColumn(ctypes.Structure):
                 ('offset_width', ctypes.c_int32), ('fixed_width', ctypes.c_int32)]
 
 
-class SdpBuckets(ctypes.Structure):
-    _fields_ = [('d_key', ctypes.c_void_p), ('d_row', ctypes.c_void_p), ('d_cnt', ctypes.c_void_p),
-                ('d_fill', ctypes.c_void_p), ('capacity', ctypes.c_int64)]
+class SdpRecords(ctypes.Structure):
+    _fields_ = [('d_k0', ctypes.c_void_p), ('d_k1', ctypes.c_void_p), ('d_meta', ctypes.c_void_p)]
+
+
+class SdpHeavy(ctypes.Structure):
+    _fields_ = [('d_h', ctypes.c_void_p), ('d_k0', ctypes.c_void_p), ('d_k1', ctypes.c_void_p),
+                ('d_meta', ctypes.c_void_p), ('n', ctypes.c_int32), ('_pad', ctypes.c_int32)]
+
+
+class SdpChunk(ctypes.Structure):
+    _fields_ = [('start', ctypes.c_int64), ('end', ctypes.c_int64), ('hbase', ctypes.c_int64),
+                ('hstride', ctypes.c_int64)]
 
 
 class SdpQPlan(ctypes.Structure):
@@ -79,7 +90,8 @@ _U64 = ctypes.c_uint64
 _D = ctypes.c_double
 _COL = ctypes.POINTER(SdpColumn)
 _BCOL = ctypes.POINTER(SdpBytesColumn)
-_BKT = ctypes.POINTER(SdpBuckets)
+_REC = ctypes.POINTER(SdpRecords)
+_HVY = ctypes.POINTER(SdpHeavy)
 
 # name -> (restype, argtypes); every status-returning entry is checked
 _SIGNATURES = {
@@ -108,17 +120,23 @@ _SIGNATURES = {
     'sdp_select_by_value': (ctypes.c_int, [_P, _P, _P, _U64, _U64, _P, _P, _P, _P]),
     'sdp_count_valid': (ctypes.c_int, [_P, _I64, _I64, _P, _P]),
     'sdp_first_valid': (ctypes.c_int, [_COL, _I32, _P, _P, _P]),
-    'sdp_group_part_rows_u64': (ctypes.c_int, [_COL, _I32, _I32, _BKT, _P, _P]),
-    'sdp_group_part_rows_bytes': (ctypes.c_int, [_BCOL, _I32, _BKT, _P, _P]),
-    'sdp_group_part_recs': (ctypes.c_int, [_BKT, _I32, _BKT, _I32, _I32, _BCOL, _I32, _P, _P]),
-    'sdp_group_dedup': (ctypes.c_int, [_BKT, _I64, _BCOL, _I32, _P, _P, _P]),
+    'sdp_part_rows_per_block': (_I64, [_I64, _I32]),
+    'sdp_part_bucket_target': (_I64, [_I32, _I32]),
+    'sdp_part_sample': (ctypes.c_int, [_COL, _BCOL, _I32, _P, _REC, _P]),
+    'sdp_part_rows': (ctypes.c_int, [_COL, _BCOL, _HVY, _I32, _I32, _P, _P, _REC, _P, _P, _P]),
+    'sdp_part_recs': (ctypes.c_int, [_REC, _I32, _P, _I64, _I32, _I32, _I32, _P, _P, _REC, _P]),
+    'sdp_part_dedup': (ctypes.c_int, [_REC, _I32, _BCOL, _P, _I64, _I32, _P, _P, _P, _P, _P]),
+    'sdp_part_compact': (ctypes.c_int, [_P, _P, _P, _P, _P, _I64, _P, _P, _P]),
+    'sdp_scan_workspace_bytes': (_I64, [_I64]),
+    'sdp_scan_u32': (ctypes.c_int, [_P, _I64, _P, _P, _I64, _P]),
     'sdp_rowmask': (ctypes.c_int, [_COL, ctypes.POINTER(_I32), _I32, _P, _I64, _P, _P]),
     'sdp_gram_workspace_bytes': (_I64, [_I64, _I32]),
     'sdp_gram': (ctypes.c_int, [_COL, _I32, _P, _P, _P, _I64, _P, _P, _P, _P]),
 }
 
 _VALUE_FUNCS = {'sdp_last_error', 'sdp_version', 'sdp_pass1_workspace_bytes', 'sdp_pass2_workspace_bytes',
-                'sdp_pass1_grid', 'sdp_gram_workspace_bytes'}
+                'sdp_pass1_grid', 'sdp_gram_workspace_bytes', 'sdp_part_rows_per_block', 'sdp_part_bucket_target',
+                'sdp_scan_workspace_bytes'}
 _STATUS_FUNCS = set(_SIGNATURES) - _VALUE_FUNCS
 
 _lib = None

@@ -41,10 +41,24 @@ GSORT_MAX = 8192
 TOPK = 50                                       # describe.py:259
 EMPTY64 = 0xFFFFFFFFFFFFFFFF
 U64 = (1 << 64) - 1
+PART_SAMPLE = 16384          # rows sampled for heavy keys (sdp_part_sample)
+HEAVY_MIN = 3                # sample occurrences that make a key heavy
+PART_CHUNK = 65536           # level-2 records per workgroup chunk
 
 
 def _u(x):
     return int(x) & U64
+
+
+def inv_mix64(x):
+    """Inverse of mix64 (sdp_common.h), so a fixed key is recovered from its record."""
+    M = U64
+    x ^= (x >> 31) ^ (x >> 62)
+    x = (x * 0x319642B2D24D8EC3) & M
+    x ^= (x >> 27) ^ (x >> 54)
+    x = (x * 0x96DE1B173F119089) & M
+    x ^= (x >> 30) ^ (x >> 60)
+    return x
 
 
 def _next_pow2(x):
@@ -382,73 +396,168 @@ class Engine:
         sdp.sdp_table_clear(ptr(slots), ptr(counts), capacity, int(bytes_keys), self._s())
         return slots, counts
 
-    # -- radix-partitioned grouping (sdp_group.hip) ------------------------------
-    def _alloc_buckets(self, nb, cap, isb, with_counts):
-        b = nat.SdpBuckets()
-        keep = {'key': self._u64(nb * cap)}
-        keep['row'] = self._u64(nb * cap) if isb else None
-        keep['cnt'] = self._u64(nb * cap) if with_counts else None
-        keep['fill'] = torch.zeros(nb, dtype=torch.int32, device=self.device)
-        b.d_key = keep['key'].data_ptr()
-        b.d_row = keep['row'].data_ptr() if isb else None
-        b.d_cnt = keep['cnt'].data_ptr() if with_counts else None
-        b.d_fill = keep['fill'].data_ptr()
-        b.capacity = cap
-        return b, keep
+    # -- two-level hash partitioning (sdp_part.hip) ------------------------------
+    def _records(self, n, isb):
+        keep = [self._u64(max(n, 1))]
+        if isb:
+            keep += [self._u64(max(n, 1)), self._u64(max(n, 1))]
+        r = nat.SdpRecords(keep[0].data_ptr(), keep[1].data_ptr() if isb else None,
+                           keep[2].data_ptr() if isb else None)
+        return r, keep
+
+    def _heavy_keys(self, col, isb):
+        """Keys seen >= HEAVY_MIN times in an evenly spaced sample: counted
+        outside the partitions (describe.py:251's hot groups)."""
+        ns = min(PART_SAMPLE, col.length)
+        s = self._s()
+        h = self._u64(ns)
+        if isb:
+            rec, keep = self._records(ns, True)
+            sdp.sdp_part_sample(None, ctypes.byref(col.sdp_bytes()), ns, ptr(h), ctypes.byref(rec), s)
+        else:
+            keep = None
+            sdp.sdp_part_sample(ctypes.byref(col.sdp()), None, ns, ptr(h), None, s)
+        hn = h.cpu().numpy().view(np.uint64)
+        pos = np.nonzero(hn != np.uint64(U64))[0]
+        if isb and pos.size:
+            meta = keep[2].cpu().numpy().view(np.uint64)
+            pos = pos[(meta[pos] >> np.uint64(40)) <= np.uint64(16)]
+        if pos.size == 0:
+            return None
+        u, first, cnt = np.unique(hn[pos], return_index=True, return_counts=True)
+        sel = np.nonzero(cnt >= HEAVY_MIN)[0]
+        if sel.size == 0:
+            return None
+        if sel.size > nat.HEAVY_MAX:
+            sel = sel[np.argsort(-cnt[sel], kind='stable')[:nat.HEAVY_MAX]]
+        rows = pos[first[sel]]
+        hv = {'h': torch.from_numpy(u[sel].view(np.int64).copy()).to(self.device), 'n': int(sel.size)}
+        if isb:
+            idx = torch.from_numpy(rows.astype(np.int64)).to(self.device)
+            hv['k0'], hv['k1'], hv['meta'] = keep[0][idx].contiguous(), keep[1][idx].contiguous(), \
+                keep[2][idx].contiguous()
+        st = nat.SdpHeavy(hv['h'].data_ptr(), hv['k0'].data_ptr() if isb else None,
+                          hv['k1'].data_ptr() if isb else None, hv['meta'].data_ptr() if isb else None, hv['n'], 0)
+        hv['struct'] = st
+        return hv
 
     def group(self, col, with_counts, dense=True):
-        """Exact groups of a column by radix-partitioned LDS aggregation.
-        Returns a tab dict; `dense` adds compacted (key, count) group arrays.
-        Falls back to the global hash table if a bucket overflows."""
+        """Exact groups of a column by two-level hash partitioning with exact
+        offsets (sdp_part.hip).  Returns a tab dict (dense (key, count) group
+        arrays when counts are needed), or None when the column needs the exact
+        global-table path (64-bit hash collision between different strings, or
+        a final bucket larger than its LDS table)."""
         isb = col.kind == 'bytes'
         with_counts = with_counts or isb
-        n = max(col.length, 1)
-        total_bits = max(0, math.ceil(math.log2(max(1.0, n / 2048.0))))
-        b1 = min(9, total_bits)
+        n = col.length
+        target = sdp.sdp_part_bucket_target(int(isb), int(with_counts))
+        total_bits = max(0, math.ceil(math.log2(max(1.0, n / target))))
+        b1 = min(10, (total_bits + 1) // 2)
         b2 = total_bits - b1
-        nb1 = 1 << b1
-        cap1 = -(-115 * n // (100 * nb1)) + 2 * (-(-n // 2048)) + 4096
-        stats = self._u64(68, zero=True)
+        if b2 > 10:
+            return None
+        nb1, nb2 = 1 << b1, 1 << b2
         s = self._s()
-        bk1, keep1 = self._alloc_buckets(nb1, cap1, isb, with_counts)
+        stats = self._u64(68, zero=True)
+        cs = None if isb else col.sdp()
         bc = col.sdp_bytes() if isb else None
-        if isb:
-            sdp.sdp_group_part_rows_bytes(ctypes.byref(bc), b1, ctypes.byref(bk1), ptr(stats), s)
+        cref = None if isb else ctypes.byref(cs)
+        bref = ctypes.byref(bc) if isb else None
+        hv = self._heavy_keys(col, isb)
+        hvref = ctypes.byref(hv['struct']) if hv else None
+        hcnt = self._u64(max(hv['n'] if hv else 1, 1), zero=True)
+        # level 1: rows -> nb1 buckets
+        rpb = sdp.sdp_part_rows_per_block(n, int(isb))
+        grid = max(1, -(-n // rpb))
+        h1 = torch.empty(nb1 * grid, dtype=torch.int32, device=self.device)
+        sdp.sdp_part_rows(cref, bref, hvref, b1, 0, ptr(h1), None, None, ptr(hcnt), ptr(stats), s)
+        o1 = self._scan(h1)
+        nrec = int(o1[-1].item())
+        r1, keep1 = self._records(nrec, isb)
+        if nrec:
+            sdp.sdp_part_rows(cref, bref, hvref, b1, 1, None, ptr(o1), ctypes.byref(r1), ptr(hcnt), ptr(stats), s)
+        # level 2: each L1 bucket -> nb2 sub-buckets, chunk by chunk
+        bstarts = o1[0:nb1 * grid:grid]
+        if b2 == 0 or nrec == 0:
+            starts = torch.cat([bstarts, o1[-1:]]) if b2 == 0 else self._u64(nb1 * nb2 + 1, zero=True)
+            rf, keepf = r1, keep1
         else:
-            cs = col.sdp()
-            sdp.sdp_group_part_rows_u64(ctypes.byref(cs), b1, int(with_counts), ctypes.byref(bk1), ptr(stats), s)
-        final, keep, nfinal, capf = bk1, keep1, nb1, cap1
-        if b2 > 0:
-            mf = min(int(keep1['fill'].max().item()), cap1)
-            nb2 = 1 << b2
-            cap2 = -(-125 * mf // (100 * nb2)) + 2 * (-(-mf // 2048)) + 512
-            bk2, keep2 = self._alloc_buckets(nb1 * nb2, cap2, isb, with_counts)
-            sdp.sdp_group_part_recs(ctypes.byref(bk1), nb1, ctypes.byref(bk2), b1, b2,
-                                    ctypes.byref(bc) if isb else None, int(with_counts), ptr(stats), s)
-            del keep1, bk1
-            final, keep, nfinal, capf = bk2, keep2, nb1 * nb2, cap2
+            bs = np.append(bstarts.cpu().numpy(), nrec).astype(np.int64)
+            sizes = np.diff(bs)
+            nch = -(-sizes // PART_CHUNK)
+            k0 = np.concatenate([[0], np.cumsum(nch)[:-1]]).astype(np.int64)
+            K = int(nch.sum())
+            bof = np.repeat(np.arange(nb1), nch)
+            j = np.arange(K, dtype=np.int64) - k0[bof]
+            ch = np.empty((K, 4), dtype=np.int64)
+            ch[:, 0] = bs[bof] + j * PART_CHUNK
+            ch[:, 1] = np.minimum(bs[bof + 1], ch[:, 0] + PART_CHUNK)
+            ch[:, 2] = nb2 * k0[bof] + j
+            ch[:, 3] = nch[bof]
+            chunks = torch.from_numpy(ch).to(self.device)
+            h2 = torch.empty(nb2 * K, dtype=torch.int32, device=self.device)
+            sdp.sdp_part_recs(ctypes.byref(r1), int(isb), ptr(chunks), K, b1, b2, 0, ptr(h2), None, None, s)
+            o2 = self._scan(h2)
+            rf, keepf = self._records(nrec, isb)
+            sdp.sdp_part_recs(ctypes.byref(r1), int(isb), ptr(chunks), K, b1, b2, 1, None, ptr(o2),
+                              ctypes.byref(rf), s)
+            del keep1, r1, h2
+            sidx = (nb2 * k0[:, None] + np.arange(nb2)[None, :] * nch[:, None]).reshape(-1)
+            sidx = np.append(sidx, nb2 * K)
+            starts = o2[torch.from_numpy(sidx).to(self.device)].contiguous()
+        nfinal = nb1 * nb2
         ngroups = torch.zeros(nfinal, dtype=torch.int32, device=self.device)
-        sdp.sdp_group_dedup(ctypes.byref(final), nfinal, ctypes.byref(bc) if isb else None, int(with_counts),
-                            ptr(ngroups), ptr(stats), s)
+        out_key = out_cnt = None
+        if with_counts:
+            out_key, out_cnt = self._u64(max(nrec, 1)), self._u64(max(nrec, 1))
+        if nrec:
+            sdp.sdp_part_dedup(ctypes.byref(rf), int(isb), bref, ptr(starts), nfinal, int(with_counts),
+                               ptr(out_key), ptr(out_cnt), ptr(ngroups), ptr(stats), s)
         st = self._host_u64(stats)
-        if st[2] or st[3]:                          # overflow: exact global-table path
+        if st[2] or st[3]:
             return None
         groups_local = sum(st[4:68])
-        tab = {'bytes': isb, 'dense': True, 'rows': st[0], 'max_key_rows': st[1], 'col': col,
-               'groups': groups_local + (1 if st[1] else 0), 'groups_local': groups_local}
-        if dense:
-            keys = self._u64(max(groups_local, 1))
-            kn = self._u64(1, zero=True)
-            offs = self._u64(nfinal)
-            sdp.sdp_compact_candidates(ptr(keep['key']), ptr(ngroups), nfinal, capf, ptr(offs), ptr(keys), ptr(kn), s)
-            counts = None
-            if with_counts:
-                counts = self._u64(max(groups_local, 1))
-                cn = self._u64(1, zero=True)
-                sdp.sdp_compact_candidates(ptr(keep['cnt']), ptr(ngroups), nfinal, capf, ptr(offs), ptr(counts),
-                                           ptr(cn), s)
-            tab.update({'slots': keys, 'counts': counts, 'capacity': max(groups_local, 1)})
+        special = st[1]
+        hc = self._host_u64(hcnt[:hv['n']]) if hv else []
+        heavy_sel = [i for i, c in enumerate(hc) if c]
+        total = groups_local + (1 if special else 0) + len(heavy_sel)
+        tab = {'bytes': isb, 'dense': True, 'rows': st[0], 'max_key_rows': 0, 'col': col,
+               'groups': total, 'groups_local': total}
+        if dense and with_counts:
+            keys = self._u64(max(total, 1))
+            counts = self._u64(max(total, 1))
+            if groups_local:
+                offs = self._scan(ngroups)
+                sdp.sdp_part_compact(ptr(out_key), ptr(out_cnt), ptr(starts), ptr(ngroups), ptr(offs), nfinal,
+                                     ptr(keys), ptr(counts), s)
+            extra_k, extra_c = [], []
+            if hv:
+                hh = self._host_u64(hv['h'])
+                meta = self._host_u64(hv['meta']) if isb else None
+                for i in heavy_sel:
+                    if isb:
+                        extra_k.append(((hh[i] >> 40) << 40) | (meta[i] & ((1 << 40) - 1)))
+                    else:
+                        extra_k.append(inv_mix64(hh[i]))
+                    extra_c.append(hc[i])
+            if special:
+                extra_k.append(inv_mix64(U64))
+                extra_c.append(special)
+            if extra_k:
+                m = len(extra_k)
+                keys[groups_local:groups_local + m] = torch.tensor(
+                    np.array(extra_k, dtype=np.uint64).view(np.int64), device=self.device)
+                counts[groups_local:groups_local + m] = torch.tensor(extra_c, dtype=torch.int64, device=self.device)
+            tab.update({'slots': keys, 'counts': counts, 'capacity': max(total, 1)})
         return tab
+
+    def _scan(self, counts_i32):
+        """Exclusive scan of int32 counts -> int64 offsets (n + 1 entries)."""
+        n = counts_i32.numel()
+        out = self._u64(n + 1)
+        work = self._bytes(sdp.sdp_scan_workspace_bytes(n))
+        sdp.sdp_scan_u32(ptr(counts_i32), n, ptr(out), ptr(work), work.numel(), self._s())
+        return out
 
     def distinct_fixed(self, col, with_counts=False, capacity_hint=None):
         """countDistinct over a fixed-width column (describe.py:143).

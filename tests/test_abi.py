@@ -22,7 +22,7 @@ def declared_functions():
 def test_header_declares_entry_points():
     names = declared_functions()
     for must in ('sdp_pass1', 'sdp_pass2', 'sdp_quantile_plan', 'sdp_hash_u64', 'sdp_hash_bytes',
-                 'sdp_group_part_rows_u64', 'sdp_group_dedup', 'sdp_gram', 'sdp_rowmask', 'sdp_first_valid',
+                 'sdp_part_rows', 'sdp_part_recs', 'sdp_part_dedup', 'sdp_scan_u32', 'sdp_gram', 'sdp_rowmask', 'sdp_first_valid',
                  'sdp_last_error'):
         assert must in names
 
@@ -49,7 +49,7 @@ def test_error_reporting_without_gpu():
 
 STRUCTS = {'sdp_column': 'SdpColumn', 'sdp_bytes_column': 'SdpBytesColumn', 'sdp_qplan': 'SdpQPlan',
            'sdp_pass1_result': 'SdpPass1Result', 'sdp_pass2_result': 'SdpPass2Result',
-           'sdp_buckets': 'SdpBuckets'}
+           'sdp_records': 'SdpRecords', 'sdp_heavy': 'SdpHeavy', 'sdp_chunk': 'SdpChunk'}
 
 
 def test_struct_layouts_match_c():
@@ -71,3 +71,14 @@ def test_struct_layouts_match_c():
         assert int(got[c]) == ctypes.sizeof(cls), c
         for f, _ in cls._fields_:
             assert int(got['%s.%s' % (c, f)]) == getattr(cls, f).offset, (c, f)
+
+
+def test_part_argument_checks_without_gpu():
+    """The partition entry points reject bad arguments before any launch."""
+    from spark_df_profiling import _native
+    with pytest.raises(_native.NativeError, match='part_rows'):
+        _native.sdp.sdp_part_rows(None, None, None, 4, 0, None, None, None, None, None, None)
+    with pytest.raises(_native.NativeError, match='scan_u32'):
+        _native.sdp.sdp_scan_u32(None, 0, None, None, 0, None)
+    assert _native.sdp.sdp_part_rows_per_block(10 ** 9, 0) % 4096 == 0
+    assert _native.sdp.sdp_part_bucket_target(1, 1) == 2048

@@ -1,0 +1,145 @@
+"""The partitioned grouping path (sdp_part.hip) vs numpy / the oracle, on
+columns large enough (>= 2^16 rows) to take it: heavy keys, skew, long and
+empty strings, nulls, NaN / -0.0, and the two u64 keys the kernels treat
+specially (UINT64_MAX, and the key whose hash is UINT64_MAX).  Needs an MI355X."""
+
+import numpy as np
+import pyarrow as pa
+import pytest
+
+import datagen
+from compare import assert_describe_equal
+
+pytestmark = pytest.mark.gpu
+
+N = 300_007
+SPECIAL = [0xFFFFFFFFFFFFFFFF, 0xCF9A04AFFA6BADC0]     # UINT64_MAX, inv_mix64(UINT64_MAX)
+
+
+def _engine_groups(arr):
+    from spark_df_profiling.columns import DeviceTable
+    from spark_df_profiling.engine import Engine
+    t = DeviceTable.from_arrow(pa.table({'c': arr}))
+    e = Engine()
+    col = t.columns[0]
+    return e, col
+
+
+def _u64_table_groups(tab):
+    import torch
+    k = tab['slots'][:tab['groups']].cpu().numpy().view(np.uint64)
+    c = tab['counts'][:tab['groups']].cpu().numpy()
+    o = np.argsort(k)
+    return k[o], c[o]
+
+
+@pytest.mark.parametrize('kind', ['uniform', 'skewed', 'special'])
+def test_group_u64_counts_exact(kind):
+    g = datagen.rng(99)
+    if kind == 'uniform':
+        v = g.integers(0, 2 ** 63, N, dtype=np.uint64)
+    elif kind == 'skewed':
+        v = np.minimum(g.zipf(1.1, N), 10 ** 7).astype(np.uint64)
+    else:
+        v = g.integers(0, 50_000, N, dtype=np.uint64)
+        v[g.random(N) < 0.2] = np.uint64(SPECIAL[0])
+        v[g.random(N) < 0.1] = np.uint64(SPECIAL[1])
+    e, col = _engine_groups(pa.array(v, type=pa.uint64()))
+    tab = e.group(col, with_counts=True)
+    assert tab is not None
+    keys, counts = _u64_table_groups(tab)
+    want_k, want_c = np.unique(v, return_counts=True)
+    assert tab['groups'] == len(want_k)
+    assert tab['rows'] == N
+    assert np.array_equal(keys, want_k)
+    assert np.array_equal(counts, want_c)
+
+
+@pytest.mark.parametrize('dtype', ['f64', 'f32', 'i32', 'i16'])
+def test_group_distinct_only(dtype):
+    g = datagen.rng(5)
+    if dtype == 'f64':
+        v = g.standard_normal(N)
+        v[g.random(N) < 0.05] = np.nan
+        v[g.random(N) < 0.05] = -0.0
+        v[g.random(N) < 0.05] = 0.0
+        v[g.random(N) < 0.3] = 2.5
+        arr, want = pa.array(v, mask=g.random(N) < 0.1), None
+    elif dtype == 'f32':
+        v = g.random(N).astype(np.float32)
+        arr = pa.array(v)
+    elif dtype == 'i32':
+        v = g.integers(-2 ** 31, 2 ** 31 - 1, N).astype(np.int32)
+        arr = pa.array(v, mask=g.random(N) < 0.05)
+    else:
+        v = g.integers(-2 ** 15, 2 ** 15, N).astype(np.int16)
+        arr = pa.array(v)
+    e, col = _engine_groups(arr)
+    tab = e.group(col, with_counts=False, dense=False)
+    assert tab is not None
+    vals = arr.to_numpy(zero_copy_only=False)
+    valid = ~np.asarray(arr.is_null().to_numpy(zero_copy_only=False))
+    x = np.asarray(vals)[valid]
+    if x.dtype.kind == 'f':
+        x = x.astype(np.float64)
+        x[x == 0] = 0.0
+        n_nan = int(np.isnan(x).any())
+        want = len(np.unique(x[~np.isnan(x)])) + n_nan
+    else:
+        want = len(np.unique(x))
+    assert tab['groups'] == want
+    assert tab['rows'] == int(valid.sum())
+
+
+def _strings():
+    g = datagen.rng(17)
+    base = ['', 'a', 'ab', 'Élysée', 'x' * 16, 'y' * 17, 'long-string-%s' % ('z' * 40)]
+    tail = ['t%07d' % i for i in range(200_000)]
+    longs = ['L%06d-%s' % (i, 'q' * (i % 30)) for i in range(5000)]
+    pick = g.random(N)
+    z = np.minimum(g.zipf(1.3, N), len(tail)) - 1
+    out = np.empty(N, dtype=object)
+    for i in range(N):
+        p = pick[i]
+        if p < 0.3:
+            out[i] = base[int(p * 100) % len(base)]
+        elif p < 0.8:
+            out[i] = tail[z[i]]
+        else:
+            out[i] = longs[int(p * 1e6) % len(longs)]
+    return out, g.random(N) < 0.05
+
+
+@pytest.mark.parametrize('atype', [pa.string(), pa.large_string(), pa.binary()])
+def test_group_bytes_counts_exact(atype):
+    vals, mask = _strings()
+    if atype == pa.binary():
+        arr = pa.array([s.encode() for s in vals], type=atype, mask=mask)
+    else:
+        arr = pa.array(vals.tolist(), type=atype, mask=mask)
+    e, col = _engine_groups(arr)
+    tab = e.group(col, with_counts=True)
+    assert tab is not None
+    m = tab['groups']
+    slots = tab['slots'][:m].cpu().numpy().view(np.uint64)
+    counts = tab['counts'][:m].cpu().numpy()
+    rows = [(int(s) & ((1 << 40) - 1)) - 1 for s in slots]
+    got_vals = e.row_bytes_values(col, rows, col)
+    got = dict(zip(got_vals, counts.tolist()))
+    assert len(got) == m                          # every group a different value
+    from collections import Counter
+    want = Counter(v for v, nul in zip(vals, mask) if not nul)
+    if atype == pa.binary():
+        want = Counter({k.encode(): c for k, c in want.items()})
+    assert got == dict(want)
+    assert tab['rows'] == int((~mask).sum())
+
+
+def test_describe_large_categorical():
+    """The categorical table above the partition threshold, through describe()."""
+    import oracle
+    from spark_df_profiling import describe
+    t = datagen.categorical_table(N, seed=21)
+    got = describe(t, plots=False)
+    want, _ = oracle.profile_raw(t)
+    assert_describe_equal(got, want)

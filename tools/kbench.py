@@ -1,0 +1,33 @@
+"""Single-kernel driver for profiling: runs one engine stage on a 1e9-row column."""
+import sys, os, time
+sys.path.insert(0, 'spark-df-profiling_amd'); sys.path.insert(0, '.')
+import torch, ctypes
+import bench
+from spark_df_profiling.engine import Engine
+from spark_df_profiling import _native as nat
+from spark_df_profiling._native import sdp, ptr
+
+what = sys.argv[1]
+rows = int(sys.argv[2]) if len(sys.argv) > 2 else 1_000_000_000
+reps = int(sys.argv[3]) if len(sys.argv) > 3 else 3
+dev = torch.device('cuda')
+t = bench.make_c3_shard(rows, 0, 1, dev)
+cols = {c.name: c for c in t.columns}
+e = Engine()
+col = cols[sys.argv[4]] if len(sys.argv) > 4 else cols['f64_norm']
+torch.cuda.synchronize()
+for r in range(reps):
+    t0 = time.perf_counter()
+    if what == 'group':
+        e.group(col, col.kind == 'bytes', dense=False)
+    elif what == 'table':
+        e._distinct_fixed_table(col) if col.kind != 'bytes' else e.value_counts_bytes_table(col)
+    elif what == 'pass1':
+        e.numeric_pass1(col)
+    elif what == 'pass2':
+        e.numeric_stats(col)
+    elif what == 'gram':
+        num = [c for c in t.columns if c.kind == 'fixed' and c.spark_type != 'date']
+        e.gram(num, [0.0] * len(num), [False] * len(num))
+    torch.cuda.synchronize()
+    print(what, col.name, 'rep', r, '%.2f ms' % ((time.perf_counter() - t0) * 1e3), flush=True)
