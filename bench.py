@@ -179,49 +179,51 @@ def table_bytes(table):
 
 
 # ----------------------------------------------------------------------------
-# algorithmic bytes per kernel launch, for the roofline object
+# roofline: per-kernel (HIP events + algorithmic bytes annotated by the engine)
+# and whole-profile (SURVEY.md §8d B_alg)
 # ----------------------------------------------------------------------------
 
-def _col_bytes(c):
-    if c.kind == 'bytes':
-        return (c.offsets.numel() * c.offsets.element_size() + c.data.numel() - 16) / max(c.length, 1) + 0.125
-    return c.values.element_size() + 0.125
-
-
-def kernel_alg_bytes(table, raw):
-    """{entry point: [bytes per launch, in launch order]} for the row-streaming
-    kernels: each reads its column once (values + validity bit); hash kernels
-    also write/read their groups (16 B per group for sets, 32 B with counts)."""
-    out = {}
+def profile_alg_bytes(table, raw):
+    """B_alg = sum_numeric 3 n (w + 1/8) + sum_string n (o + L + 1/8)
+    + sum_date n (w + 1/8) + sum_all 32 D, per shard (n = this rank's rows)."""
+    from spark_df_profiling.engine import col_read_bytes
+    b = 0.0
     for c in table.columns:
-        b = raw['columns'][c.name]
-        n = c.length
-        w = _col_bytes(c)
-        if c.kind == 'bytes':
-            out.setdefault('sdp_hash_bytes', []).append(n * w + 32 * b['distinct_count'])
-        elif c.spark_type in ('double', 'float', 'bigint', 'int', 'smallint', 'tinyint', 'date'):
-            out.setdefault('sdp_pass1', []).append(n * w)
-            out.setdefault('sdp_hash_u64', []).append(n * w + 16 * b['distinct_count'])
-            if 'numeric' in b:
-                out.setdefault('sdp_pass2', []).append(n * w)
-    return out
+        info = raw['columns'][c.name]
+        rb = col_read_bytes(c)
+        if c.kind == 'fixed' and c.spark_type in ('double', 'float', 'bigint', 'int', 'smallint', 'tinyint'):
+            b += 3 * rb
+        else:
+            b += rb
+        b += 32.0 * info['distinct_count'] / max(1, int(os.environ.get('WORLD_SIZE', '1')))
+    return b
 
 
-def roofline(rec, alg):
-    """Dominant entry point by total event time -> achieved GB/s vs HBM peak."""
+def roofline(rec, steps, step_s, prof_bytes):
+    """Dominant kernel (entry point + label) by total HIP-event time -> achieved
+    GB/s = its algorithmic bytes per launch / its mean launch duration."""
     torch.cuda.synchronize()
-    times = {k: [a.elapsed_time(b) for a, b in v] for k, v in rec.items()}
-    tot = {k: sum(v) for k, v in times.items()}
-    dom = max((k for k in tot if k in alg), key=lambda k: tot[k])
-    nl = len(times[dom])
-    steps = max(1, nl // max(1, len(alg[dom])))
-    per_launch_bytes = sum(alg[dom]) / len(alg[dom])
-    avg_ms = tot[dom] / nl
-    achieved = per_launch_bytes / (avg_ms * 1e-3) / 1e9
-    return {'bound': 'hbm', 'kernel': dom, 'achieved': round(achieved, 1), 'peak': HBM_PEAK_GBS,
-            'unit': 'GB/s', 'frac': round(achieved / HBM_PEAK_GBS, 4), 'traffic': None,
-            'launches_per_step': nl // steps, 'avg_launch_ms': round(avg_ms, 4),
-            'alg_bytes_per_launch': int(per_launch_bytes)}, {k: round(v / steps, 3) for k, v in tot.items()}
+    tot, nbytes, nl = {}, {}, {}
+    for k, v in rec.items():
+        tot[k] = sum(a.elapsed_time(b) for a, b, _ in v)
+        nl[k] = len(v)
+        nbytes[k] = sum(x for _, _, x in v if x is not None) if any(x is not None for _, _, x in v) else None
+    dom = max((k for k in tot if nbytes[k]), key=lambda k: tot[k])
+    avg_ms = tot[dom] / nl[dom]
+    per_launch = nbytes[dom] / nl[dom]
+    achieved = per_launch / (avg_ms * 1e-3) / 1e9
+    prof_gbs = prof_bytes / step_s / 1e9
+    out = {'bound': 'hbm', 'kernel': dom, 'achieved': round(achieved, 1), 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
+           'frac': round(achieved / HBM_PEAK_GBS, 4), 'traffic': None,
+           'launches_per_step': nl[dom] // steps, 'avg_launch_ms': round(avg_ms, 4),
+           'alg_bytes_per_launch': int(per_launch),
+           'share_of_step': round(tot[dom] / steps / (step_s * 1e3), 3),
+           'whole_profile': {'alg_bytes_per_step': int(prof_bytes), 'achieved': round(prof_gbs, 1),
+                             'frac': round(prof_gbs / HBM_PEAK_GBS, 4)}}
+    per_kernel = {k: {'ms_per_step': round(tot[k] / steps, 3), 'launches_per_step': nl[k] // steps,
+                      'gbs': (round(nbytes[k] / (tot[k] * 1e-3) / 1e9, 1) if nbytes[k] and tot[k] > 0 else None)}
+                  for k in sorted(tot, key=lambda k: -tot[k])}
+    return out, per_kernel
 
 
 # ----------------------------------------------------------------------------
@@ -269,6 +271,10 @@ def main():
     ap.add_argument('--no-plots', action='store_true')
     args = ap.parse_args()
 
+    if not args.no_plots:
+        # histogram rendering workers (spawned before this process touches the GPU)
+        from spark_df_profiling import plot
+        plot.start_pool()
     world = int(os.environ.get('WORLD_SIZE', '1'))
     rank = int(os.environ.get('RANK', '0'))
     local = int(os.environ.get('LOCAL_RANK', '0'))
@@ -313,7 +319,8 @@ def main():
     if comm is not None:
         el = torch.tensor([elapsed], dtype=torch.float64, device=device)
         elapsed = float(torch.stack(comm.allgather(el)).max().item())
-    rl, per_kernel_ms = roofline(rec, kernel_alg_bytes(table, raw))
+    step_s = elapsed / args.steps
+    rl, per_kernel = roofline(rec, args.steps, step_s, profile_alg_bytes(table, raw))
 
     if rank != 0:
         return
@@ -327,7 +334,7 @@ def main():
                    'rows': args.rows, 'columns': 16, 'parallelism': 'row-shard x%d' % world,
                    'plots': not args.no_plots},
         'roofline': rl,
-        'per_kernel_ms_per_step': per_kernel_ms,
+        'per_kernel': per_kernel,
         'resident_gb_per_gpu': round(table_bytes(table) / 1e9, 2),
         'gen_s': round(t_gen, 1),
     }

@@ -229,6 +229,21 @@ int sdp_select_by_value(const uint64_t *d_sel, const uint64_t *d_vals, const uin
 int sdp_count_valid(const uint8_t *d_validity, int64_t bit_offset, int64_t length,
                     uint64_t *d_out, void *stream);
 
+/* ---- small-range integral columns (sdp_bitmap.hip) -------------------------
+ * countDistinct (describe.py:143) of an integral / date column whose values lie
+ * in [lo, lo + range), range <= SDP_BITMAP_MAX_BITS (lo, range from pass-1
+ * min/max): one bit per possible value, per-workgroup LDS bitmaps OR-reduced.
+ * Nulls are skipped.  d_bitmap (nullable, ceil(range/32) u32): the OR-ed bitmap
+ * (ranks all-gather and re-reduce it with sdp_bitmap_reduce); *d_out += the
+ * number of set bits (d_out zeroed by the caller). */
+#define SDP_BITMAP_MAX_BITS (1 << 20)
+int64_t sdp_bitmap_workspace_bytes(int64_t length, int64_t range);
+int sdp_distinct_bitmap(const sdp_column *col, int64_t lo, int64_t range, void *d_work,
+                        int64_t work_bytes, uint32_t *d_bitmap, uint64_t *d_out, void *stream);
+/* OR of nparts bitmaps of nwords words (d_parts[p * nwords + w]) + popcount. */
+int sdp_bitmap_reduce(const uint32_t *d_parts, int32_t nparts, int64_t nwords, uint32_t *d_bitmap,
+                      uint64_t *d_out, void *stream);
+
 /* ---- two-level hash partitioning with exact offsets (sdp_part.hip) ---------
  * Replaces countDistinct (describe.py:143) and groupBy(c).count()
  * (describe.py:251).  Records are structure-of-arrays: fixed-width keys are one

@@ -23,6 +23,7 @@ MAX_WINDOWS = 5
 PASS1_WAVES = 4          # SDP_PASS1_WAVES
 PART_MAX_GRID = 1024     # SDP_PART_MAX_GRID
 HEAVY_MAX = 256
+BITMAP_MAX_BITS = 1 << 20        # SDP_BITMAP_MAX_BITS
 
 # enum sdp_dtype
 I8, I16, I32, I64, F32, F64, U8, U16, U32, U64, BOOL = 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11
@@ -128,6 +129,9 @@ _SIGNATURES = {
     'sdp_part_dedup': (ctypes.c_int, [_REC, _I32, _BCOL, _P, _I64, _I32, _P, _P, _P, _P, _P]),
     'sdp_part_compact': (ctypes.c_int, [_P, _P, _P, _P, _P, _I64, _P, _P, _P]),
     'sdp_scan_workspace_bytes': (_I64, [_I64]),
+    'sdp_bitmap_workspace_bytes': (_I64, [_I64, _I64]),
+    'sdp_distinct_bitmap': (ctypes.c_int, [_COL, _I64, _I64, _P, _I64, _P, _P, _P]),
+    'sdp_bitmap_reduce': (ctypes.c_int, [_P, _I32, _I64, _P, _P, _P]),
     'sdp_scan_u32': (ctypes.c_int, [_P, _I64, _P, _P, _I64, _P]),
     'sdp_rowmask': (ctypes.c_int, [_COL, ctypes.POINTER(_I32), _I32, _P, _I64, _P, _P]),
     'sdp_gram_workspace_bytes': (_I64, [_I64, _I32]),
@@ -136,7 +140,7 @@ _SIGNATURES = {
 
 _VALUE_FUNCS = {'sdp_last_error', 'sdp_version', 'sdp_pass1_workspace_bytes', 'sdp_pass2_workspace_bytes',
                 'sdp_pass1_grid', 'sdp_gram_workspace_bytes', 'sdp_part_rows_per_block', 'sdp_part_bucket_target',
-                'sdp_scan_workspace_bytes'}
+                'sdp_scan_workspace_bytes', 'sdp_bitmap_workspace_bytes'}
 _STATUS_FUNCS = set(_SIGNATURES) - _VALUE_FUNCS
 
 _lib = None
@@ -172,15 +176,18 @@ class _Caller:
             return fn
 
         def call(*args):
+            global _pending
             rec = _recorder
             if rec is not None:
+                note, _pending = _pending, None
                 ev0 = torch.cuda.Event(enable_timing=True)
                 ev0.record()
             rc = fn(*args)
             if rec is not None:
                 ev1 = torch.cuda.Event(enable_timing=True)
                 ev1.record()
-                rec.setdefault(name, []).append((ev0, ev1))
+                key = name if note is None or not note[0] else '%s[%s]' % (name, note[0])
+                rec.setdefault(key, []).append((ev0, ev1, None if note is None else note[1]))
             if rc != 0:
                 msg = lib.sdp_last_error().decode(errors='replace')
                 raise NativeError('%s failed (status %d): %s' % (name, rc, msg))
@@ -191,10 +198,23 @@ class _Caller:
 
 sdp = _Caller()
 
-# Optional per-entry-point HIP event timing (bench.py): {name: [(start, end)]}.
+# Optional per-entry-point HIP event timing (bench.py):
+# {name or name[label]: [(start, end, alg_bytes or None)]}.
 # Events are recorded on the current torch stream, the stream every entry point
 # is launched on; nothing synchronises until the caller reads them.
 _recorder = None
+
+
+_pending = None
+
+
+def annotate(label, alg_bytes):
+    """Tag the next entry-point call while recording: it is keyed as
+    `name[label]` and carries its algorithmic bytes (compulsory HBM traffic:
+    inputs read once, outputs written once) for the roofline."""
+    global _pending
+    if _recorder is not None:
+        _pending = (label, float(alg_bytes))
 
 
 def start_recording():

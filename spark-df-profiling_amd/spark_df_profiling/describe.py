@@ -21,6 +21,7 @@ import numpy as np
 import pandas as pd
 import pyarrow as pa
 
+from . import _native as nat
 from .columns import DATE_TYPES, FLOAT_TYPES, INT_TYPES, DeviceColumn, DeviceTable
 from .engine import PROBS, TOPK, Engine, hist_edges  # noqa: F401
 from .utils import corr_from_gram, pretty_name
@@ -74,6 +75,15 @@ def _value_counts_first(engine, col, k):
     return _series(engine.first_rows(col, k), col).value_counts()
 
 
+def _distinct_count(engine, col, p1, hint):
+    """countDistinct (describe.py:143) of a NUM/DATE column: a value bitmap when
+    the integral range from pass 1 is small, else exact hash grouping."""
+    if (p1['count'] and col.kind == 'fixed' and col.dtype in engine.BITMAP_DTYPES
+            and p1['imax'] - p1['imin'] + 1 <= nat.BITMAP_MAX_BITS):
+        return engine.distinct_bitmap(col, p1['imin'], p1['imax'] - p1['imin'] + 1)
+    return engine.distinct_fixed(col, with_counts=False, capacity_hint=hint)['groups']
+
+
 def describe_1d(engine: Engine, col: DeviceColumn, nrows, bins, k, freq, bundle):
     """describe.py:136-189 for one column; `bundle` receives raw engine outputs."""
     spark_t = col.spark_type
@@ -92,7 +102,7 @@ def describe_1d(engine: Engine, col: DeviceColumn, nrows, bins, k, freq, bundle)
         hint = p1['n_valid']
         if spark_t in INT_TYPES and p1['count']:
             hint = min(hint, p1['imax'] - p1['imin'] + 1 + (p1['n_valid'] - p1['count']))
-        distinct = engine.distinct_fixed(col, with_counts=False, capacity_hint=hint)['groups']
+        distinct = _distinct_count(engine, col, p1, hint)
     elif spark_t in DATE_TYPES:
         p1 = engine.minmax_pass(col)
         bundle['minmax'] = p1
@@ -100,7 +110,7 @@ def describe_1d(engine: Engine, col: DeviceColumn, nrows, bins, k, freq, bundle)
         hint = p1['n_valid']
         if p1['count']:
             hint = min(hint, p1['imax'] - p1['imin'] + 1)
-        distinct = engine.distinct_fixed(col, with_counts=False, capacity_hint=hint)['groups']
+        distinct = _distinct_count(engine, col, p1, hint)
     elif col.kind == 'fixed':                      # boolean, decimal(20,0) from uint64
         tab = engine.distinct_fixed(col, with_counts=True)
         distinct, count = tab['groups'], tab['rows']
@@ -232,18 +242,18 @@ def describe(df, bins=10, corr_reject=0.9, **kwargs):
     k_vals, t_freq = kwargs.get('k_vals') or {}, kwargs.get('t_freq') or {}
     bundles = OrderedDict()
     ldesc = OrderedDict()
+    pending = OrderedDict()
     for col in table.columns:
         b = bundles.setdefault(col.name, {'spark_type': col.spark_type})
         ldesc[col.name] = describe_1d(engine, col, n, bins, k_vals.get(col.name, 2), t_freq.get(col.name, 'D'), b)
+        if plots and ldesc[col.name]['type'] == 'NUM':
+            # rendered by worker processes while the next columns' kernels run
+            st = b['numeric']
+            pending[col.name] = _submit_plot(st)
 
-    if plots:
-        from .plot import complete_histogram, mini_histogram, hist_frame
-        for name, s in ldesc.items():
-            if s['type'] == 'NUM':
-                st = bundles[name]['numeric']
-                frame = hist_frame(st.hist_counts, st.edges, st.width)
-                s['histogram'] = complete_histogram(frame)
-                s['mini_histogram'] = mini_histogram(frame)
+    for name, fut in pending.items():
+        s = ldesc[name]
+        s['histogram'], s['mini_histogram'] = fut.result() if hasattr(fut, 'result') else fut
 
     # correlation rejection (describe.py:89-100)
     corr = None
@@ -260,6 +270,16 @@ def describe(df, bins=10, corr_reject=0.9, **kwargs):
     if raw is not None:
         raw.update({'columns': bundles, 'corr': corr})
     return _assemble(ldesc, table_stats, len(table.columns))
+
+
+def _submit_plot(st):
+    """describe.py:227-228 histogram + mini_histogram for one NUM column: a
+    pool future, or the strings themselves when SDP_PLOT_WORKERS=0."""
+    from . import plot
+    import os
+    if os.environ.get('SDP_PLOT_WORKERS', '') == '0':
+        return plot.render_pair(st.hist_counts, st.edges, st.width)
+    return plot.submit(st.hist_counts, st.edges, st.width)
 
 
 def corr_matrix(engine, table, columns, bundles):

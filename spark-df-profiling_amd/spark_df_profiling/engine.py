@@ -50,6 +50,29 @@ def _u(x):
     return int(x) & U64
 
 
+DTYPE_NAME = {nat.I8: 'i8', nat.I16: 'i16', nat.I32: 'i32', nat.I64: 'i64', nat.U8: 'u8', nat.U16: 'u16',
+              nat.U32: 'u32', nat.U64: 'u64', nat.F32: 'f32', nat.F64: 'f64', nat.BOOL: 'bool'}
+
+
+def col_read_bytes(col):
+    """Compulsory bytes of one read of a column: values (or offsets + string
+    bytes) plus the validity bit."""
+    n = col.length
+    vb = n / 8.0 if col.validity is not None else 0.0
+    if col.kind == 'bytes':
+        if col.fixed_width:
+            return n * col.fixed_width + vb
+        return n * col.offset_width + max(0, col.data.numel() - 16) + vb
+    if col.kind != 'fixed':
+        return vb
+    return n * nat.ELEM_SIZE.get(col.dtype, 8) + vb
+
+
+def _label(col, stage=''):
+    base = 'bytes' if col.kind == 'bytes' else DTYPE_NAME.get(col.dtype, 'fixed')
+    return base + ('/' + stage if stage else '')
+
+
 def inv_mix64(x):
     """Inverse of mix64 (sdp_common.h), so a fixed key is recovered from its record."""
     M = U64
@@ -203,6 +226,7 @@ class Engine:
         cand_counts = torch.zeros(max(nw, 1) * nseg, dtype=torch.int32, device=self.device)
         res_dev = self._bytes(ctypes.sizeof(nat.SdpPass1Result))
         cs = col.sdp()
+        nat.annotate(_label(col), col_read_bytes(col))
         sdp.sdp_pass1(ctypes.byref(cs), ptr(plan_dev), ptr(work), work.numel(), ptr(cand), ptr(cand_counts), cap,
                       ptr(res_dev), self._s())
         local = self._read(res_dev, nat.SdpPass1Result)
@@ -339,6 +363,7 @@ class Engine:
         res = self._bytes(ctypes.sizeof(nat.SdpPass2Result))
         hist = self._u64(bins)
         cs = col.sdp()
+        nat.annotate(_label(col), col_read_bytes(col))
         sdp.sdp_pass2(ctypes.byref(cs), float(mean), ptr(e), bins, int(mono), float(hi_t), float(lo_t), ptr(work),
                       work.numel(), ptr(res), ptr(hist), self._s())
         r = self._read(res, nat.SdpPass2Result)
@@ -470,11 +495,15 @@ class Engine:
         rpb = sdp.sdp_part_rows_per_block(n, int(isb))
         grid = max(1, -(-n // rpb))
         h1 = torch.empty(nb1 * grid, dtype=torch.int32, device=self.device)
+        rb = col_read_bytes(col)
+        recw = 24 if isb else 8
+        nat.annotate(_label(col, 'count'), rb)
         sdp.sdp_part_rows(cref, bref, hvref, b1, 0, ptr(h1), None, None, ptr(hcnt), ptr(stats), s)
         o1 = self._scan(h1)
         nrec = int(o1[-1].item())
         r1, keep1 = self._records(nrec, isb)
         if nrec:
+            nat.annotate(_label(col, 'scatter'), rb + nrec * recw)
             sdp.sdp_part_rows(cref, bref, hvref, b1, 1, None, ptr(o1), ctypes.byref(r1), ptr(hcnt), ptr(stats), s)
         # level 2: each L1 bucket -> nb2 sub-buckets, chunk by chunk
         bstarts = o1[0:nb1 * grid:grid]
@@ -496,9 +525,11 @@ class Engine:
             ch[:, 3] = nch[bof]
             chunks = torch.from_numpy(ch).to(self.device)
             h2 = torch.empty(nb2 * K, dtype=torch.int32, device=self.device)
+            nat.annotate(('bytes' if isb else 'u64') + '/count', nrec * recw)
             sdp.sdp_part_recs(ctypes.byref(r1), int(isb), ptr(chunks), K, b1, b2, 0, ptr(h2), None, None, s)
             o2 = self._scan(h2)
             rf, keepf = self._records(nrec, isb)
+            nat.annotate(('bytes' if isb else 'u64') + '/scatter', 2 * nrec * recw)
             sdp.sdp_part_recs(ctypes.byref(r1), int(isb), ptr(chunks), K, b1, b2, 1, None, ptr(o2),
                               ctypes.byref(rf), s)
             del keep1, r1, h2
@@ -511,6 +542,7 @@ class Engine:
         if with_counts:
             out_key, out_cnt = self._u64(max(nrec, 1)), self._u64(max(nrec, 1))
         if nrec:
+            nat.annotate('bytes' if isb else ('u64/counts' if with_counts else 'u64'), nrec * recw)
             sdp.sdp_part_dedup(ctypes.byref(rf), int(isb), bref, ptr(starts), nfinal, int(with_counts),
                                ptr(out_key), ptr(out_cnt), ptr(ngroups), ptr(stats), s)
         st = self._host_u64(stats)
@@ -559,6 +591,26 @@ class Engine:
         sdp.sdp_scan_u32(ptr(counts_i32), n, ptr(out), ptr(work), work.numel(), self._s())
         return out
 
+    BITMAP_DTYPES = (nat.I8, nat.I16, nat.I32, nat.I64, nat.U8, nat.U16, nat.U32)
+
+    def distinct_bitmap(self, col, lo, range_):
+        """countDistinct (describe.py:143) of an integral column whose values lie
+        in [lo, lo + range_), range_ <= 2^20: LDS bitmaps (sdp_bitmap.hip).  Ranks
+        all-gather their OR-ed bitmaps and re-reduce them."""
+        nw = (range_ + 31) // 32
+        work = self._bytes(sdp.sdp_bitmap_workspace_bytes(col.length, range_))
+        bm = torch.empty(nw, dtype=torch.int32, device=self.device)
+        out = self._u64(1, zero=True)
+        cs = col.sdp()
+        nat.annotate(_label(col), col_read_bytes(col))
+        sdp.sdp_distinct_bitmap(ctypes.byref(cs), int(lo), int(range_), ptr(work), work.numel(), ptr(bm), ptr(out),
+                                self._s())
+        if self.comm.world > 1:
+            allb = torch.cat(self.comm.allgather(bm))
+            out.zero_()
+            sdp.sdp_bitmap_reduce(ptr(allb), self.comm.world, nw, None, ptr(out), self._s())
+        return int(out.item())
+
     def distinct_fixed(self, col, with_counts=False, capacity_hint=None):
         """countDistinct over a fixed-width column (describe.py:143).
 
@@ -580,6 +632,7 @@ class Engine:
         slots, counts = self._table(cap, False, with_counts)
         stats = self._u64(4, zero=True)
         cs = col.sdp()
+        nat.annotate(_label(col), col_read_bytes(col))
         sdp.sdp_hash_u64(ctypes.byref(cs), ptr(row_counts), ptr(slots), ptr(counts), cap, int(with_counts),
                          ptr(stats), self._s())
         st = self._host_u64(stats)
@@ -603,6 +656,7 @@ class Engine:
         slots, counts = self._table(cap, True, True)
         stats = self._u64(4, zero=True)
         bc = col.sdp_bytes()
+        nat.annotate(_label(col), col_read_bytes(col))
         sdp.sdp_hash_bytes(ctypes.byref(bc), ptr(row_counts), ptr(slots), ptr(counts), cap, ptr(stats), self._s())
         st = self._host_u64(stats)
         tab = {'slots': slots, 'counts': counts, 'capacity': cap, 'bytes': True, 'rows': st[1], 'groups': st[0],
@@ -835,11 +889,13 @@ class Engine:
         cn = (ctypes.c_int32 * C)(*[int(x) for x in check_nan])
         work = self._bytes(sdp.sdp_gram_workspace_bytes(n, C))
         keep = torch.empty((n + 31) // 32 + 1, dtype=torch.int32, device=self.device)
+        nat.annotate('', sum(n / 8.0 for c in cols if c.validity is not None))
         sdp.sdp_rowmask(arr, cn, C, ptr(work), work.numel(), ptr(keep), self._s())
         sh = torch.tensor([float(x) for x in shifts], dtype=torch.float64, device=self.device)
         G = torch.empty(C * C, dtype=torch.float64, device=self.device)
         s = torch.empty(C, dtype=torch.float64, device=self.device)
         nn = torch.empty(1, dtype=torch.float64, device=self.device)
+        nat.annotate('', sum(col_read_bytes(c) - (n / 8.0 if c.validity is not None else 0) for c in cols) + n / 8.0)
         sdp.sdp_gram(arr, C, ptr(keep), ptr(sh), ptr(work), work.numel(), ptr(G), ptr(s), ptr(nn), self._s())
         packed = self.comm.allreduce_sum(torch.cat([G, s, nn]))   # fp64 partial sums over ranks
         host = packed.cpu().numpy()

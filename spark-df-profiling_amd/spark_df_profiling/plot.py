@@ -66,3 +66,72 @@ def complete_histogram(hist_data):
     ax.set_ylabel('Frequency')
     fig.subplots_adjust(left=0.15, right=0.95, top=0.9, bottom=0.1, wspace=0, hspace=0)
     return _encode(fig)
+
+
+def render_pair(counts, edges, width):
+    """(histogram, mini_histogram) data URIs of one column's bins."""
+    frame = hist_frame(counts, edges, width)
+    return complete_histogram(frame), mini_histogram(frame)
+
+
+# ----------------------------------------------------------------------------
+# Rendering pool.  matplotlib costs ~20 ms of pure-Python CPU per image (24
+# images for a 12-numeric-column table), longer than the GPU statistics
+# themselves, so describe() hands each column's bins to worker processes as
+# soon as pass 2 has produced them and collects the strings at the end: the
+# rendering overlaps the remaining columns' kernels.  Workers are spawned (a
+# fresh interpreter: never a fork of a process holding the GPU) and import
+# only this module's dependencies.
+# ----------------------------------------------------------------------------
+
+_POOL = None
+
+
+def _warm():
+    return render_pair(np.array([1, 0, 2]), [0.0, 1.0, 2.0], 1.0)[1][:len(BASE)]
+
+
+def start_pool(workers=None):
+    """Start (once) the spawn-context worker pool and wait until every worker
+    has imported matplotlib.  Call early (before heavy GPU allocation) to keep
+    the one-time start-up out of the first describe()."""
+    global _POOL
+    if _POOL is not None:
+        return _POOL
+    import multiprocessing as mp
+    import os
+    from concurrent.futures import ProcessPoolExecutor
+    n = workers or int(os.environ.get('SDP_PLOT_WORKERS', '0')) or min(8, os.cpu_count() or 1)
+    _POOL = ProcessPoolExecutor(max_workers=n, mp_context=mp.get_context('spawn'))
+    # spawn re-runs the parent's __main__ in every child unless it cannot find
+    # it; hide it while the workers start (they need only this module)
+    import sys
+    main = sys.modules.get('__main__')
+    saved = {a: getattr(main, a) for a in ('__file__', '__spec__') if main is not None and hasattr(main, a)}
+    try:
+        if '__file__' in saved:
+            del main.__file__
+        if '__spec__' in saved:
+            main.__spec__ = None
+        futs = [_POOL.submit(_warm) for _ in range(2 * n)]
+    finally:
+        for a, v in saved.items():
+            setattr(main, a, v)
+    for f in futs:
+        f.result()
+    import atexit
+    atexit.register(shutdown_pool)
+    return _POOL
+
+
+def shutdown_pool():
+    global _POOL
+    if _POOL is not None:
+        _POOL.shutdown(wait=True, cancel_futures=True)
+        _POOL = None
+
+
+def submit(counts, edges, width):
+    """Future of render_pair(counts, edges, width) on the pool."""
+    pool = start_pool()
+    return pool.submit(render_pair, np.asarray(counts, dtype=np.int64), [float(e) for e in edges], float(width))
