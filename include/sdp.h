@@ -254,8 +254,8 @@ int sdp_bitmap_reduce(const uint32_t *d_parts, int32_t nparts, int64_t nwords, u
  * H1[bucket][block]) -> sdp_scan_u32 -> phase 1 (scatter at exact offsets) ->
  * sdp_part_recs phase 0/1 per chunk with the next b2 bits -> sdp_scan_u32 ->
  * sdp_part_dedup (one workgroup per final bucket, LDS table).
- * d_stats (68 x u64, zeroed): [0] valid rows, [1] fixed-key records whose
- * h == UINT64_MAX (kept outside the tables), [2] 64-bit hash collision between
+ * d_stats (68 x u64, zeroed): [0] valid rows, [1] fixed-key rows whose
+ * h == UINT64_MAX (counted by phase 0, never made records), [2] 64-bit hash collision between
  * different byte strings, [3] LDS table full, [4..67] groups (64 counters). */
 #define SDP_PART_MAX_GRID 1024
 typedef struct sdp_records {
@@ -298,7 +298,9 @@ int sdp_part_recs(const sdp_records *in, int32_t is_bytes, const sdp_chunk *d_ch
                   int64_t nchunks, int32_t b1, int32_t b2, int32_t phase, uint32_t *d_hist,
                   const uint64_t *d_offsets, const sdp_records *out, void *stream);
 /* Final bucket f = records [d_starts[f], d_starts[f+1]).  Distinct only (fixed
- * keys, !with_counts): group totals in d_stats.  Otherwise the groups of f go to
+ * keys, !with_counts): group totals in d_stats; buckets are sized for
+ * sdp_part_bucket_target distinct keys, or (with_counts == 2) for 4 x that
+ * when the hash bits run out (more than 2^30 rows on one device).  Otherwise the groups of f go to
  * d_out_key/d_out_cnt at [d_starts[f], + d_ngroups[f]): fixed keys as the
  * order-preserving u64 key, byte keys as (hash tag << 40 | row + 1). */
 int sdp_part_dedup(const sdp_records *in, int32_t is_bytes, const sdp_bytes_column *bcol,

@@ -152,6 +152,15 @@ __device__ __forceinline__ int64_t wave_sum_i64(int64_t v) {
 }
 
 __device__ __forceinline__ int lane_id() { return threadIdx.x & (WAVE - 1); }
+
+// Workgroup barrier for LDS hand-offs only.  __syncthreads() carries a
+// workgroup release/acquire fence, which drains vmcnt: every global load still
+// in flight (a prefetched next tile) would be waited for at the barrier.  This
+// waits for this wave's LDS operations only, so prefetches keep flying.  Use it
+// only where the barrier orders LDS accesses, never global memory.
+__device__ __forceinline__ void lds_barrier() {
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
 // number of set bits of `mask` below this lane
 __device__ __forceinline__ int lane_rank(uint64_t mask) {
     return __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32),

@@ -477,6 +477,11 @@ class Engine:
         n = col.length
         target = sdp.sdp_part_bucket_target(int(isb), int(with_counts))
         total_bits = max(0, math.ceil(math.log2(max(1.0, n / target))))
+        large = False
+        if total_bits > 20 and not isb and not with_counts:
+            # > 2^30 rows: 4x larger final buckets on the workgroup-table kernel
+            total_bits = max(20, math.ceil(math.log2(max(1.0, n / (4 * target)))))
+            large = True
         b1 = min(10, (total_bits + 1) // 2)
         b2 = total_bits - b1
         if b2 > 10:
@@ -543,7 +548,7 @@ class Engine:
             out_key, out_cnt = self._u64(max(nrec, 1)), self._u64(max(nrec, 1))
         if nrec:
             nat.annotate('bytes' if isb else ('u64/counts' if with_counts else 'u64'), nrec * recw)
-            sdp.sdp_part_dedup(ctypes.byref(rf), int(isb), bref, ptr(starts), nfinal, int(with_counts),
+            sdp.sdp_part_dedup(ctypes.byref(rf), int(isb), bref, ptr(starts), nfinal, int(with_counts) | (2 if large else 0),
                                ptr(out_key), ptr(out_cnt), ptr(ngroups), ptr(stats), s)
         st = self._host_u64(stats)
         if st[2] or st[3]:
