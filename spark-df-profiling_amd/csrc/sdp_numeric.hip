@@ -10,12 +10,13 @@
 //   pass 2         -> mad, CASE-WHEN histogram, outlier counts (one HBM read)
 // All block partials are merged by a single-block kernel in block order, so
 // every result is deterministic for a given grid.
+#include <type_traits>
 #include "sdp_common.h"
 
 namespace sdp {
 
 constexpr int P1_BLOCK = 256;
-constexpr int P1_UNROLL = 4;          // 16-B vectors per thread per tile
+constexpr int P1_UNROLL = 2;          // 16-B vectors per thread per tile (x2: the next tile is prefetched)
 constexpr int P1_MAX_GRID = 1024;     // 4 blocks per CU on 256 CUs
 constexpr int SORT_MAX = 16384;       // one-workgroup LDS bitonic sort (128 KiB)
 
@@ -194,6 +195,31 @@ struct P1Ctx {
     bool hne[SDP_MAX_WINDOWS]; // hi != lo
 };
 
+// U 16-byte vectors per thread of a grid-strided tile (+ their validity bits).
+// Streaming loops load the NEXT tile into a second VecTile before working on
+// the current one, so a wave always has a tile of loads in flight.
+template <typename T, int U, int NT>
+struct VecTile {
+    static constexpr int VPT = Vec16<T>::N;
+    Vec16<T> v[U];
+    uint32_t vb[U];
+    __device__ __forceinline__ void load(const sdp_column &col, int64_t tile, int64_t nvec) {
+        const Vec16<T> *vals = (const Vec16<T> *)col.d_values;
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int64_t vi = tile * ((int64_t)NT * U) + (int64_t)u * NT + threadIdx.x;
+            if (vi < nvec) {
+                v[u] = vals[vi];
+                vb[u] = valid_bits(col.d_validity, col.validity_bit_offset, vi * VPT, VPT);
+            } else {
+                vb[u] = 0;
+#pragma unroll
+                for (int e = 0; e < VPT; ++e) v[u].v[e] = (T)0;
+            }
+        }
+    }
+};
+
 // One element; every lane of the wave calls this in lockstep (ballots inside).
 template <typename T>
 __device__ __forceinline__ void p1_elem(P1Thread &st, const P1Ctx &cx, T x, bool valid) {
@@ -279,28 +305,22 @@ __global__ void __launch_bounds__(P1_BLOCK, 4) pass1_kernel(sdp_column col, cons
     const int64_t n = col.length;
     const int64_t nvec = n / VPT;
     const Vec16<T> *vals = (const Vec16<T> *)col.d_values;
-    const int64_t tile_vecs = (int64_t)P1_BLOCK * P1_UNROLL;
+    // 8-byte types: 2 vectors per tile; narrower ones 1 (4-16 elements already)
+    constexpr int U = sizeof(T) >= 8 ? P1_UNROLL : 1;
+    const int64_t tile_vecs = (int64_t)P1_BLOCK * U;
     const int64_t ntiles = (nvec + tile_vecs - 1) / tile_vecs;
+    (void)vals;
+    VecTile<T, U, P1_BLOCK> cur, nxt;
+    if ((int64_t)blockIdx.x < ntiles) cur.load(col, blockIdx.x, nvec);
     for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
-        Vec16<T> v[P1_UNROLL];
-        uint32_t vb[P1_UNROLL];
+        const bool more = tile + gridDim.x < ntiles;
+        if (more) nxt.load(col, tile + gridDim.x, nvec);          // next tile in flight
 #pragma unroll
-        for (int u = 0; u < P1_UNROLL; ++u) {
-            const int64_t vi = tile * tile_vecs + (int64_t)u * P1_BLOCK + threadIdx.x;
-            if (vi < nvec) {
-                v[u] = vals[vi];
-                vb[u] = valid_bits(col.d_validity, col.validity_bit_offset, vi * VPT, VPT);
-            } else {
-                vb[u] = 0;
+        for (int u = 0; u < U; ++u) {
 #pragma unroll
-                for (int e = 0; e < VPT; ++e) v[u].v[e] = (T)0;
-            }
+            for (int e = 0; e < VPT; ++e) p1_elem<T>(st, cx, cur.v[u].v[e], (cur.vb[u] >> e) & 1u);
         }
-#pragma unroll
-        for (int u = 0; u < P1_UNROLL; ++u) {
-#pragma unroll
-            for (int e = 0; e < VPT; ++e) p1_elem<T>(st, cx, v[u].v[e], (vb[u] >> e) & 1u);
-        }
+        if (more) cur = nxt;
     }
     // tail elements (n % VPT) by the first wave of block 0
     if (blockIdx.x == 0 && threadIdx.x < WAVE) {
@@ -630,7 +650,7 @@ __global__ void column_keys_kernel(sdp_column col, uint64_t *out, uint64_t *out_
 // ============================================================================
 
 constexpr int P2_BLOCK = 256;
-constexpr int P2_UNROLL = 2;
+constexpr int P2_UNROLL = 4;
 
 struct P2Ctx {
     double mean, hi_t, lo_t, e0, inv_w;
@@ -718,27 +738,21 @@ __global__ void __launch_bounds__(P2_BLOCK, 4) pass2_kernel(sdp_column col, doub
     const int64_t n = col.length;
     const int64_t nvec = n / VPT;
     const Vec16<T> *vals = (const Vec16<T> *)col.d_values;
-    const int64_t tile_vecs = (int64_t)P2_BLOCK * P2_UNROLL;
+    // (wider tiles of the narrower types run out of registers)
+    constexpr int U = sizeof(T) >= 8 ? P2_UNROLL : (std::is_same<T, float>::value ? P2_UNROLL / 2 : 1);
+    const int64_t tile_vecs = (int64_t)P2_BLOCK * U;
     const int64_t ntiles = (nvec + tile_vecs - 1) / tile_vecs;
+    (void)vals;
+    VecTile<T, U, P2_BLOCK> cur, nxt;
+    if ((int64_t)blockIdx.x < ntiles) cur.load(col, blockIdx.x, nvec);
     for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
-        Vec16<T> v[P2_UNROLL];
-        uint32_t vb[P2_UNROLL];
+        const bool more = tile + gridDim.x < ntiles;
+        if (more) nxt.load(col, tile + gridDim.x, nvec);          // next tile in flight
 #pragma unroll
-        for (int u = 0; u < P2_UNROLL; ++u) {
-            const int64_t vi = tile * tile_vecs + (int64_t)u * P2_BLOCK + threadIdx.x;
-            if (vi < nvec) {
-                v[u] = vals[vi];
-                vb[u] = valid_bits(col.d_validity, col.validity_bit_offset, vi * VPT, VPT);
-            } else {
-                vb[u] = 0;
+        for (int u = 0; u < U; ++u)
 #pragma unroll
-                for (int e = 0; e < VPT; ++e) v[u].v[e] = (T)0;
-            }
-        }
-#pragma unroll
-        for (int u = 0; u < P2_UNROLL; ++u)
-#pragma unroll
-            for (int e = 0; e < VPT; ++e) p2_elem<T, SMALL>(st, c, s_hist, v[u].v[e], (vb[u] >> e) & 1u);
+            for (int e = 0; e < VPT; ++e) p2_elem<T, SMALL>(st, c, s_hist, cur.v[u].v[e], (cur.vb[u] >> e) & 1u);
+        if (more) cur = nxt;
     }
     if (blockIdx.x == 0 && threadIdx.x < WAVE) {
         const int64_t i = nvec * VPT + threadIdx.x;
