@@ -269,6 +269,8 @@ def main():
     ap.add_argument('--cpu-sample-rows', type=int, default=1 << 20)
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--no-plots', action='store_true')
+    ap.add_argument('--workers', type=int, default=None,
+                    help='columns profiled concurrently per GPU (default: SDP_COLUMN_WORKERS or 1)')
     args = ap.parse_args()
 
     if not args.no_plots:
@@ -290,13 +292,17 @@ def main():
 
     from spark_df_profiling import describe
     from spark_df_profiling import _native as nat
+    from spark_df_profiling.describe import column_workers
+    from spark_df_profiling.engine import Engine
 
     t_gen = time.perf_counter()
     table = make_c3_shard(args.rows, rank, world, device)
     t_gen = time.perf_counter() - t_gen
 
+    column_workers_used = column_workers(Engine(device=device, comm=comm), args.workers)
+
     def step(raw=None):
-        return describe(table, comm=comm, plots=not args.no_plots, raw=raw)
+        return describe(table, comm=comm, plots=not args.no_plots, raw=raw, workers=args.workers)
 
     for _ in range(args.warmup):
         step()
@@ -332,7 +338,8 @@ def main():
         'config': {'workload': 'C3: %d rows x 16 mixed columns (6 f64, 4 i64, 2 f32, 3 utf8, 1 date32), '
                                '5%% nulls, row-sharded' % args.rows,
                    'rows': args.rows, 'columns': 16, 'parallelism': 'row-shard x%d' % world,
-                   'plots': not args.no_plots},
+                   'plots': not args.no_plots,
+                   'column_workers': column_workers_used},
         'roofline': rl,
         'per_kernel': per_kernel,
         'resident_gb_per_gpu': round(table_bytes(table) / 1e9, 2),

@@ -69,41 +69,51 @@ __global__ void rowmask_kernel(const MaskCol *cols, int ncols, int64_t n, uint32
 struct GramCol {
     const void *p;
     int32_t dtype;
-    int32_t _pad;
+    int32_t width;             // bytes per value
 };
 
-// 4 consecutive rows [r, r+4) of column c as doubles (0 beyond n)
-__device__ __forceinline__ void load4(const GramCol &gc, int64_t r, int64_t n, double out[4]) {
-    if (r + 4 <= n) {
-        switch (gc.dtype) {
-        case SDP_F64: {
-            const double2 *q = (const double2 *)((const double *)gc.p + r);
-            const double2 a = q[0], b = q[1];
-            out[0] = a.x; out[1] = a.y; out[2] = b.x; out[3] = b.y;
-            return;
-        }
-        case SDP_F32: {
-            const float4 a = *(const float4 *)((const float *)gc.p + r);
-            out[0] = a.x; out[1] = a.y; out[2] = a.z; out[3] = a.w;
-            return;
-        }
-        case SDP_I64: {
-            const longlong2 *q = (const longlong2 *)((const int64_t *)gc.p + r);
-            const longlong2 a = q[0], b = q[1];
-            out[0] = (double)a.x; out[1] = (double)a.y; out[2] = (double)b.x; out[3] = (double)b.y;
-            return;
-        }
-        case SDP_I32: {
-            const int4 a = *(const int4 *)((const int32_t *)gc.p + r);
-            out[0] = a.x; out[1] = a.y; out[2] = a.z; out[3] = a.w;
-            return;
-        }
-        default:
-            break;
-        }
-    }
+// 4 consecutive rows [r, r+4) of a column: raw bytes first, doubles after.
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+struct Raw4 {
+    u32x4 lo, hi;
+};
+// Rows [r, r + 32) lie inside the column (the fast path's margin), so every
+// lane loads the same two 16-byte words whatever its dtype -- one load form
+// per register, no divergent branch between loads, no waits until conv4.
+// Lanes of columns absent from the tile read column 0 (cache hits) as dtype 0.
+__device__ __forceinline__ void raw4(const GramCol &gc, int64_t r, Raw4 &x) {
+    // (4-byte types use only `lo`; their `hi` is the next lane group's rows, a cache hit)
+    const __attribute__((address_space(1))) u32x4 *b =
+        (const __attribute__((address_space(1))) u32x4 *)((const char *)gc.p + r * gc.width);
+    x.lo = b[0];
+    x.hi = b[1];
+}
+__device__ __forceinline__ void conv4(int dt, const Raw4 &x, double out[4]) {
+    const uint32_t w[8] = {x.lo[0], x.lo[1], x.lo[2], x.lo[3], x.hi[0], x.hi[1], x.hi[2], x.hi[3]};
 #pragma unroll
-    for (int m = 0; m < 4; ++m) out[m] = (r + m < n) ? load_as_double(gc.p, gc.dtype, r + m) : 0.0;
+    for (int m = 0; m < 4; ++m) {
+        const uint64_t u64 = ((uint64_t)w[2 * m + 1] << 32) | w[2 * m];
+        double v;
+        switch (dt) {
+        case SDP_F64: v = __longlong_as_double((long long)u64); break;
+        case SDP_I64: v = (double)(int64_t)u64; break;
+        case SDP_F32: v = (double)__uint_as_float(w[m]); break;
+        case SDP_I32: v = (double)(int32_t)w[m]; break;
+        case SDP_U32: v = (double)w[m]; break;
+        case SDP_I16: v = (double)(int16_t)(w[m >> 1] >> (16 * (m & 1))); break;
+        case SDP_U16: v = (double)(uint16_t)(w[m >> 1] >> (16 * (m & 1))); break;
+        case SDP_I8: v = (double)(int8_t)(w[0] >> (8 * m)); break;
+        case SDP_U8: v = (double)(uint8_t)(w[0] >> (8 * m)); break;
+        default: v = 0.0;
+        }
+        out[m] = v;
+    }
+}
+// element-wise (the column's last rows); 0 beyond n and for dtype 0
+__device__ __forceinline__ void load4_tail(const GramCol &gc, int64_t r, int64_t n, double out[4]) {
+#pragma unroll
+    for (int m = 0; m < 4; ++m)
+        out[m] = r + m < n ? load_as_double(gc.p, gc.dtype, r + m) : 0.0;
 }
 
 template <int TILE>
@@ -130,8 +140,8 @@ __global__ void __launch_bounds__(G_BLOCK) gram_kernel(const GramCol *cols, int 
         const int ci = ti * TILE + 16 * a + cl, cj = tj * TILE + 16 * a + cl;
         va[a] = ci < ncols;
         vb[a] = cj < ncols;
-        ca[a] = va[a] ? cols[ci] : GramCol{nullptr, 0, 0};
-        cb[a] = vb[a] ? cols[cj] : GramCol{nullptr, 0, 0};
+        ca[a] = va[a] ? cols[ci] : GramCol{cols[0].p, 0, cols[0].width};   // dtype 0 converts to 0.0
+        cb[a] = vb[a] ? cols[cj] : GramCol{cols[0].p, 0, cols[0].width};
         ka[a] = va[a] ? shift[ci] : 0.0;
         kb[a] = vb[a] ? shift[cj] : 0.0;
     }
@@ -145,37 +155,36 @@ __global__ void __launch_bounds__(G_BLOCK) gram_kernel(const GramCol *cols, int 
     for (int a = 0; a < NT; ++a) csum[a] = 0.0;
     double nkeep = 0.0;
 
+    // UNR k-blocks per iteration.  Away from the column end (a wave-uniform
+    // test) every lane issues the raw 16-byte loads of all UNR blocks back to
+    // back -- no dtype branch sits between a load and the next one, so nothing
+    // waits on memory before the conversions -- and only then converts; the
+    // last blocks of the column take the element-wise path.
+    constexpr int UNR = TILE == 16 ? 4 : (TILE == 32 ? 2 : 1);
     const int64_t c0 = (int64_t)s * rows_per_chunk;
     const int64_t c1 = min(n, c0 + rows_per_chunk);
-    for (int64_t r0 = c0 + (int64_t)wid * 16; r0 < c1; r0 += (int64_t)G_WAVES * 16) {
-        const int64_t r = r0 + 4 * q;
+    auto consume = [&](const double (&xa)[NT][4], const double (&xb)[NT][4], int64_t r, uint32_t kw) {
         uint32_t kbits = 0;
-        if (r < n) {
-            const uint32_t w = keep[r >> 5];
-            kbits = (w >> (r & 31)) & 0xFu;
+        if (r < c1) {
+            kbits = (kw >> (r & 31)) & 0xFu;
             if (r + 4 > c1) kbits &= (1u << (int)(c1 - r)) - 1u;   // chunk boundary
         }
         if (diag && cl == 0) nkeep += (double)__popc(kbits);
-        double xa[NT][4], xb[NT][4];
+        double ya[NT][4], yb[NT][4];
 #pragma unroll
         for (int a = 0; a < NT; ++a) {
-            if (va[a]) load4(ca[a], r, n, xa[a]);
-            else { xa[a][0] = xa[a][1] = xa[a][2] = xa[a][3] = 0.0; }
 #pragma unroll
-            for (int m = 0; m < 4; ++m) xa[a][m] = ((kbits >> m) & 1u) ? xa[a][m] - ka[a] : 0.0;
+            for (int m = 0; m < 4; ++m) ya[a][m] = ((kbits >> m) & 1u) ? xa[a][m] - ka[a] : 0.0;
             if (diag) {
 #pragma unroll
-                for (int m = 0; m < 4; ++m) csum[a] += xa[a][m];
+                for (int m = 0; m < 4; ++m) csum[a] += ya[a][m];
             }
         }
         if (!diag) {
 #pragma unroll
-            for (int b = 0; b < NT; ++b) {
-                if (vb[b]) load4(cb[b], r, n, xb[b]);
-                else { xb[b][0] = xb[b][1] = xb[b][2] = xb[b][3] = 0.0; }
+            for (int b = 0; b < NT; ++b)
 #pragma unroll
-                for (int m = 0; m < 4; ++m) xb[b][m] = ((kbits >> m) & 1u) ? xb[b][m] - kb[b] : 0.0;
-            }
+                for (int m = 0; m < 4; ++m) yb[b][m] = ((kbits >> m) & 1u) ? xb[b][m] - kb[b] : 0.0;
         }
 #pragma unroll
         for (int m = 0; m < 4; ++m)
@@ -183,8 +192,48 @@ __global__ void __launch_bounds__(G_BLOCK) gram_kernel(const GramCol *cols, int 
             for (int a = 0; a < NT; ++a)
 #pragma unroll
                 for (int b = 0; b < NT; ++b)
-                    acc[a][b] = __builtin_amdgcn_mfma_f64_16x16x4f64(xa[a][m], diag ? xa[b][m] : xb[b][m],
-                                                                      acc[a][b], 0, 0, 0);
+                    acc[a][b] = __builtin_amdgcn_mfma_f64_16x16x4f64(ya[a][m], diag ? ya[b][m] : yb[b][m], acc[a][b],
+                                                                      0, 0, 0);
+    };
+    for (int64_t rb = c0 + (int64_t)wid * 16 * UNR; rb < c1; rb += (int64_t)G_WAVES * 16 * UNR) {
+        if (rb + 16 * UNR + 32 <= n) {
+            uint32_t kw[UNR];
+            Raw4 ra[UNR][NT], rbw[UNR][NT];
+#pragma unroll
+            for (int u = 0; u < UNR; ++u) {
+                const int64_t r = rb + 16 * u + 4 * q;
+                kw[u] = r < c1 ? keep[r >> 5] : 0u;
+#pragma unroll
+                for (int a = 0; a < NT; ++a) raw4(ca[a], r, ra[u][a]);
+                if (!diag) {
+#pragma unroll
+                    for (int b = 0; b < NT; ++b) raw4(cb[b], r, rbw[u][b]);
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < UNR; ++u) {
+                double xa[NT][4], xb[NT][4];
+#pragma unroll
+                for (int a = 0; a < NT; ++a) conv4(ca[a].dtype, ra[u][a], xa[a]);
+                if (!diag) {
+#pragma unroll
+                    for (int b = 0; b < NT; ++b) conv4(cb[b].dtype, rbw[u][b], xb[b]);
+                }
+                consume(xa, xb, rb + 16 * u + 4 * q, kw[u]);
+            }
+        } else {
+            for (int u = 0; u < UNR; ++u) {
+                const int64_t r = rb + 16 * u + 4 * q;
+                double xa[NT][4], xb[NT][4];
+#pragma unroll
+                for (int a = 0; a < NT; ++a) load4_tail(ca[a], r, n, xa[a]);
+                if (!diag) {
+#pragma unroll
+                    for (int b = 0; b < NT; ++b) load4_tail(cb[b], r, n, xb[b]);
+                }
+                consume(xa, xb, r, r < c1 ? keep[r >> 5] : 0u);
+            }
+        }
     }
 
     // ---- combine the 4 waves through LDS (fixed order), write the chunk partial ----
@@ -273,7 +322,10 @@ static GramGeom gram_geom(int64_t n, int ncols) {
     g.tile = ncols <= 16 ? 16 : (ncols <= 32 ? 32 : 64);
     g.side = (ncols + g.tile - 1) / g.tile;
     g.T = g.side * (g.side + 1) / 2;
-    int64_t S = (1024 + g.T - 1) / g.T;
+    // enough workgroups for several rounds at full occupancy (a single
+    // 1024-workgroup round left a tail when fewer than 4 waves/SIMD fit)
+    const int64_t target = g.tile == 16 ? 8192 : 4096;
+    int64_t S = (target + g.T - 1) / g.T;
     const int64_t min_rows = 4096;
     const int64_t max_s = (n + min_rows - 1) / min_rows;
     if (S > max_s) S = max_s;
@@ -285,6 +337,15 @@ static GramGeom gram_geom(int64_t n, int ncols) {
     if (g.S < 1) g.S = 1;
     g.rows_per_chunk = rpc;
     return g;
+}
+
+static int gram_width(int dt) {
+    switch (dt) {
+    case SDP_F64: case SDP_I64: return 8;
+    case SDP_F32: case SDP_I32: case SDP_U32: return 4;
+    case SDP_I16: case SDP_U16: return 2;
+    default: return 1;
+    }
 }
 
 static int64_t align256(int64_t x) { return (x + 255) / 256 * 256; }
@@ -350,7 +411,7 @@ extern "C" int sdp_gram(const sdp_column *cols, int32_t ncols, const uint32_t *d
     w += align256((int64_t)g.S * g.side * g.tile * sizeof(double));
     double *pn = (double *)w;
     GramCol *h = (GramCol *)malloc(sizeof(GramCol) * ncols);
-    for (int i = 0; i < ncols; ++i) { h[i].p = cols[i].d_values; h[i].dtype = cols[i].dtype; h[i]._pad = 0; }
+    for (int i = 0; i < ncols; ++i) { h[i].p = cols[i].d_values; h[i].dtype = cols[i].dtype; h[i].width = gram_width(cols[i].dtype); }
     hipStream_t s = (hipStream_t)stream;
     hipError_t e = hipMemcpyAsync(d_cols, h, sizeof(GramCol) * ncols, hipMemcpyHostToDevice, s);
     if (e == hipSuccess) e = hipStreamSynchronize(s);

@@ -12,6 +12,7 @@ device pointers from the torch caching allocator are valid in our kernels.
 from __future__ import annotations
 
 import ctypes
+import threading
 import os
 
 import torch  # noqa: F401  (must precede the dlopen, see module docstring)
@@ -176,10 +177,9 @@ class _Caller:
             return fn
 
         def call(*args):
-            global _pending
             rec = _recorder
             if rec is not None:
-                note, _pending = _pending, None
+                note, _tls.pending = getattr(_tls, 'pending', None), None
                 ev0 = torch.cuda.Event(enable_timing=True)
                 ev0.record()
             rc = fn(*args)
@@ -205,16 +205,15 @@ sdp = _Caller()
 _recorder = None
 
 
-_pending = None
+_tls = threading.local()            # the pending annotation is per thread (column workers)
 
 
 def annotate(label, alg_bytes):
     """Tag the next entry-point call while recording: it is keyed as
     `name[label]` and carries its algorithmic bytes (compulsory HBM traffic:
     inputs read once, outputs written once) for the roofline."""
-    global _pending
     if _recorder is not None:
-        _pending = (label, float(alg_bytes))
+        _tls.pending = (label, float(alg_bytes))
 
 
 def start_recording():

@@ -240,16 +240,25 @@ def describe(df, bins=10, corr_reject=0.9, **kwargs):
         raise ValueError('df cannot be empty')
 
     k_vals, t_freq = kwargs.get('k_vals') or {}, kwargs.get('t_freq') or {}
-    bundles = OrderedDict()
-    ldesc = OrderedDict()
+    bundles = OrderedDict((col.name, {'spark_type': col.spark_type}) for col in table.columns)
+    ldesc = OrderedDict((col.name, None) for col in table.columns)
     pending = OrderedDict()
-    for col in table.columns:
-        b = bundles.setdefault(col.name, {'spark_type': col.spark_type})
-        ldesc[col.name] = describe_1d(engine, col, n, bins, k_vals.get(col.name, 2), t_freq.get(col.name, 'D'), b)
-        if plots and ldesc[col.name]['type'] == 'NUM':
-            # rendered by worker processes while the next columns' kernels run
-            st = b['numeric']
-            pending[col.name] = _submit_plot(st)
+
+    def one(eng, col):
+        res = describe_1d(eng, col, n, bins, k_vals.get(col.name, 2), t_freq.get(col.name, 'D'), bundles[col.name])
+        # rendered by worker processes while the next columns' kernels run
+        fut = _submit_plot(bundles[col.name]['numeric']) if plots and res['type'] == 'NUM' else None
+        return res, fut
+
+    workers = column_workers(engine, kwargs.pop('workers', None))
+    if workers > 1:
+        done = _describe_concurrent(engine, table.columns, one, workers)
+    else:
+        done = {col.name: one(engine, col) for col in table.columns}
+    for name in ldesc:
+        ldesc[name], fut = done[name]
+        if fut is not None:
+            pending[name] = fut
 
     for name, fut in pending.items():
         s = ldesc[name]
@@ -270,6 +279,90 @@ def describe(df, bins=10, corr_reject=0.9, **kwargs):
     if raw is not None:
         raw.update({'columns': bundles, 'corr': corr})
     return _assemble(ldesc, table_stats, len(table.columns))
+
+
+def column_workers(engine, requested=None):
+    """Columns profiled at once on one device (SDP_COLUMN_WORKERS, default 1).
+    Each worker owns a HIP stream, so one column's latency-bound grouping
+    kernels overlap another's VALU-bound moment passes and the host-side
+    readbacks of both.  Sharded runs stay sequential: every rank must issue
+    its collectives in the same order."""
+    import os
+    w = requested if requested is not None else int(os.environ.get('SDP_COLUMN_WORKERS', '1'))
+    if engine.comm.world > 1 or engine.device.type != 'cuda':
+        return 1
+    return max(1, int(w))
+
+
+def _column_temp_bytes(col):
+    """Peak device temporaries of one column's profile: the grouping record
+    buffers (two generations) plus (key, count) outputs where counts are kept."""
+    n = col.length
+    if col.kind == 'bytes':
+        return 64 * n
+    if col.kind == 'fixed':
+        numeric = col.spark_type in INT_TYPES or col.spark_type in ('float', 'double')
+        return (16 if numeric else 32) * n
+    return 0
+
+
+class _DeviceBudget:
+    """Admits a column only while the temporaries of the columns in flight
+    fit the device memory left after the resident table."""
+
+    def __init__(self, device, reserve=4 << 30):
+        import threading
+        import torch
+        free, _ = torch.cuda.mem_get_info(device)
+        self.cap = max(0, free - reserve)
+        self.used = 0
+        self.busy = 0
+        self.cv = threading.Condition()
+
+    def acquire(self, need):
+        with self.cv:
+            # a column larger than the whole budget runs alone
+            self.cv.wait_for(lambda: self.busy == 0 or self.used + need <= self.cap)
+            self.used += need
+            self.busy += 1
+
+    def release(self, need):
+        with self.cv:
+            self.used -= need
+            self.busy -= 1
+            self.cv.notify_all()
+
+
+def _describe_concurrent(engine, columns, one, workers):
+    """Run `one(engine, col)` for every column on `workers` threads, each with
+    its own stream and Engine; largest columns first.  Results are per column
+    and independent of the schedule."""
+    import threading
+    import torch
+    from concurrent.futures import ThreadPoolExecutor
+    dev = engine.device
+    torch.cuda.synchronize(dev)             # the table's uploads are visible to every stream
+    budget = _DeviceBudget(dev)
+    local = threading.local()
+
+    def task(col):
+        if not hasattr(local, 'engine'):
+            local.stream = torch.cuda.Stream(device=dev)
+            local.engine = Engine(device=dev, comm=engine.comm, stream=local.stream)
+        need = _column_temp_bytes(col)
+        budget.acquire(need)
+        try:
+            with torch.cuda.stream(local.stream):
+                out = one(local.engine, col)
+            local.stream.synchronize()
+        finally:
+            budget.release(need)
+        return out
+
+    order = sorted(columns, key=lambda c: -_column_temp_bytes(c))
+    with ThreadPoolExecutor(max_workers=workers, thread_name_prefix='sdp-col') as ex:
+        futs = {col.name: ex.submit(task, col) for col in order}
+        return {name: f.result() for name, f in futs.items()}
 
 
 def _submit_plot(st):
