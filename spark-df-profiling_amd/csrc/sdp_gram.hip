@@ -109,6 +109,26 @@ __device__ __forceinline__ void conv4(int dt, const Raw4 &x, double out[4]) {
         out[m] = v;
     }
 }
+// The four common dtypes without a per-lane branch (lanes of one wave hold
+// different columns): both conversions of the 8-byte and of the 4-byte
+// interpretation are formed and selected.  Integer -> double is exact below
+// 2^53 and correctly rounded above (one rounding in the final add).
+__device__ __forceinline__ void conv4_common(bool is8, bool isf, const Raw4 &x, double out[4]) {
+    const uint32_t w[8] = {x.lo[0], x.lo[1], x.lo[2], x.lo[3], x.hi[0], x.hi[1], x.hi[2], x.hi[3]};
+#pragma unroll
+    for (int m = 0; m < 4; ++m) {
+        const uint32_t lo = w[2 * m], hi = w[2 * m + 1];
+        const double f64 = __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
+        const double i64 = __builtin_fma((double)(int32_t)hi, 4294967296.0, (double)lo);
+        const double f32 = (double)__uint_as_float(w[m]);
+        const double i32 = (double)(int32_t)w[m];
+        out[m] = is8 ? (isf ? f64 : i64) : (isf ? f32 : i32);
+    }
+}
+__device__ __forceinline__ bool common_dtype(int dt) {
+    return dt == SDP_F64 || dt == SDP_I64 || dt == SDP_F32 || dt == SDP_I32 || dt == 0;
+}
+
 // element-wise (the column's last rows); 0 beyond n and for dtype 0
 __device__ __forceinline__ void load4_tail(const GramCol &gc, int64_t r, int64_t n, double out[4]) {
 #pragma unroll
@@ -145,6 +165,17 @@ __global__ void __launch_bounds__(G_BLOCK) gram_kernel(const GramCol *cols, int 
         ka[a] = va[a] ? shift[ci] : 0.0;
         kb[a] = vb[a] ? shift[cj] : 0.0;
     }
+    // per-lane conversion selectors; `common` is wave-uniform
+    bool a8[NT], af[NT], b8[NT], bf[NT], all_common = true;
+#pragma unroll
+    for (int a = 0; a < NT; ++a) {
+        a8[a] = ca[a].width == 8 && ca[a].dtype != 0;
+        af[a] = ca[a].dtype == SDP_F64 || ca[a].dtype == SDP_F32;
+        b8[a] = cb[a].width == 8 && cb[a].dtype != 0;
+        bf[a] = cb[a].dtype == SDP_F64 || cb[a].dtype == SDP_F32;
+        all_common = all_common && common_dtype(ca[a].dtype) && common_dtype(cb[a].dtype);
+    }
+    const bool common = __all(all_common);
     d4 acc[NT][NT];
 #pragma unroll
     for (int a = 0; a < NT; ++a)
@@ -213,11 +244,20 @@ __global__ void __launch_bounds__(G_BLOCK) gram_kernel(const GramCol *cols, int 
 #pragma unroll
             for (int u = 0; u < UNR; ++u) {
                 double xa[NT][4], xb[NT][4];
+                if (common) {
 #pragma unroll
-                for (int a = 0; a < NT; ++a) conv4(ca[a].dtype, ra[u][a], xa[a]);
-                if (!diag) {
+                    for (int a = 0; a < NT; ++a) conv4_common(a8[a], af[a], ra[u][a], xa[a]);
+                    if (!diag) {
 #pragma unroll
-                    for (int b = 0; b < NT; ++b) conv4(cb[b].dtype, rbw[u][b], xb[b]);
+                        for (int b = 0; b < NT; ++b) conv4_common(b8[b], bf[b], rbw[u][b], xb[b]);
+                    }
+                } else {
+#pragma unroll
+                    for (int a = 0; a < NT; ++a) conv4(ca[a].dtype, ra[u][a], xa[a]);
+                    if (!diag) {
+#pragma unroll
+                        for (int b = 0; b < NT; ++b) conv4(cb[b].dtype, rbw[u][b], xb[b]);
+                    }
                 }
                 consume(xa, xb, rb + 16 * u + 4 * q, kw[u]);
             }
@@ -281,34 +321,54 @@ __global__ void __launch_bounds__(G_BLOCK) gram_kernel(const GramCol *cols, int 
     }
 }
 
+// Sum of the S chunk partials of every output entry.  A block owns R_EB
+// entries of one tile; each entry's S partials are split into R_P contiguous
+// parts summed by separate threads, and the parts are added in part order
+// (deterministic for a given S).  One thread per entry looping over S = 8192
+// partials took 7 ms; this takes well under 0.1 ms.
+constexpr int R_EB = 16;
+constexpr int R_P = 16;
+__device__ __forceinline__ double sum_parts(const double *base, int64_t stride, int S, double (*red)[R_EB]) {
+    const int el = threadIdx.x % R_EB, p = threadIdx.x / R_EB;
+    const int s0 = (int)((int64_t)S * p / R_P), s1 = (int)((int64_t)S * (p + 1) / R_P);
+    double v = 0.0;
+    for (int s = s0; s < s1; ++s) v += base[(int64_t)s * stride];
+    red[p][el] = v;
+    __syncthreads();
+    double tot = 0.0;
+    if (p == 0)
+        for (int k = 0; k < R_P; ++k) tot += red[k][el];
+    __syncthreads();
+    return tot;
+}
+
 template <int TILE>
-__global__ void gram_reduce_kernel(const double *part_g, const double *part_cs, const double *part_n, int ncols,
-                                   int ntiles_side, int T, int S, double *G, double *colsum, double *nout) {
-    const int t = blockIdx.x;
+__global__ void __launch_bounds__(R_EB * R_P) gram_reduce_kernel(const double *part_g, const double *part_cs,
+                                                                const double *part_n, int ncols, int ntiles_side,
+                                                                int T, int S, double *G, double *colsum, double *nout) {
+    constexpr int EGROUPS = TILE * TILE / R_EB;
+    __shared__ double red[R_P][R_EB];
+    const int t = blockIdx.x / EGROUPS, eg = blockIdx.x % EGROUPS;
     int ti = 0, rem = t;
     while (rem >= ntiles_side - ti) { rem -= ntiles_side - ti; ++ti; }
     const int tj = ti + rem;
-    for (int e = threadIdx.x; e < TILE * TILE; e += blockDim.x) {
+    const int el = threadIdx.x % R_EB, p = threadIdx.x / R_EB;
+    const int e = eg * R_EB + el;
+    const double v = sum_parts(part_g + (int64_t)t * TILE * TILE + e, (int64_t)T * TILE * TILE, S, red);
+    if (p == 0) {
         const int i = ti * TILE + e / TILE, j = tj * TILE + e % TILE;
-        if (i >= ncols || j >= ncols) continue;
-        double v = 0.0;
-        for (int s = 0; s < S; ++s) v += part_g[((int64_t)s * T + t) * TILE * TILE + e];
-        G[(int64_t)i * ncols + j] = v;
-        G[(int64_t)j * ncols + i] = v;
+        if (i < ncols && j < ncols) {
+            G[(int64_t)i * ncols + j] = v;
+            G[(int64_t)j * ncols + i] = v;
+        }
     }
-    if (ti == tj) {
-        for (int e = threadIdx.x; e < TILE; e += blockDim.x) {
-            const int i = ti * TILE + e;
-            if (i >= ncols) continue;
-            double v = 0.0;
-            for (int s = 0; s < S; ++s) v += part_cs[((int64_t)s * ntiles_side + ti) * TILE + e];
-            colsum[i] = v;
-        }
-        if (ti == 0 && threadIdx.x == 0) {
-            double v = 0.0;
-            for (int s = 0; s < S; ++s) v += part_n[s];
-            *nout = v;
-        }
+    if (ti == tj && eg < TILE / R_EB) {       // column sums of this diagonal tile
+        const double c = sum_parts(part_cs + (int64_t)ti * TILE + e, (int64_t)ntiles_side * TILE, S, red);
+        if (p == 0 && ti * TILE + e < ncols) colsum[ti * TILE + e] = c;
+    }
+    if (t == 0 && eg == 0) {                  // kept rows
+        const double c = sum_parts(part_n, 1, S, red);
+        if (threadIdx.x == 0) *nout = c;
     }
 }
 
@@ -435,15 +495,15 @@ extern "C" int sdp_gram(const sdp_column *cols, int32_t ncols, const uint32_t *d
     if (rc) return rc;
     switch (g.tile) {
     case 16:
-        hipLaunchKernelGGL(gram_reduce_kernel<16>, dim3(g.T), dim3(256), 0, s, pg, pcs, pn, ncols, g.side, g.T, g.S,
+        hipLaunchKernelGGL(gram_reduce_kernel<16>, dim3(g.T * (16 * 16 / R_EB)), dim3(R_EB * R_P), 0, s, pg, pcs, pn, ncols, g.side, g.T, g.S,
                            d_gram, d_colsum, d_n);
         break;
     case 32:
-        hipLaunchKernelGGL(gram_reduce_kernel<32>, dim3(g.T), dim3(256), 0, s, pg, pcs, pn, ncols, g.side, g.T, g.S,
+        hipLaunchKernelGGL(gram_reduce_kernel<32>, dim3(g.T * (32 * 32 / R_EB)), dim3(R_EB * R_P), 0, s, pg, pcs, pn, ncols, g.side, g.T, g.S,
                            d_gram, d_colsum, d_n);
         break;
     default:
-        hipLaunchKernelGGL(gram_reduce_kernel<64>, dim3(g.T), dim3(256), 0, s, pg, pcs, pn, ncols, g.side, g.T, g.S,
+        hipLaunchKernelGGL(gram_reduce_kernel<64>, dim3(g.T * (64 * 64 / R_EB)), dim3(R_EB * R_P), 0, s, pg, pcs, pn, ncols, g.side, g.T, g.S,
                            d_gram, d_colsum, d_n);
     }
     return check_launch("gram_reduce_kernel");
