@@ -159,6 +159,16 @@ int sdp_radix_hist(const uint64_t *d_keys, const uint64_t *d_n, uint64_t prefix,
 /* Keep keys whose bits >= shift equal `prefix`; append to d_out. */
 int sdp_radix_filter(const uint64_t *d_keys, const uint64_t *d_n, uint64_t prefix,
                      int32_t shift, uint64_t *d_out, uint64_t *d_out_n, void *stream);
+/* k-th smallest (0-based) of d_keys[:*d_n] (all within [lo_key, hi_key]) into
+ * *d_result, UINT64_MAX when k >= *d_n.  Every radix round's digit is chosen on
+ * the device, so the call queues its kernels without synchronising; n_cap
+ * bounds *d_n.  Single rank (sharded runs all-reduce per round through
+ * sdp_radix_hist / sdp_radix_filter).  Replaces the per-percentile Spark jobs
+ * of describe.py:203-208. */
+int64_t sdp_select_kth_workspace_bytes(int64_t n_cap);
+int sdp_select_kth(const uint64_t *d_keys, const uint64_t *d_n, int64_t n_cap, int64_t k,
+                   uint64_t lo_key, uint64_t hi_key, void *d_work, int64_t work_bytes,
+                   uint64_t *d_result, void *stream);
 /* Sort <= 16384 keys in place (one workgroup, LDS bitonic). */
 int sdp_sort_small(uint64_t *d_keys, const uint64_t *d_n, void *stream);
 /* Write the order-preserving keys of all na.drop rows (fallback select). */

@@ -611,6 +611,120 @@ __global__ void radix_filter_kernel(const uint64_t *keys, const uint64_t *n_ptr,
     }
 }
 
+// ---- device-driven k-th key (single rank) ----------------------------------------
+// The digit of every radix round is chosen on the GPU (radix_decide_kernel) from
+// a state the next round's kernels read, so a whole select -- up to six 11-bit
+// rounds -- is queued without a host round trip; the host reads the results of
+// all quantiles of a column at once.
+struct SelState {
+    uint64_t prefix;     // digits fixed so far (bits above shift + 11)
+    int64_t k;           // rank among the keys that match prefix
+    int32_t shift;       // bit position of the digit of the current round
+    int32_t done;
+    uint64_t result;
+};
+
+__global__ void select_init_kernel(SelState *st, uint64_t prefix, int64_t k, int shift, uint64_t *hist) {
+    if (threadIdx.x == 0) {
+        st->prefix = prefix;
+        st->k = k;
+        st->shift = shift;
+        st->done = 0;
+        st->result = EMPTY64;
+    }
+    for (int i = threadIdx.x; i < 2048; i += blockDim.x) hist[i] = 0;
+}
+
+__global__ void radix_hist_st_kernel(const uint64_t *keys, const uint64_t *n_ptr, const SelState *st,
+                                     uint64_t *hist) {
+    if (st->done) return;
+    __shared__ uint32_t h[2048];
+    for (int i = threadIdx.x; i < 2048; i += blockDim.x) h[i] = 0;
+    __syncthreads();
+    const uint64_t n = *n_ptr, prefix = st->prefix;
+    const int shift = st->shift, top = shift + 11;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t k = keys[i];
+        if (top >= 64 || (k >> top) == prefix) atomicAdd(&h[(k >> shift) & 2047u], 1u);
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < 2048; i += blockDim.x)
+        if (h[i]) atomicAdd((unsigned long long *)&hist[i], (unsigned long long)h[i]);
+}
+
+// one workgroup of 1024 threads: digit j with cum[j-1] <= k < cum[j]; the
+// histogram and the next round's output counter are cleared for the next round
+__global__ void __launch_bounds__(1024) radix_decide_kernel(uint64_t *hist, SelState *st, uint64_t *next_n,
+                                                            uint64_t *result) {
+    if (st->done) return;
+    __shared__ uint64_t s[1024];
+    __shared__ int s_j;
+    __shared__ uint64_t s_before;
+    const int t = threadIdx.x;
+    const uint64_t a = hist[2 * t], b = hist[2 * t + 1];
+    s[t] = a + b;
+    if (t == 0) { s_j = -1; s_before = 0; }
+    __syncthreads();
+    for (int o = 1; o < 1024; o <<= 1) {        // inclusive scan of the pair sums
+        const uint64_t v = t >= o ? s[t - o] : 0;
+        __syncthreads();
+        s[t] += v;
+        __syncthreads();
+    }
+    const uint64_t k = (uint64_t)st->k;
+    const uint64_t excl = s[t] - a - b;
+    if (excl <= k && k < s[t]) {
+        s_j = k < excl + a ? 2 * t : 2 * t + 1;
+        s_before = k < excl + a ? excl : excl + a;
+    }
+    __syncthreads();
+    hist[2 * t] = 0;
+    hist[2 * t + 1] = 0;
+    if (t == 0) {
+        if (s_j < 0) {                          // k beyond the keys: no such rank
+            st->done = 1;
+            st->result = EMPTY64;
+            if (result) *result = EMPTY64;
+        } else {
+            st->k = (int64_t)(k - s_before);
+            st->prefix = (st->shift + 11 >= 64 ? 0ull : (st->prefix << 11)) | (uint64_t)s_j;
+            if (st->shift == 0) {
+                st->done = 1;
+                st->result = st->prefix;
+                if (result) *result = st->prefix;
+            } else {
+                st->shift -= 11;
+            }
+        }
+        if (next_n) *next_n = 0;
+    }
+}
+
+__global__ void radix_filter_st_kernel(const uint64_t *keys, const uint64_t *n_ptr, const SelState *st,
+                                       uint64_t *out, uint64_t *out_n) {
+    if (st->done) return;
+    __shared__ uint64_t s_buf[STAGE];
+    __shared__ uint32_t s_cnt;
+    __shared__ uint64_t s_gbase;
+    if (threadIdx.x == 0) s_cnt = 0;
+    __syncthreads();
+    Stager sg{s_buf, &s_cnt, &s_gbase};
+    const uint64_t n = *n_ptr, prefix = st->prefix;
+    const int top = st->shift + 11;
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    const uint64_t iters = (n + stride - 1) / stride;
+    for (uint64_t it = 0; it < iters; ++it) {
+        const uint64_t i = it * stride + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+        uint64_t k = 0;
+        bool keep = false;
+        if (i < n) {
+            k = keys[i];
+            keep = top >= 64 ? true : ((k >> top) == prefix);
+        }
+        stage_push(sg, keep, k, out, (unsigned long long *)out_n, it + 1 == iters);
+    }
+}
+
 __global__ void __launch_bounds__(1024) sort_small_kernel(uint64_t *keys, const uint64_t *n_ptr) {
     __shared__ uint64_t s[SORT_MAX];
     const int n = (int)min((uint64_t)SORT_MAX, *n_ptr);
@@ -915,6 +1029,48 @@ extern "C" int sdp_radix_filter(const uint64_t *d_keys, const uint64_t *d_n, uin
     hipLaunchKernelGGL(radix_filter_kernel, dim3(512), dim3(256), 0, (hipStream_t)stream, d_keys, d_n, prefix,
                        shift, d_out, d_out_n);
     return check_launch("radix_filter_kernel");
+}
+
+static int64_t sel_align(int64_t x) { return (x + 255) / 256 * 256; }
+
+extern "C" int64_t sdp_select_kth_workspace_bytes(int64_t n_cap) {
+    if (n_cap < 0) return -1;
+    return sel_align(sizeof(SelState)) + sel_align(2048 * 8) + 2 * sel_align(8) + 2 * sel_align(8 * (n_cap > 0 ? n_cap : 1));
+}
+
+extern "C" int sdp_select_kth(const uint64_t *d_keys, const uint64_t *d_n, int64_t n_cap, int64_t k,
+                              uint64_t lo_key, uint64_t hi_key, void *d_work, int64_t work_bytes,
+                              uint64_t *d_result, void *stream) {
+    if (n_cap < 0 || k < 0 || d_result == nullptr) return set_error(SDP_EINVAL, "sdp_select_kth: args");
+    if (work_bytes < sdp_select_kth_workspace_bytes(n_cap)) return set_error(SDP_ECAP, "sdp_select_kth: workspace");
+    char *w = (char *)d_work;
+    SelState *st = (SelState *)w;
+    w += sel_align(sizeof(SelState));
+    uint64_t *hist = (uint64_t *)w;
+    w += sel_align(2048 * 8);
+    uint64_t *cnt[2] = {(uint64_t *)w, (uint64_t *)(w + sel_align(8))};
+    w += 2 * sel_align(8);
+    uint64_t *buf[2] = {(uint64_t *)w, (uint64_t *)(w + sel_align(8 * (n_cap > 0 ? n_cap : 1)))};
+    const uint64_t x = lo_key ^ hi_key;
+    const int shift0 = x ? ((63 - __builtin_clzll(x)) / 11) * 11 : 0;
+    const uint64_t prefix0 = shift0 + 11 < 64 ? (lo_key >> (shift0 + 11)) : 0ull;
+    hipStream_t s = (hipStream_t)stream;
+    hipLaunchKernelGGL(select_init_kernel, dim3(1), dim3(256), 0, s, st, prefix0, k, shift0, hist);
+    int rc = check_launch("select_init_kernel");
+    if (rc) return rc;
+    const uint64_t *cur = d_keys, *cur_n = d_n;
+    for (int shift = shift0, r = 0;; shift -= 11, ++r) {
+        hipLaunchKernelGGL(radix_hist_st_kernel, dim3(512), dim3(256), 0, s, cur, cur_n, st, hist);
+        hipLaunchKernelGGL(radix_decide_kernel, dim3(1), dim3(1024), 0, s, hist, st, shift ? cnt[r & 1] : nullptr,
+                           d_result);
+        if ((rc = check_launch("radix_decide_kernel"))) return rc;
+        if (shift == 0) break;
+        hipLaunchKernelGGL(radix_filter_st_kernel, dim3(512), dim3(256), 0, s, cur, cur_n, st, buf[r & 1], cnt[r & 1]);
+        if ((rc = check_launch("radix_filter_st_kernel"))) return rc;
+        cur = buf[r & 1];
+        cur_n = cnt[r & 1];
+    }
+    return 0;
 }
 
 extern "C" int sdp_sort_small(uint64_t *d_keys, const uint64_t *d_n, void *stream) {

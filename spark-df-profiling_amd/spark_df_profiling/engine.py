@@ -234,6 +234,8 @@ class Engine:
 
     def merge_pass1(self, local: nat.SdpPass1Result):
         """All-gather the per-rank pass-1 states and merge them in rank order."""
+        if self.comm.world == 1:
+            return merge_pass1_results([local])
         raw = torch.frombuffer(bytearray(bytes(local)), dtype=torch.uint8).to(self.device)
         parts = [nat.SdpPass1Result.from_buffer_copy(p.cpu().numpy().tobytes()) for p in self.comm.allgather(raw)]
         return merge_pass1_results(parts)
@@ -298,6 +300,7 @@ class Engine:
         dense = {}
         values = {}
         fallback = None
+        queued = []              # single rank: (rank, arr, arr_n, n_cap, k, lo, hi), selected on the device
         for r in ranks:
             key = None
             for w in range(nw):
@@ -314,7 +317,11 @@ class Engine:
                         if w not in dense:
                             dense[w] = self._compact(cand_info, w)
                         arr, arr_n = dense[w]
-                        key = self.select_kth(arr, arr_n, rr - p1['w_eq_lo'][w], lo, hi)
+                        if self.comm.world == 1:
+                            queued.append((r, arr, arr_n, arr.numel(), rr - p1['w_eq_lo'][w], lo, hi))
+                            key = 'queued'
+                        else:
+                            key = self.select_kth(arr, arr_n, rr - p1['w_eq_lo'][w], lo, hi)
                     else:
                         key = hi
                     break
@@ -322,8 +329,22 @@ class Engine:
                 if fallback is None:
                     fallback = self._all_keys(col)
                 arr, arr_n = fallback
-                key = self.select_kth(arr, arr_n, r, 0, EMPTY64)
+                if self.comm.world == 1:
+                    queued.append((r, arr, arr_n, arr.numel(), r, 0, EMPTY64))
+                    key = 'queued'
+                else:
+                    key = self.select_kth(arr, arr_n, r, 0, EMPTY64)
             values[r] = key
+        if queued:
+            # every select of the column runs back to back on the stream; one readback
+            cap = max(q[3] for q in queued)
+            work = self._bytes(sdp.sdp_select_kth_workspace_bytes(cap))
+            res = self._u64(len(queued))
+            for i, (r, arr, arr_n, ncap, kk, lo, hi) in enumerate(queued):
+                sdp.sdp_select_kth(ptr(arr), ptr(arr_n), ncap, int(kk), _u(lo), _u(hi), ptr(work), work.numel(),
+                                   ptr(res[i:]), self._s())
+            for (r, *_), key in zip(queued, self._host_u64(res)):
+                values[r] = key
         out = {}
         for p in probs:
             pos, lo_r, hi_r = needed[p]
@@ -339,7 +360,10 @@ class Engine:
 
     def _compact(self, cand_info, w):
         nseg, cap = cand_info['nseg'], cand_info['cap']
-        out = self._u64(max(1, int(cand_info['counts'][w * nseg:(w + 1) * nseg].sum().item())))
+        if self.comm.world == 1:     # sized by the slot capacity: no readback of the counts
+            out = self._u64(max(1, nseg * cap))
+        else:
+            out = self._u64(max(1, int(cand_info['counts'][w * nseg:(w + 1) * nseg].sum().item())))
         out_n = self._u64(1, zero=True)
         base = cand_info['cand'][w * nseg * cap:]
         sdp.sdp_compact_candidates(ptr(base), ptr(cand_info['counts'][w * nseg:]), nseg, cap,
@@ -367,6 +391,9 @@ class Engine:
         sdp.sdp_pass2(ctypes.byref(cs), float(mean), ptr(e), bins, int(mono), float(hi_t), float(lo_t), ptr(work),
                       work.numel(), ptr(res), ptr(hist), self._s())
         r = self._read(res, nat.SdpPass2Result)
+        if self.comm.world == 1:
+            return {'abs_dev_sum': float(r.abs_dev_sum), 'n_high': int(r.n_high), 'n_low': int(r.n_low),
+                    'n_unbinned': int(r.n_unbinned), 'hist': hist.cpu().numpy().astype(np.int64)}
         # merge ranks: counts sum exactly; abs-dev sums gathered and added in rank order
         vec = torch.tensor([r.n_high, r.n_low, r.n_unbinned], dtype=torch.int64, device=self.device)
         vec = self.comm.allreduce_sum(torch.cat([vec, hist]))
