@@ -951,15 +951,18 @@ constexpr int WV_W = 4;                 // waves per workgroup
 constexpr int WV_SLOTS = 2048;          // table slots per wave (16 KB)
 constexpr int WV_Q = 20;                // records per lane per batch
 constexpr int WV_BATCH = WV_Q * WAVE;   // 1280
-template <bool LIMIT>
-__device__ __forceinline__ uint32_t wave_insert_batch(uint64_t *T, const uint64_t *in_h, int64_t rb, int64_t hi,
-                                                      int lane, bool &full) {
-    uint64_t hq[WV_Q];
+__device__ __forceinline__ void wave_load_batch(uint64_t (&hq)[WV_Q], const uint64_t *in_h, int64_t rb, int64_t hi,
+                                                int lane) {
 #pragma unroll
     for (int q = 0; q < WV_Q; ++q) {
         const int64_t r = rb + (int64_t)q * WAVE + lane;
         hq[q] = r < hi ? in_h[r] : EMPTY64;
     }
+}
+// inserts this lane's records of the batch starting at rb (loaded by wave_load_batch)
+template <bool LIMIT>
+__device__ __forceinline__ uint32_t wave_insert_regs(uint64_t *T, uint64_t (&hq)[WV_Q], int64_t rb, int64_t hi,
+                                                     int lane, bool &full) {
     const int64_t rem = hi - rb - lane;
     int left = rem <= 0 ? 0 : (int)min((int64_t)WV_Q, (rem + WAVE - 1) / WAVE);
     uint64_t x = 0;
@@ -989,6 +992,8 @@ __device__ __forceinline__ uint32_t wave_insert_batch(uint64_t *T, const uint64_
     return fresh;
 }
 
+// The first batch of the wave's next bucket is loaded before the current bucket
+// is inserted, so its memory latency overlaps the LDS probing.
 __global__ void __launch_bounds__(WV_W * WAVE) part_dedup_u64_wave_kernel(const uint64_t *in_h,
                                                                           const uint64_t *starts,
                                                                           int64_t nbuckets, uint64_t *stats) {
@@ -997,20 +1002,49 @@ __global__ void __launch_bounds__(WV_W * WAVE) part_dedup_u64_wave_kernel(const 
     uint64_t *T = tab[w];
     uint64_t groups = 0;
     bool full = false;
-    for (int64_t f = (int64_t)blockIdx.x * WV_W + w; f < nbuckets; f += (int64_t)gridDim.x * WV_W) {
-        const int64_t lo = starts[f], hi = starts[f + 1];
-        if (lo == hi) continue;
-#pragma unroll
-        for (int k = 0; k < WV_SLOTS / WAVE; ++k) T[k * WAVE + lane] = EMPTY64;
-        __builtin_amdgcn_wave_barrier();
-        uint32_t fresh = 0;
-        if (hi - lo <= WV_BATCH) {
-            fresh = wave_insert_batch<false>(T, in_h, lo, hi, lane, full);
-        } else {
-            for (int64_t rb = lo; rb < hi; rb += WV_BATCH) fresh += wave_insert_batch<true>(T, in_h, rb, hi, lane, full);
+    const int64_t stride = (int64_t)gridDim.x * WV_W;
+    int64_t f = (int64_t)blockIdx.x * WV_W + w;
+    int64_t lo = 0, hi = 0;
+    uint64_t hq[WV_Q];
+    if (f < nbuckets) {
+        lo = starts[f];
+        hi = starts[f + 1];
+        wave_load_batch(hq, in_h, lo, hi, lane);
+    }
+    uint64_t hn[WV_Q];
+    // one step: prefetch bucket fn into `nxt`, insert bucket f from `cur`
+    auto step = [&](uint64_t (&cur)[WV_Q], uint64_t (&nxt)[WV_Q]) {
+        const int64_t fn = f + stride;
+        int64_t lo_n = 0, hi_n = 0;
+        if (fn < nbuckets) {
+            lo_n = starts[fn];
+            hi_n = starts[fn + 1];
+            wave_load_batch(nxt, in_h, lo_n, hi_n, lane);
         }
-        groups += fresh;
-        __builtin_amdgcn_wave_barrier();
+        if (lo != hi) {
+#pragma unroll
+            for (int k = 0; k < WV_SLOTS / WAVE; ++k) T[k * WAVE + lane] = EMPTY64;
+            __builtin_amdgcn_wave_barrier();
+            uint32_t fresh = 0;
+            if (hi - lo <= WV_BATCH) {
+                fresh = wave_insert_regs<false>(T, cur, lo, hi, lane, full);
+            } else {
+                for (int64_t rb = lo; rb < hi; rb += WV_BATCH) {
+                    if (rb != lo) wave_load_batch(cur, in_h, rb, hi, lane);
+                    fresh += wave_insert_regs<true>(T, cur, rb, hi, lane, full);
+                }
+            }
+            groups += fresh;
+            __builtin_amdgcn_wave_barrier();
+        }
+        lo = lo_n;
+        hi = hi_n;
+        f = fn;
+    };
+    while (f < nbuckets) {
+        step(hq, hn);
+        if (f >= nbuckets) break;
+        step(hn, hq);
     }
     groups = wave_sum_u64(groups);
     const bool any_full = __any(full);
