@@ -175,7 +175,7 @@ struct P1Partial {
 };
 
 struct P1Thread {
-    uint32_t count, n_valid, n_nan, n_zero;
+    uint32_t count, n_valid, n_nan, n_zero, n_skip;
     int64_t isum, imin, imax;
     double dmin, dmax;
     double s1, s1c, s2, s3, s3c, s4;
@@ -187,12 +187,10 @@ constexpr int P1_WPB = 4;            // waves per pass-1 block (P1_BLOCK / WAVE)
 
 struct P1Ctx {
     uint64_t lo[SDP_MAX_WINDOWS], hi[SDP_MAX_WINDOWS];
+    uint64_t *seg[SDP_MAX_WINDOWS];   // this wave's candidate slot range of window w
     int nw;
     double K;
-    uint64_t *cand;           // [nw][grid][P1_WPB][cap]: one slot range per wave
     int64_t cap;
-    int grid;
-    bool hne[SDP_MAX_WINDOWS]; // hi != lo
 };
 
 // U 16-byte vectors per thread of a grid-strided tile (+ their validity bits).
@@ -221,6 +219,12 @@ struct VecTile {
 };
 
 // One element; every lane of the wave calls this in lockstep (ballots inside).
+// Window counts use the key with skipped elements (null, NaN, padding) mapped
+// to key 0: no skipped element is above a bound or strictly inside a window,
+// and the ones counted as equal to a bound of 0 are taken off in the block
+// epilogue (n_skip), as are eqhi counts of windows with lo == hi -- so each
+// window costs two compare-and-carry counts, one equality count and the
+// inside test, with no per-element validity masking.
 template <typename T>
 __device__ __forceinline__ void p1_elem(P1Thread &st, const P1Ctx &cx, T x, bool valid) {
     const double xd = Elem<T>::d(x);
@@ -228,7 +232,7 @@ __device__ __forceinline__ void p1_elem(P1Thread &st, const P1Ctx &cx, T x, bool
     const bool ok = valid && !isnan_;
     st.n_valid += valid;
     st.n_nan += (valid && isnan_);
-    uint64_t key = 0;
+    st.n_skip += !ok;
     if (ok) {
         st.count += 1;
         if (Elem<T>::is_float) {
@@ -247,27 +251,26 @@ __device__ __forceinline__ void p1_elem(P1Thread &st, const P1Ctx &cx, T x, bool
         st.s2 += d2;
         two_sum_acc(st.s3, st.s3c, d2 * d);
         st.s4 = fma(d2, d2, st.s4);
-        key = Elem<T>::key(x);
     }
+    const uint64_t key = ok ? Elem<T>::key(x) : 0ull;
+    // Every window slot is evaluated: unused ones have lo = hi = UINT64_MAX
+    // (nothing inside, nothing above; their counts are never read), which
+    // keeps the loop free of per-window branches.
 #pragma unroll
     for (int w = 0; w < SDP_MAX_WINDOWS; ++w) {
-        if (w < cx.nw) {
-            const uint64_t lo = cx.lo[w], hi = cx.hi[w];
-            st.gt[w] += (ok && key > hi);
-            st.eqlo[w] += (ok && key == lo);
-            st.eqhi[w] += (ok && key == hi && cx.hne[w]);
-            const bool inside = ok && key > lo && key < hi;
-            const uint64_t m = __ballot(inside);
-            if (m) {   // wave-uniform; no atomics: this wave owns its slot range
-                if (inside) {
-                    const uint32_t pos = st.wcur[w] + (uint32_t)lane_rank(m);
-                    if ((int64_t)pos < cx.cap) {
-                        const int64_t seg = ((int64_t)w * cx.grid + blockIdx.x) * P1_WPB + (threadIdx.x / WAVE);
-                        cx.cand[seg * cx.cap + pos] = key;
-                    }
-                }
-                st.wcur[w] += (uint32_t)__popcll(m);
+        const uint64_t lo = cx.lo[w], hi = cx.hi[w];
+        st.gt[w] += (uint32_t)(key > hi);
+        st.eqlo[w] += (uint32_t)(key == lo);
+        st.eqhi[w] += (uint32_t)(key == hi);
+        // lane masks straight from the compares (no bool round trip through a VGPR)
+        const uint64_t m = __builtin_amdgcn_uicmpl(key, lo, 34 /*UGT*/) & __builtin_amdgcn_uicmpl(key, hi, 36 /*ULT*/);
+        if (m) {   // wave-uniform; no atomics: this wave owns its slot range
+            const uint32_t c = st.wcur[w];
+            if ((m >> lane_id()) & 1u) {
+                const uint32_t pos = c + (uint32_t)lane_rank(m);
+                if ((int64_t)pos < cx.cap) cx.seg[w][pos] = key;
             }
+            st.wcur[w] = c + (uint32_t)__popcll(m);
         }
     }
 }
@@ -282,17 +285,16 @@ __global__ void __launch_bounds__(P1_BLOCK, 4) pass1_kernel(sdp_column col, cons
     cx.nw = plan->n_windows;
 #pragma unroll
     for (int w = 0; w < SDP_MAX_WINDOWS; ++w) {
-        cx.lo[w] = plan->lo[w];
-        cx.hi[w] = plan->hi[w];
-        cx.hne[w] = cx.hi[w] != cx.lo[w];
+        cx.lo[w] = w < cx.nw ? plan->lo[w] : EMPTY64;
+        cx.hi[w] = w < cx.nw ? plan->hi[w] : EMPTY64;
+        const int64_t seg = ((int64_t)w * gridDim.x + blockIdx.x) * P1_WPB + (threadIdx.x / WAVE);
+        cx.seg[w] = cand + seg * cap;
     }
     cx.K = plan->shift;
-    cx.cand = cand;
     cx.cap = cap;
-    cx.grid = gridDim.x;
 
     P1Thread st;
-    st.count = st.n_valid = st.n_nan = st.n_zero = 0;
+    st.count = st.n_valid = st.n_nan = st.n_zero = st.n_skip = 0;
     st.isum = 0;
     st.imin = INT64_MAX;
     st.imax = INT64_MIN;
@@ -352,11 +354,15 @@ __global__ void __launch_bounds__(P1_BLOCK, 4) pass1_kernel(sdp_column col, cons
             s_i[wid][0] = isum; s_i[wid][1] = imn; s_i[wid][2] = imx;
             s_u[wid][0] = c0; s_u[wid][1] = c1; s_u[wid][2] = c2; s_u[wid][3] = c3;
         }
+        const uint64_t skip = wave_sum_u64(st.n_skip);
 #pragma unroll
         for (int w = 0; w < W_; ++w) {
             const uint64_t g = wave_sum_u64(st.gt[w]);
-            const uint64_t e1 = wave_sum_u64(st.eqlo[w]);
-            const uint64_t e2 = wave_sum_u64(st.eqhi[w]);
+            uint64_t e1 = wave_sum_u64(st.eqlo[w]);
+            uint64_t e2 = wave_sum_u64(st.eqhi[w]);
+            if (cx.lo[w] == 0) e1 -= skip;                  // skipped elements carry key 0
+            if (cx.hi[w] == 0) e2 -= skip;
+            if (cx.hi[w] == cx.lo[w]) e2 = 0;               // one bound: counted as eqlo only
             if (lane == 0) {
                 s_u[wid][4 + w] = g; s_u[wid][4 + W_ + w] = e1; s_u[wid][4 + 2 * W_ + w] = e2;
                 s_u[wid][4 + 3 * W_ + w] = st.wcur[w];

@@ -17,6 +17,7 @@ e = Engine()
 col = cols[sys.argv[4]] if len(sys.argv) > 4 else cols['f64_norm']
 torch.cuda.synchronize()
 for r in range(reps):
+    rec = nat.start_recording() if r == reps - 1 else None
     t0 = time.perf_counter()
     if what == 'group':
         e.group(col, col.kind == 'bytes', dense=False)
@@ -31,3 +32,7 @@ for r in range(reps):
         e.gram(num, [0.0] * len(num), [False] * len(num))
     torch.cuda.synchronize()
     print(what, col.name, 'rep', r, '%.2f ms' % ((time.perf_counter() - t0) * 1e3), flush=True)
+    if rec is not None:
+        nat.stop_recording()
+        for k, v in rec.items():
+            print('   %-40s %8.3f ms x%d' % (k, sum(a.elapsed_time(b) for a, b, _ in v), len(v)))
