@@ -230,11 +230,9 @@ def roofline(rec, steps, step_s, prof_bytes):
 # CPU baseline: the oracle (CPU restatement, not reference Spark) on a sample
 # ----------------------------------------------------------------------------
 
-def cpu_baseline(sample_rows, device):
+def shard_to_arrow(shard):
+    """A device table of the C3 generator as a host Arrow table (same values)."""
     import pyarrow as pa
-    import oracle
-    sys.path.insert(0, ROOT)
-    shard = make_c3_shard(sample_rows, 0, 1, device)
     arrays = {}
     for c in shard.columns:
         n = c.length
@@ -249,7 +247,14 @@ def cpu_baseline(sample_rows, device):
         else:
             arr = pa.array(c.values.cpu().numpy(), mask=~valid)
         arrays[c.name] = arr
-    table = pa.table(arrays)
+    return pa.table(arrays)
+
+
+def cpu_baseline(sample_rows, device):
+    import oracle
+    sys.path.insert(0, ROOT)
+    shard = make_c3_shard(sample_rows, 0, 1, device)
+    table = shard_to_arrow(shard)
     del shard
     torch.cuda.empty_cache()
     t0 = time.perf_counter()

@@ -170,13 +170,26 @@ class DeviceTable:
     def slice_rows(self, start, stop):
         return DeviceTable([c.slice_rows(start, stop) for c in self.columns], stop - start)
 
+    STREAM_MIN_ROWS = 1 << 16
+
     @classmethod
-    def from_arrow(cls, table, device=None):
+    def from_arrow(cls, table, device=None, streamed=None):
+        """Upload an Arrow table.  Tables of >= STREAM_MIN_ROWS rows (or with
+        streamed=True) go through the pinned double-buffered staging pipeline
+        (ingest.py); small ones column by column."""
         if isinstance(table, pa.RecordBatch):
             table = pa.Table.from_batches([table])
         device = torch.device(device or 'cuda')
+        if streamed or (streamed is None and table.num_rows >= cls.STREAM_MIN_ROWS):
+            from .ingest import from_arrow_streamed
+            return from_arrow_streamed(table, device)
         cols = [column_from_arrow(name, table.column(name), device) for name in table.column_names]
         return cls(cols, table.num_rows)
+
+    @classmethod
+    def from_parquet(cls, path, columns=None, device=None, **kw):
+        from .ingest import from_parquet
+        return from_parquet(path, columns=columns, device=device, **kw)
 
 
 # ----------------------------------------------------------------------------

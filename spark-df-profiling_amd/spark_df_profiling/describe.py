@@ -45,6 +45,10 @@ def as_device_table(df, device=None) -> DeviceTable:
         return df
     if isinstance(df, (pa.Table, pa.RecordBatch)):
         return DeviceTable.from_arrow(df, device)
+    import os
+    if isinstance(df, (str, os.PathLike)) and str(df).endswith('.parquet'):
+        # the reference's inputs come from spark.read.parquet (examples/Demo.ipynb:63)
+        return DeviceTable.from_parquet(str(df), device=device)
     # Spark DataFrame (pyspark optional): collect as Arrow, never row by row
     to_arrow = getattr(df, 'toArrow', None) or getattr(df, '_collect_as_arrow', None)
     if to_arrow is not None and type(df).__module__.startswith('pyspark'):
@@ -52,7 +56,7 @@ def as_device_table(df, device=None) -> DeviceTable:
         if isinstance(got, list):
             got = pa.Table.from_batches(got)
         return DeviceTable.from_arrow(got, device)
-    raise TypeError('df must be of type pyspark.sql.DataFrame, pyarrow.Table or DeviceTable')
+    raise TypeError('df must be of type pyspark.sql.DataFrame, pyarrow.Table, a .parquet path or DeviceTable')
 
 
 def _series(values, col: DeviceColumn) -> pd.Series:
