@@ -772,9 +772,11 @@ __global__ void column_keys_kernel(sdp_column col, uint64_t *out, uint64_t *out_
 constexpr int P2_BLOCK = 256;
 constexpr int P2_UNROLL = 4;
 
+constexpr int P2_SMALL_BINS = 16;
 struct P2Ctx {
     double mean, hi_t, lo_t, e0, inv_w;
     const double *edges;      // LDS copy
+    double ev[P2_SMALL_BINS]; // the edges again, wave-uniform (SGPRs), for the cumulative path
     int bins;
     bool monotone;
 };
@@ -798,15 +800,19 @@ __device__ __forceinline__ int case_bin(const P2Ctx &c, double x) {
     return -1;
 }
 
-constexpr int P2_SMALL_BINS = 16;
 
 struct P2Thread {
     double mad;
-    uint32_t high, low, unbinned;
+    uint32_t high, low, unbinned, okc;
     uint32_t bc[P2_SMALL_BINS];       // wave-uniform bin counts (SGPRs) for bins <= 16
 };
 
-template <typename T, bool SMALL>
+// SMALL: <= 16 bins counted per wave with ballots.  MONO (finite non-decreasing
+// edges): bc[j] counts x >= e_j, one compare against a wave-uniform edge per
+// bin and no bin search; the CASE-WHEN bins are differences of these
+// cumulative counts (bin j = [e_j, e_j+1), last bin x >= e_b-1, x < e_0 unbinned),
+// formed once per wave in the epilogue.
+template <typename T, bool SMALL, bool MONO>
 __device__ __forceinline__ void p2_elem(P2Thread &st, const P2Ctx &c, uint32_t *lds_hist, T x,
                                         bool valid) {
     const double xd = Elem<T>::d(x);
@@ -815,6 +821,14 @@ __device__ __forceinline__ void p2_elem(P2Thread &st, const P2Ctx &c, uint32_t *
     if (valid) {
         st.high += spark_gt(xd, c.hi_t);
         st.low += spark_lt(xd, c.lo_t);
+    }
+    if (SMALL && MONO) {
+        st.okc += ok;
+        if (ok) st.mad += fabs(xd - c.mean);
+#pragma unroll
+        for (int j = 0; j < P2_SMALL_BINS; ++j)
+            if (j < c.bins) st.bc[j] += (uint32_t)__popcll(__ballot(ok && xd >= c.ev[j]));
+        return;
     }
     int bin = -1;
     if (ok) {
@@ -832,7 +846,7 @@ __device__ __forceinline__ void p2_elem(P2Thread &st, const P2Ctx &c, uint32_t *
     }
 }
 
-template <typename T, bool SMALL>
+template <typename T, bool SMALL, bool MONO>
 __global__ void __launch_bounds__(P2_BLOCK, 4) pass2_kernel(sdp_column col, double mean, const double *edges,
                                                          int bins, int monotone, double hi_t, double lo_t,
                                                          double *part_mad, uint64_t *part_cnt) {
@@ -846,12 +860,14 @@ __global__ void __launch_bounds__(P2_BLOCK, 4) pass2_kernel(sdp_column col, doub
     c.mean = mean; c.hi_t = hi_t; c.lo_t = lo_t; c.edges = s_edges; c.bins = bins;
     c.monotone = monotone != 0;
     c.e0 = s_edges[0];
+#pragma unroll
+    for (int j = 0; j < P2_SMALL_BINS; ++j) c.ev[j] = (MONO && j < bins) ? edges[j] : 0.0;   // uniform loads
     {
         const double w = (bins > 1) ? (s_edges[bins - 1] - s_edges[0]) / (double)(bins - 1) : 0.0;
         c.inv_w = (w > 0.0) ? 1.0 / w : 0.0;
     }
     P2Thread st;
-    st.mad = 0.0; st.high = st.low = st.unbinned = 0;
+    st.mad = 0.0; st.high = st.low = st.unbinned = st.okc = 0;
 #pragma unroll
     for (int j = 0; j < P2_SMALL_BINS; ++j) st.bc[j] = 0;
 
@@ -871,7 +887,7 @@ __global__ void __launch_bounds__(P2_BLOCK, 4) pass2_kernel(sdp_column col, doub
 #pragma unroll
         for (int u = 0; u < U; ++u)
 #pragma unroll
-            for (int e = 0; e < VPT; ++e) p2_elem<T, SMALL>(st, c, s_hist, cur.v[u].v[e], (cur.vb[u] >> e) & 1u);
+            for (int e = 0; e < VPT; ++e) p2_elem<T, SMALL, MONO>(st, c, s_hist, cur.v[u].v[e], (cur.vb[u] >> e) & 1u);
         if (more) cur = nxt;
     }
     if (blockIdx.x == 0 && threadIdx.x < WAVE) {
@@ -879,14 +895,21 @@ __global__ void __launch_bounds__(P2_BLOCK, 4) pass2_kernel(sdp_column col, doub
         const bool inb = i < n;
         T x = inb ? ((const T *)col.d_values)[i] : (T)0;
         const bool valid = inb && valid_bit(col.d_validity, col.validity_bit_offset, i);
-        p2_elem<T, SMALL>(st, c, s_hist, x, valid);
+        p2_elem<T, SMALL, MONO>(st, c, s_hist, x, valid);
     }
     // ---- block reduction (fixed order) ----
     __shared__ double s_mad[P2_BLOCK / WAVE];
     __shared__ uint64_t s_u[P2_BLOCK / WAVE][3];
     const int wid = threadIdx.x / WAVE, lane = lane_id();
     const double mad = wave_sum_f64(st.mad);
-    const uint64_t hi = wave_sum_u64(st.high), lo = wave_sum_u64(st.low), ub = wave_sum_u64(st.unbinned);
+    const uint64_t hi = wave_sum_u64(st.high), lo = wave_sum_u64(st.low);
+    uint64_t ub = wave_sum_u64(st.unbinned);
+    if (SMALL && MONO) {                // cumulative counts -> CASE-WHEN bins (wave-uniform)
+        ub = wave_sum_u64(st.okc) - st.bc[0];
+#pragma unroll
+        for (int j = 0; j < P2_SMALL_BINS - 1; ++j)
+            if (j + 1 < bins) st.bc[j] -= st.bc[j + 1];
+    }
     if (lane == 0) { s_mad[wid] = mad; s_u[wid][0] = hi; s_u[wid][1] = lo; s_u[wid][2] = ub; }
     if (SMALL && lane == 0) {
 #pragma unroll
@@ -1107,14 +1130,18 @@ extern "C" int sdp_pass2(const sdp_column *col, double mean, const double *d_edg
     uint64_t *pc = (uint64_t *)((char *)d_work + (int64_t)grid * sizeof(double));
     const size_t lds = (size_t)bins * (sizeof(double) + sizeof(uint32_t)) + 16;
     hipStream_t s = (hipStream_t)stream;
-    if (bins <= P2_SMALL_BINS) {
+    if (bins <= P2_SMALL_BINS && edges_monotone) {
         SDP_DISPATCH_NUMERIC(col->dtype,
-            hipLaunchKernelGGL((pass2_kernel<T, true>), dim3(grid), dim3(P2_BLOCK), lds, s, *col, mean, d_edges,
-                               bins, edges_monotone, hi_t, lo_t, pm, pc));
+            hipLaunchKernelGGL((pass2_kernel<T, true, true>), dim3(grid), dim3(P2_BLOCK), lds, s, *col, mean,
+                               d_edges, bins, edges_monotone, hi_t, lo_t, pm, pc));
+    } else if (bins <= P2_SMALL_BINS) {
+        SDP_DISPATCH_NUMERIC(col->dtype,
+            hipLaunchKernelGGL((pass2_kernel<T, true, false>), dim3(grid), dim3(P2_BLOCK), lds, s, *col, mean,
+                               d_edges, bins, edges_monotone, hi_t, lo_t, pm, pc));
     } else {
         SDP_DISPATCH_NUMERIC(col->dtype,
-            hipLaunchKernelGGL((pass2_kernel<T, false>), dim3(grid), dim3(P2_BLOCK), lds, s, *col, mean, d_edges,
-                               bins, edges_monotone, hi_t, lo_t, pm, pc));
+            hipLaunchKernelGGL((pass2_kernel<T, false, false>), dim3(grid), dim3(P2_BLOCK), lds, s, *col, mean,
+                               d_edges, bins, edges_monotone, hi_t, lo_t, pm, pc));
     }
     rc = check_launch("pass2_kernel");
     if (rc) return rc;
