@@ -812,7 +812,7 @@ struct P2Thread {
 // bin and no bin search; the CASE-WHEN bins are differences of these
 // cumulative counts (bin j = [e_j, e_j+1), last bin x >= e_b-1, x < e_0 unbinned),
 // formed once per wave in the epilogue.
-template <typename T, bool SMALL, bool MONO>
+template <typename T, bool SMALL, bool MONO, int NB>
 __device__ __forceinline__ void p2_elem(P2Thread &st, const P2Ctx &c, uint32_t *lds_hist, T x,
                                         bool valid) {
     const double xd = Elem<T>::d(x);
@@ -825,9 +825,13 @@ __device__ __forceinline__ void p2_elem(P2Thread &st, const P2Ctx &c, uint32_t *
     if (SMALL && MONO) {
         st.okc += ok;
         if (ok) st.mad += fabs(xd - c.mean);
+        // per-lane counts (compare + add-with-carry each; summed over the wave
+        // in the epilogue): wave ballots of every element of a tile ran out of
+        // SGPRs.  A skipped element compares as -inf; unused edges are +inf
+        // and their counts are never read.
+        const double xv = ok ? xd : -__builtin_inf();
 #pragma unroll
-        for (int j = 0; j < P2_SMALL_BINS; ++j)
-            if (j < c.bins) st.bc[j] += (uint32_t)__popcll(__ballot(ok && xd >= c.ev[j]));
+        for (int j = 0; j < NB; ++j) st.bc[j] += (uint32_t)(xv >= c.ev[j]);
         return;
     }
     int bin = -1;
@@ -846,7 +850,7 @@ __device__ __forceinline__ void p2_elem(P2Thread &st, const P2Ctx &c, uint32_t *
     }
 }
 
-template <typename T, bool SMALL, bool MONO>
+template <typename T, bool SMALL, bool MONO, int NB = P2_SMALL_BINS>
 __global__ void __launch_bounds__(P2_BLOCK, 4) pass2_kernel(sdp_column col, double mean, const double *edges,
                                                          int bins, int monotone, double hi_t, double lo_t,
                                                          double *part_mad, uint64_t *part_cnt) {
@@ -861,7 +865,7 @@ __global__ void __launch_bounds__(P2_BLOCK, 4) pass2_kernel(sdp_column col, doub
     c.monotone = monotone != 0;
     c.e0 = s_edges[0];
 #pragma unroll
-    for (int j = 0; j < P2_SMALL_BINS; ++j) c.ev[j] = (MONO && j < bins) ? edges[j] : 0.0;   // uniform loads
+    for (int j = 0; j < P2_SMALL_BINS; ++j) c.ev[j] = j < bins ? edges[j] : __builtin_inf();   // uniform loads
     {
         const double w = (bins > 1) ? (s_edges[bins - 1] - s_edges[0]) / (double)(bins - 1) : 0.0;
         c.inv_w = (w > 0.0) ? 1.0 / w : 0.0;
@@ -887,7 +891,7 @@ __global__ void __launch_bounds__(P2_BLOCK, 4) pass2_kernel(sdp_column col, doub
 #pragma unroll
         for (int u = 0; u < U; ++u)
 #pragma unroll
-            for (int e = 0; e < VPT; ++e) p2_elem<T, SMALL, MONO>(st, c, s_hist, cur.v[u].v[e], (cur.vb[u] >> e) & 1u);
+            for (int e = 0; e < VPT; ++e) p2_elem<T, SMALL, MONO, NB>(st, c, s_hist, cur.v[u].v[e], (cur.vb[u] >> e) & 1u);
         if (more) cur = nxt;
     }
     if (blockIdx.x == 0 && threadIdx.x < WAVE) {
@@ -895,7 +899,7 @@ __global__ void __launch_bounds__(P2_BLOCK, 4) pass2_kernel(sdp_column col, doub
         const bool inb = i < n;
         T x = inb ? ((const T *)col.d_values)[i] : (T)0;
         const bool valid = inb && valid_bit(col.d_validity, col.validity_bit_offset, i);
-        p2_elem<T, SMALL, MONO>(st, c, s_hist, x, valid);
+        p2_elem<T, SMALL, MONO, NB>(st, c, s_hist, x, valid);
     }
     // ---- block reduction (fixed order) ----
     __shared__ double s_mad[P2_BLOCK / WAVE];
@@ -904,7 +908,9 @@ __global__ void __launch_bounds__(P2_BLOCK, 4) pass2_kernel(sdp_column col, doub
     const double mad = wave_sum_f64(st.mad);
     const uint64_t hi = wave_sum_u64(st.high), lo = wave_sum_u64(st.low);
     uint64_t ub = wave_sum_u64(st.unbinned);
-    if (SMALL && MONO) {                // cumulative counts -> CASE-WHEN bins (wave-uniform)
+    if (SMALL && MONO) {                // per-lane cumulative counts -> CASE-WHEN bins of the wave
+#pragma unroll
+        for (int j = 0; j < P2_SMALL_BINS; ++j) st.bc[j] = j < NB ? (uint32_t)wave_sum_u64(st.bc[j]) : 0u;
         ub = wave_sum_u64(st.okc) - st.bc[0];
 #pragma unroll
         for (int j = 0; j < P2_SMALL_BINS - 1; ++j)
@@ -1130,7 +1136,11 @@ extern "C" int sdp_pass2(const sdp_column *col, double mean, const double *d_edg
     uint64_t *pc = (uint64_t *)((char *)d_work + (int64_t)grid * sizeof(double));
     const size_t lds = (size_t)bins * (sizeof(double) + sizeof(uint32_t)) + 16;
     hipStream_t s = (hipStream_t)stream;
-    if (bins <= P2_SMALL_BINS && edges_monotone) {
+    if (bins <= 10 && edges_monotone) {          // describe()'s default bins=10
+        SDP_DISPATCH_NUMERIC(col->dtype,
+            hipLaunchKernelGGL((pass2_kernel<T, true, true, 10>), dim3(grid), dim3(P2_BLOCK), lds, s, *col, mean,
+                               d_edges, bins, edges_monotone, hi_t, lo_t, pm, pc));
+    } else if (bins <= P2_SMALL_BINS && edges_monotone) {
         SDP_DISPATCH_NUMERIC(col->dtype,
             hipLaunchKernelGGL((pass2_kernel<T, true, true>), dim3(grid), dim3(P2_BLOCK), lds, s, *col, mean,
                                d_edges, bins, edges_monotone, hi_t, lo_t, pm, pc));
