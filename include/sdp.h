@@ -135,7 +135,8 @@ int sdp_quantile_plan(uint64_t *d_sample, int32_t n_sample, const double *probs,
  * (keys strictly inside window w) go to wave-private slot ranges: segment
  * s = (w*grid + b)*SDP_PASS1_WAVES + wave holds d_cand[s*slot_capacity ...], its
  * count (clamped to slot_capacity; overflow flagged in w_overflow) in
- * d_cand_counts[s]. */
+ * d_cand_counts[s].  slot_capacity 0 = the plan has no windows (moments and min/max
+ * only). */
 int sdp_pass1(const sdp_column *col, const sdp_qplan *d_plan, void *d_work,
               int64_t work_bytes, uint64_t *d_cand, uint32_t *d_cand_counts,
               int64_t slot_capacity, sdp_pass1_result *d_result, void *stream);

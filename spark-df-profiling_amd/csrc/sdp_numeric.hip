@@ -225,7 +225,7 @@ struct VecTile {
 // epilogue (n_skip), as are eqhi counts of windows with lo == hi -- so each
 // window costs two compare-and-carry counts, one equality count and the
 // inside test, with no per-element validity masking.
-template <typename T>
+template <typename T, bool WIN>
 __device__ __forceinline__ void p1_elem(P1Thread &st, const P1Ctx &cx, T x, bool valid) {
     const double xd = Elem<T>::d(x);
     const bool isnan_ = Elem<T>::is_float && (xd != xd);
@@ -252,6 +252,7 @@ __device__ __forceinline__ void p1_elem(P1Thread &st, const P1Ctx &cx, T x, bool
         two_sum_acc(st.s3, st.s3c, d2 * d);
         st.s4 = fma(d2, d2, st.s4);
     }
+    if (!WIN) return;                   // no quantile windows (date/timestamp min/max)
     const uint64_t key = ok ? Elem<T>::key(x) : 0ull;
     // Every window slot is evaluated: unused ones have lo = hi = UINT64_MAX
     // (nothing inside, nothing above; their counts are never read), which
@@ -275,7 +276,7 @@ __device__ __forceinline__ void p1_elem(P1Thread &st, const P1Ctx &cx, T x, bool
     }
 }
 
-template <typename T>
+template <typename T, bool WIN>
 __global__ void __launch_bounds__(P1_BLOCK, 4) pass1_kernel(sdp_column col, const sdp_qplan *plan,
                                                          P1Partial *partials, uint64_t *cand,
                                                          uint32_t *cand_counts, int64_t cap) {
@@ -320,7 +321,7 @@ __global__ void __launch_bounds__(P1_BLOCK, 4) pass1_kernel(sdp_column col, cons
 #pragma unroll
         for (int u = 0; u < U; ++u) {
 #pragma unroll
-            for (int e = 0; e < VPT; ++e) p1_elem<T>(st, cx, cur.v[u].v[e], (cur.vb[u] >> e) & 1u);
+            for (int e = 0; e < VPT; ++e) p1_elem<T, WIN>(st, cx, cur.v[u].v[e], (cur.vb[u] >> e) & 1u);
         }
         if (more) cur = nxt;
     }
@@ -330,7 +331,7 @@ __global__ void __launch_bounds__(P1_BLOCK, 4) pass1_kernel(sdp_column col, cons
         const bool inb = i < n;
         T x = inb ? ((const T *)col.d_values)[i] : (T)0;
         const bool valid = inb && valid_bit(col.d_validity, col.validity_bit_offset, i);
-        p1_elem<T>(st, cx, x, valid);
+        p1_elem<T, WIN>(st, cx, x, valid);
     }
 
     // ---- block reduction: waves, then LDS, fixed order ----------------------
@@ -1026,9 +1027,15 @@ extern "C" int sdp_pass1(const sdp_column *col, const sdp_qplan *d_plan, void *d
     if (slot_capacity < 0 || slot_capacity > 0xFFFFFFFFll) return set_error(SDP_EINVAL, "sdp_pass1: slot_capacity");
     hipStream_t s = (hipStream_t)stream;
     P1Partial *parts = (P1Partial *)d_work;
-    SDP_DISPATCH_NUMERIC(col->dtype,
-        hipLaunchKernelGGL(pass1_kernel<T>, dim3(grid), dim3(P1_BLOCK), 0, s, *col, d_plan, parts, d_cand,
-                           d_cand_counts, slot_capacity));
+    if (slot_capacity > 0) {
+        SDP_DISPATCH_NUMERIC(col->dtype,
+            hipLaunchKernelGGL((pass1_kernel<T, true>), dim3(grid), dim3(P1_BLOCK), 0, s, *col, d_plan, parts, d_cand,
+                               d_cand_counts, slot_capacity));
+    } else {            // no windows: moments / min / max only
+        SDP_DISPATCH_NUMERIC(col->dtype,
+            hipLaunchKernelGGL((pass1_kernel<T, false>), dim3(grid), dim3(P1_BLOCK), 0, s, *col, d_plan, parts,
+                               d_cand, d_cand_counts, slot_capacity));
+    }
     rc = check_launch("pass1_kernel");
     if (rc) return rc;
     hipLaunchKernelGGL(pass1_merge_kernel, dim3(1), dim3(MERGE_T), 0, s, parts, grid, d_plan, d_result);
