@@ -457,18 +457,25 @@ class Engine:
                            keep[2].data_ptr() if isb else None)
         return r, keep
 
-    def _heavy_keys(self, col, isb):
+    def _heavy_keys(self, col, isb, gather=False):
         """Keys seen >= HEAVY_MIN times in an evenly spaced sample: counted
-        outside the partitions (describe.py:251's hot groups)."""
-        ns = min(PART_SAMPLE, col.length)
+        outside the partitions (describe.py:251's hot groups).  gather=True
+        (fixed keys of a sharded table): the samples of all ranks are pooled,
+        so every rank picks the same heavy keys."""
+        ns = min(PART_SAMPLE, max(col.length, 1))
         s = self._s()
         h = self._u64(ns)
-        if isb:
+        if col.length == 0:
+            h.fill_(-1)
+            keep = None
+        elif isb:
             rec, keep = self._records(ns, True)
             sdp.sdp_part_sample(None, ctypes.byref(col.sdp_bytes()), ns, ptr(h), ctypes.byref(rec), s)
         else:
             keep = None
             sdp.sdp_part_sample(ctypes.byref(col.sdp()), None, ns, ptr(h), None, s)
+        if gather and self.comm.world > 1:
+            h = torch.cat(self.comm.allgatherv(h))
         hn = h.cpu().numpy().view(np.uint64)
         pos = np.nonzero(hn != np.uint64(U64))[0]
         if isb and pos.size:
@@ -615,6 +622,106 @@ class Engine:
             tab.update({'slots': keys, 'counts': counts, 'capacity': max(total, 1)})
         return tab
 
+    def group_sharded(self, col):
+        """countDistinct (describe.py:143) of a fixed-width column of a
+        row-sharded table, on the partitioning kernels: level-1 buckets (top
+        B1 hash bits) are owned by contiguous rank ranges, so after the local
+        bucket scatter ONE all-to-all of 8-byte records hands every owner all
+        records of its buckets; level 2 and the LDS de-duplication then run on
+        the owner, and the group counts are all-reduced.  Heavy keys come from
+        the pooled samples of all ranks (the same set everywhere) and are
+        counted locally and all-reduced.  Returns None when the owner tables
+        overflow (the caller takes the table-exchange path)."""
+        comm, world, rank = self.comm, self.comm.world, self.comm.rank
+        n = col.length
+        s = self._s()
+        B1 = 10
+        nb1 = 1 << B1
+        n_all = int(comm.allreduce_sum(torch.tensor([n], dtype=torch.int64, device=self.device)).item())
+        target = sdp.sdp_part_bucket_target(0, 0)
+        b2 = min(10, max(1, math.ceil(math.log2(max(2.0, n_all / nb1 / target)))))
+        nb2 = 1 << b2
+        stats = self._u64(68, zero=True)
+        cs = col.sdp()
+        hv = self._heavy_keys(col, False, gather=True)
+        hvref = ctypes.byref(hv['struct']) if hv else None
+        hcnt = self._u64(max(hv['n'] if hv else 1, 1), zero=True)
+        # level 1 on this rank's rows
+        rpb = sdp.sdp_part_rows_per_block(max(n, 1), 0)
+        grid = max(1, -(-n // rpb))
+        h1 = torch.zeros(nb1 * grid, dtype=torch.int32, device=self.device)
+        rb = col_read_bytes(col)
+        if n:
+            nat.annotate(_label(col, 'count'), rb)
+            sdp.sdp_part_rows(ctypes.byref(cs), None, hvref, B1, 0, ptr(h1), None, None, ptr(hcnt), ptr(stats), s)
+        o1 = self._scan(h1)
+        bs = o1[0:nb1 * grid:grid].cpu().numpy().astype(np.int64)
+        nrec = int(o1[-1].item())
+        bs = np.append(bs, nrec)
+        r1, keep1 = self._records(nrec, False)
+        if nrec:
+            nat.annotate(_label(col, 'scatter'), rb + nrec * 8)
+            sdp.sdp_part_rows(ctypes.byref(cs), None, hvref, B1, 1, None, ptr(o1), ctypes.byref(r1), ptr(hcnt),
+                              ptr(stats), s)
+        # ownership: rank r owns buckets [lo[r], lo[r + 1])
+        lo = [(r * nb1) // world for r in range(world + 1)]
+        send = [int(bs[lo[r + 1]] - bs[lo[r]]) for r in range(world)]
+        sizes = torch.from_numpy(np.diff(bs)).to(self.device)
+        all_sizes = torch.stack(comm.allgather(sizes)).cpu().numpy()          # [world, nb1]
+        recv = comm.alltoallv(keep1[0][:nrec], send)
+        del keep1, r1
+        my = list(range(lo[rank], lo[rank + 1]))
+        # received layout: source-rank-major, my buckets in order inside each part
+        part_tot = all_sizes[:, lo[rank]:lo[rank + 1]].sum(axis=1)
+        part_base = np.concatenate([[0], np.cumsum(part_tot)[:-1]]).astype(np.int64)
+        segs = []                                                            # (bucket idx, start, end)
+        for bi, b in enumerate(my):
+            for src in range(world):
+                st0 = part_base[src] + all_sizes[src, lo[rank]:b].sum()
+                m = int(all_sizes[src, b])
+                for c0 in range(0, m, PART_CHUNK):
+                    segs.append((bi, st0 + c0, st0 + min(m, c0 + PART_CHUNK)))
+        nmy = len(my)
+        nrecv = int(recv.numel())
+        groups_local = 0
+        if nrecv:
+            seg = np.array(segs, dtype=np.int64)
+            nch = np.bincount(seg[:, 0], minlength=nmy).astype(np.int64)
+            k0 = np.concatenate([[0], np.cumsum(nch)[:-1]]).astype(np.int64)
+            K = int(nch.sum())
+            j = np.arange(K, dtype=np.int64) - k0[seg[:, 0]]
+            ch = np.empty((K, 4), dtype=np.int64)
+            ch[:, 0], ch[:, 1] = seg[:, 1], seg[:, 2]
+            ch[:, 2] = nb2 * k0[seg[:, 0]] + j
+            ch[:, 3] = nch[seg[:, 0]]
+            chunks = torch.from_numpy(ch).to(self.device)
+            rin = nat.SdpRecords(recv.data_ptr(), None, None)
+            h2 = torch.empty(nb2 * K, dtype=torch.int32, device=self.device)
+            nat.annotate('u64/count', nrecv * 8)
+            sdp.sdp_part_recs(ctypes.byref(rin), 0, ptr(chunks), K, B1, b2, 0, ptr(h2), None, None, s)
+            o2 = self._scan(h2)
+            rf, keepf = self._records(nrecv, False)
+            nat.annotate('u64/scatter', 2 * nrecv * 8)
+            sdp.sdp_part_recs(ctypes.byref(rin), 0, ptr(chunks), K, B1, b2, 1, None, ptr(o2), ctypes.byref(rf), s)
+            del recv, h2
+            sidx = (nb2 * k0[:, None] + np.arange(nb2)[None, :] * nch[:, None]).reshape(-1)
+            sidx = np.append(sidx, nb2 * K)
+            starts = o2[torch.from_numpy(sidx).to(self.device)].contiguous()
+            ngroups = torch.zeros(nmy * nb2, dtype=torch.int32, device=self.device)
+            nat.annotate('u64', nrecv * 8)
+            sdp.sdp_part_dedup(ctypes.byref(rf), 0, None, ptr(starts), nmy * nb2, 0, None, None, ptr(ngroups),
+                               ptr(stats), s)
+        st = stats.clone()
+        st[4] = st[4:68].sum()
+        tot = comm.allreduce_sum(torch.cat([st[:5], hcnt[:max(hv['n'], 1)] if hv else hcnt[:1]]))
+        t = self._host_u64(tot)
+        if t[2] or t[3]:
+            return None
+        heavy_present = sum(1 for c in t[5:5 + (hv['n'] if hv else 0)] if c)
+        groups = t[4] + heavy_present + (1 if t[1] else 0)
+        return {'bytes': False, 'dense': False, 'rows': t[0], 'max_key_rows': 0, 'col': col, 'groups': groups,
+                'groups_local': groups, 'sharded': True}
+
     def _scan(self, counts_i32):
         """Exclusive scan of int32 counts -> int64 offsets (n + 1 entries)."""
         n = counts_i32.numel()
@@ -631,7 +738,7 @@ class Engine:
         all-gather their OR-ed bitmaps and re-reduce them."""
         nw = (range_ + 31) // 32
         work = self._bytes(sdp.sdp_bitmap_workspace_bytes(col.length, range_))
-        bm = torch.empty(nw, dtype=torch.int32, device=self.device)
+        bm = torch.zeros(nw, dtype=torch.int32, device=self.device)      # (an empty shard writes nothing)
         out = self._u64(1, zero=True)
         cs = col.sdp()
         nat.annotate(_label(col), col_read_bytes(col))
@@ -650,9 +757,16 @@ class Engine:
         the radix-partitioned LDS grouping wins for near-unique keys (50 vs 80
         ms); a global table sized by a small key range (<= rows / 4) stays
         cache-resident and wins there (23 vs 44 ms)."""
-        small_range = capacity_hint is not None and capacity_hint * 4 <= max(col.length, 1)
+        n = col.length
+        if self.comm.world > 1:       # the path choice must agree on every rank: decide on the global rows
+            n = int(self.comm.allreduce_sum(torch.tensor([n], dtype=torch.int64, device=self.device)).item())
+        small_range = capacity_hint is not None and capacity_hint * 4 <= max(n, 1)
         if self.comm.world == 1 and not small_range and col.length >= (1 << 16):
             tab = self.group(col, with_counts, dense=with_counts)
+            if tab is not None:
+                return tab
+        if self.comm.world > 1 and not with_counts and not small_range:
+            tab = self.group_sharded(col)          # collective: every rank takes this branch
             if tab is not None:
                 return tab
         return self._distinct_fixed_table(col, with_counts, capacity_hint)

@@ -38,6 +38,7 @@ def main():
     tables = {
         'demo': datagen.demo_like_table(60_000),
         'numeric': datagen.numeric_table(40_000),
+        'numeric_big': datagen.numeric_table(300_001, seed=11),
         'categorical': datagen.categorical_table(30_000),
         'dates': datagen.date_table(20_000),
         'corr': datagen.corr_table(20_000),
