@@ -111,3 +111,18 @@ def test_parquet_round_trip(tmp_path):
     assert_describe_equal(describe(str(path), plots=False), describe(want, plots=False))
     sub = from_parquet(str(path), columns=['word', 'f64'], device=dev)
     assert sub.column_names == ['word', 'f64']
+
+
+def test_profile_report_to_file(tmp_path):
+    """ProfileReport(df).to_file() end to end on the GPU path (__init__.py:19-124)."""
+    import datagen
+    from spark_df_profiling import ProfileReport
+    t = datagen.demo_like_table(20_000)
+    rep = ProfileReport(t, sample=5)
+    out = tmp_path / 'r.html'
+    rep.to_file(str(out))
+    text = out.read_text(encoding='utf8')
+    assert text.startswith('<!doctype html>') and 'Dataset info' in text
+    assert 'data:image/png;base64' in text                  # histograms rendered
+    assert set(rep.get_description()) == {'table', 'variables', 'freq'}
+    assert 'reclat_city' in rep.get_rejected_variables(0.9)
