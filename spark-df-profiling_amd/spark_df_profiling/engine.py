@@ -50,6 +50,14 @@ def _u(x):
     return int(x) & U64
 
 
+class _nullctx:
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        return False
+
+
 DTYPE_NAME = {nat.I8: 'i8', nat.I16: 'i16', nat.I32: 'i32', nat.I64: 'i64', nat.U8: 'u8', nat.U16: 'u16',
               nat.U32: 'u32', nat.U64: 'u64', nat.F32: 'f32', nat.F64: 'f64', nat.BOOL: 'bool'}
 
@@ -175,6 +183,14 @@ class Engine:
         t = torch.frombuffer(bytearray(raw), dtype=torch.uint8)
         return t.to(self.device)
 
+    def _h2d(self, arr):
+        """Host numpy array -> device tensor without a host round trip: staged
+        through pinned memory and copied asynchronously on the engine's stream
+        (a pageable copy would wait for every kernel queued before it)."""
+        t = torch.from_numpy(np.ascontiguousarray(arr))
+        with torch.cuda.stream(self.stream) if self.stream is not None else _nullctx():
+            return t.pin_memory().to(self.device, non_blocking=True)
+
     @staticmethod
     def _host_u64(t):
         return [int(x) & U64 for x in t.cpu().numpy().view(np.uint64).tolist()]
@@ -190,7 +206,7 @@ class Engine:
         sdp.sdp_sample_keys(ctypes.byref(cs), ns, ptr(sample), self._s())
         parts = self.comm.allgather(sample)
         allk = torch.cat(parts) if len(parts) > 1 else sample
-        pr = torch.tensor(list(probs), dtype=torch.float64, device=self.device)
+        pr = self._h2d(np.array(list(probs), dtype=np.float64))
         plan_dev = self._bytes(ctypes.sizeof(nat.SdpQPlan))
         sdp.sdp_quantile_plan(ptr(allk), allk.numel(), ptr(pr), len(probs), int(col.is_float), ptr(plan_dev),
                               self._s())
@@ -379,7 +395,7 @@ class Engine:
 
     def pass2(self, col, mean, edges, hi_t, lo_t):
         bins = len(edges)
-        e = torch.tensor([float(x) for x in edges], dtype=torch.float64, device=self.device)
+        e = self._h2d(np.array([float(x) for x in edges], dtype=np.float64))
         mono = all(math.isfinite(float(x)) for x in edges) and all(
             float(edges[i]) <= float(edges[i + 1]) for i in range(bins - 1))
         need = sdp.sdp_pass2_workspace_bytes(col.length, col.dtype, bins)
@@ -390,10 +406,13 @@ class Engine:
         nat.annotate(_label(col), col_read_bytes(col))
         sdp.sdp_pass2(ctypes.byref(cs), float(mean), ptr(e), bins, int(mono), float(hi_t), float(lo_t), ptr(work),
                       work.numel(), ptr(res), ptr(hist), self._s())
-        r = self._read(res, nat.SdpPass2Result)
-        if self.comm.world == 1:
+        if self.comm.world == 1:         # result struct and bins in one readback
+            sz = ctypes.sizeof(nat.SdpPass2Result)
+            raw = torch.cat([res[:sz], hist.view(torch.uint8)]).cpu().numpy()
+            r = nat.SdpPass2Result.from_buffer_copy(raw[:sz].tobytes())
             return {'abs_dev_sum': float(r.abs_dev_sum), 'n_high': int(r.n_high), 'n_low': int(r.n_low),
-                    'n_unbinned': int(r.n_unbinned), 'hist': hist.cpu().numpy().astype(np.int64)}
+                    'n_unbinned': int(r.n_unbinned), 'hist': raw[sz:].view(np.int64).astype(np.int64)}
+        r = self._read(res, nat.SdpPass2Result)
         # merge ranks: counts sum exactly; abs-dev sums gathered and added in rank order
         vec = torch.tensor([r.n_high, r.n_low, r.n_unbinned], dtype=torch.int64, device=self.device)
         vec = self.comm.allreduce_sum(torch.cat([vec, hist]))
@@ -490,9 +509,9 @@ class Engine:
         if sel.size > nat.HEAVY_MAX:
             sel = sel[np.argsort(-cnt[sel], kind='stable')[:nat.HEAVY_MAX]]
         rows = pos[first[sel]]
-        hv = {'h': torch.from_numpy(u[sel].view(np.int64).copy()).to(self.device), 'n': int(sel.size)}
+        hv = {'h': self._h2d(u[sel].view(np.int64).copy()), 'n': int(sel.size)}
         if isb:
-            idx = torch.from_numpy(rows.astype(np.int64)).to(self.device)
+            idx = self._h2d(rows.astype(np.int64))
             hv['k0'], hv['k1'], hv['meta'] = keep[0][idx].contiguous(), keep[1][idx].contiguous(), \
                 keep[2][idx].contiguous()
         st = nat.SdpHeavy(hv['h'].data_ptr(), hv['k0'].data_ptr() if isb else None,
@@ -539,7 +558,9 @@ class Engine:
         nat.annotate(_label(col, 'count'), rb)
         sdp.sdp_part_rows(cref, bref, hvref, b1, 0, ptr(h1), None, None, ptr(hcnt), ptr(stats), s)
         o1 = self._scan(h1)
-        nrec = int(o1[-1].item())
+        # record count and L1 bucket starts in one readback
+        bsn = torch.cat([o1[0:nb1 * grid:grid], o1[-1:]]).cpu().numpy().astype(np.int64)
+        nrec = int(bsn[-1])
         r1, keep1 = self._records(nrec, isb)
         if nrec:
             nat.annotate(_label(col, 'scatter'), rb + nrec * recw)
@@ -550,7 +571,7 @@ class Engine:
             starts = torch.cat([bstarts, o1[-1:]]) if b2 == 0 else self._u64(nb1 * nb2 + 1, zero=True)
             rf, keepf = r1, keep1
         else:
-            bs = np.append(bstarts.cpu().numpy(), nrec).astype(np.int64)
+            bs = bsn
             sizes = np.diff(bs)
             nch = -(-sizes // PART_CHUNK)
             k0 = np.concatenate([[0], np.cumsum(nch)[:-1]]).astype(np.int64)
@@ -562,7 +583,7 @@ class Engine:
             ch[:, 1] = np.minimum(bs[bof + 1], ch[:, 0] + PART_CHUNK)
             ch[:, 2] = nb2 * k0[bof] + j
             ch[:, 3] = nch[bof]
-            chunks = torch.from_numpy(ch).to(self.device)
+            chunks = self._h2d(ch)
             h2 = torch.empty(nb2 * K, dtype=torch.int32, device=self.device)
             nat.annotate(('bytes' if isb else 'u64') + '/count', nrec * recw)
             sdp.sdp_part_recs(ctypes.byref(r1), int(isb), ptr(chunks), K, b1, b2, 0, ptr(h2), None, None, s)
@@ -574,7 +595,7 @@ class Engine:
             del keep1, r1, h2
             sidx = (nb2 * k0[:, None] + np.arange(nb2)[None, :] * nch[:, None]).reshape(-1)
             sidx = np.append(sidx, nb2 * K)
-            starts = o2[torch.from_numpy(sidx).to(self.device)].contiguous()
+            starts = o2[self._h2d(sidx)].contiguous()
         nfinal = nb1 * nb2
         ngroups = torch.zeros(nfinal, dtype=torch.int32, device=self.device)
         out_key = out_cnt = None
@@ -584,12 +605,12 @@ class Engine:
             nat.annotate('bytes' if isb else ('u64/counts' if with_counts else 'u64'), nrec * recw)
             sdp.sdp_part_dedup(ctypes.byref(rf), int(isb), bref, ptr(starts), nfinal, int(with_counts) | (2 if large else 0),
                                ptr(out_key), ptr(out_cnt), ptr(ngroups), ptr(stats), s)
-        st = self._host_u64(stats)
+        both = self._host_u64(torch.cat([stats, hcnt[:hv['n']]]) if hv else stats)   # one readback
+        st, hc = both[:68], both[68:]
         if st[2] or st[3]:
             return None
         groups_local = sum(st[4:68])
         special = st[1]
-        hc = self._host_u64(hcnt[:hv['n']]) if hv else []
         heavy_sel = [i for i, c in enumerate(hc) if c]
         total = groups_local + (1 if special else 0) + len(heavy_sel)
         tab = {'bytes': isb, 'dense': True, 'rows': st[0], 'max_key_rows': 0, 'col': col,
