@@ -199,6 +199,51 @@ def profile_alg_bytes(table, raw):
     return b
 
 
+_DT = {'f64': 'double', 'f32': 'float', 'i64': 'long', 'i32': 'int', 'i16': 'short', 'i8': 'signed char',
+       'u64': 'unsigned long', 'u32': 'unsigned int'}
+
+
+def label_kernels(label):
+    """rocprof kernel-name prefixes behind one entry-point label
+    (`sdp_<entry>[<dtype>/<stage>]`, engine.annotate)."""
+    name, _, arg = label.partition('[')
+    arg = arg.rstrip(']')
+    dt, _, stage = arg.partition('/')
+    if name == 'sdp_part_recs':
+        b = 'true' if dt == 'bytes' else 'false'
+        return ['sdp::part_%s_recs_kernel<%s>' % ('count' if stage == 'count' else 'scatter', b)]
+    if name == 'sdp_part_rows':
+        st = 'count' if stage == 'count' else 'scatter'
+        if dt == 'bytes':
+            return ['sdp::part_%s_rows_bytes_kernel' % st]
+        return ['sdp::part_%s_rows_u64_kernel<%s>' % (st, _DT.get(dt, dt))]
+    if name == 'sdp_part_dedup':
+        return ['sdp::part_dedup_bytes_kernel'] if dt == 'bytes' else ['sdp::part_dedup_u64']
+    if name in ('sdp_pass1', 'sdp_pass2'):
+        return ['sdp::%s_kernel<%s' % (name[4:], _DT.get(dt, dt))]
+    if name == 'sdp_gram':
+        return ['sdp::gram_kernel<']
+    return []
+
+
+def pmc_traffic(label):
+    """HBM bytes per launch of the kernel(s) behind `label`, from the newest
+    committed PMC summary (profiles/*_traffic.json, tools/gpu_traffic.sh:
+    rocprofv3 FETCH_SIZE and WRITE_SIZE passes over this bench), or None."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, 'profiles', '*_traffic.json')), key=os.path.getmtime)
+    if not files:
+        return None, None
+    with open(files[-1]) as fh:
+        summ = json.load(fh)
+    pre = label_kernels(label)
+    hits = [v for k, v in summ['kernels'].items() if any(k.startswith(p) for p in pre)]
+    if not hits:
+        return None, None
+    n = sum(v['dispatches'] for v in hits)
+    return sum(v['traffic_bytes'] * v['dispatches'] for v in hits) / n, os.path.basename(files[-1])
+
+
 def roofline(rec, steps, step_s, prof_bytes):
     """Dominant kernel (entry point + label) by total HIP-event time -> achieved
     GB/s = its algorithmic bytes per launch / its mean launch duration."""
@@ -213,8 +258,13 @@ def roofline(rec, steps, step_s, prof_bytes):
     per_launch = nbytes[dom] / nl[dom]
     achieved = per_launch / (avg_ms * 1e-3) / 1e9
     prof_gbs = prof_bytes / step_s / 1e9
+    traffic, tsrc = pmc_traffic(dom)
     out = {'bound': 'hbm', 'kernel': dom, 'achieved': round(achieved, 1), 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
-           'frac': round(achieved / HBM_PEAK_GBS, 4), 'traffic': None,
+           'frac': round(achieved / HBM_PEAK_GBS, 4),
+           'traffic': int(traffic) if traffic is not None else None,
+           'traffic_unit': 'bytes per launch (PMC FETCH_SIZE x2 + WRITE_SIZE)',
+           'traffic_over_alg': round(traffic / per_launch, 3) if traffic is not None else None,
+           'traffic_source': ('profiles/' + tsrc) if tsrc else None,
            'launches_per_step': nl[dom] // steps, 'avg_launch_ms': round(avg_ms, 4),
            'alg_bytes_per_launch': int(per_launch),
            'share_of_step': round(tot[dom] / steps / (step_s * 1e3), 3),
