@@ -1080,39 +1080,114 @@ extern "C" int64_t sdp_select_kth_workspace_bytes(int64_t n_cap) {
     return sel_align(sizeof(SelState)) + sel_align(2048 * 8) + 2 * sel_align(8) + 2 * sel_align(8 * (n_cap > 0 ? n_cap : 1));
 }
 
+struct SelWork {
+    SelState *st;
+    uint64_t *hist;
+    uint64_t *cnt[2];
+    uint64_t *buf[2];
+};
+static SelWork sel_layout(void *d_work, int64_t n_cap) {
+    char *w = (char *)d_work;
+    SelWork L;
+    L.st = (SelState *)w;
+    w += sel_align(sizeof(SelState));
+    L.hist = (uint64_t *)w;
+    w += sel_align(2048 * 8);
+    L.cnt[0] = (uint64_t *)w;
+    L.cnt[1] = (uint64_t *)(w + sel_align(8));
+    w += 2 * sel_align(8);
+    L.buf[0] = (uint64_t *)w;
+    L.buf[1] = (uint64_t *)(w + sel_align(8 * (n_cap > 0 ? n_cap : 1)));
+    return L;
+}
+static int sel_shift0(uint64_t lo_key, uint64_t hi_key) {
+    const uint64_t x = lo_key ^ hi_key;
+    return x ? ((63 - __builtin_clzll(x)) / 11) * 11 : 0;
+}
+
 extern "C" int sdp_select_kth(const uint64_t *d_keys, const uint64_t *d_n, int64_t n_cap, int64_t k,
                               uint64_t lo_key, uint64_t hi_key, void *d_work, int64_t work_bytes,
                               uint64_t *d_result, void *stream) {
     if (n_cap < 0 || k < 0 || d_result == nullptr) return set_error(SDP_EINVAL, "sdp_select_kth: args");
     if (work_bytes < sdp_select_kth_workspace_bytes(n_cap)) return set_error(SDP_ECAP, "sdp_select_kth: workspace");
-    char *w = (char *)d_work;
-    SelState *st = (SelState *)w;
-    w += sel_align(sizeof(SelState));
-    uint64_t *hist = (uint64_t *)w;
-    w += sel_align(2048 * 8);
-    uint64_t *cnt[2] = {(uint64_t *)w, (uint64_t *)(w + sel_align(8))};
-    w += 2 * sel_align(8);
-    uint64_t *buf[2] = {(uint64_t *)w, (uint64_t *)(w + sel_align(8 * (n_cap > 0 ? n_cap : 1)))};
-    const uint64_t x = lo_key ^ hi_key;
-    const int shift0 = x ? ((63 - __builtin_clzll(x)) / 11) * 11 : 0;
+    const SelWork L = sel_layout(d_work, n_cap);
+    const int shift0 = sel_shift0(lo_key, hi_key);
     const uint64_t prefix0 = shift0 + 11 < 64 ? (lo_key >> (shift0 + 11)) : 0ull;
     hipStream_t s = (hipStream_t)stream;
-    hipLaunchKernelGGL(select_init_kernel, dim3(1), dim3(256), 0, s, st, prefix0, k, shift0, hist);
+    hipLaunchKernelGGL(select_init_kernel, dim3(1), dim3(256), 0, s, L.st, prefix0, k, shift0, L.hist);
     int rc = check_launch("select_init_kernel");
     if (rc) return rc;
     const uint64_t *cur = d_keys, *cur_n = d_n;
     for (int shift = shift0, r = 0;; shift -= 11, ++r) {
-        hipLaunchKernelGGL(radix_hist_st_kernel, dim3(512), dim3(256), 0, s, cur, cur_n, st, hist);
-        hipLaunchKernelGGL(radix_decide_kernel, dim3(1), dim3(1024), 0, s, hist, st, shift ? cnt[r & 1] : nullptr,
-                           d_result);
+        hipLaunchKernelGGL(radix_hist_st_kernel, dim3(512), dim3(256), 0, s, cur, cur_n, L.st, L.hist);
+        hipLaunchKernelGGL(radix_decide_kernel, dim3(1), dim3(1024), 0, s, L.hist, L.st,
+                           shift ? L.cnt[r & 1] : nullptr, d_result);
         if ((rc = check_launch("radix_decide_kernel"))) return rc;
         if (shift == 0) break;
-        hipLaunchKernelGGL(radix_filter_st_kernel, dim3(512), dim3(256), 0, s, cur, cur_n, st, buf[r & 1], cnt[r & 1]);
+        hipLaunchKernelGGL(radix_filter_st_kernel, dim3(512), dim3(256), 0, s, cur, cur_n, L.st, L.buf[r & 1],
+                           L.cnt[r & 1]);
         if ((rc = check_launch("radix_filter_st_kernel"))) return rc;
-        cur = buf[r & 1];
-        cur_n = cnt[r & 1];
+        cur = L.buf[r & 1];
+        cur_n = L.cnt[r & 1];
     }
     return 0;
+}
+
+// ---- the same select, one round per call (row-sharded tables) ----------------------
+// Every rank runs the same rounds on its own keys; between sdp_select_hist and
+// sdp_select_step the caller all-reduces d_hist on the same stream (RCCL is
+// stream-ordered), so the digit each rank's decide kernel picks is the global
+// one and no round needs a host round trip.
+extern "C" int sdp_select_rounds(uint64_t lo_key, uint64_t hi_key) { return sel_shift0(lo_key, hi_key) / 11 + 1; }
+
+extern "C" int sdp_select_init(int64_t k, uint64_t lo_key, uint64_t hi_key, void *d_work, int64_t work_bytes,
+                               int64_t n_cap, uint64_t *d_hist, void *stream) {
+    if (n_cap < 0 || k < 0 || d_hist == nullptr) return set_error(SDP_EINVAL, "sdp_select_init: args");
+    if (work_bytes < sdp_select_kth_workspace_bytes(n_cap)) return set_error(SDP_ECAP, "sdp_select_init: workspace");
+    const SelWork L = sel_layout(d_work, n_cap);
+    const int shift0 = sel_shift0(lo_key, hi_key);
+    const uint64_t prefix0 = shift0 + 11 < 64 ? (lo_key >> (shift0 + 11)) : 0ull;
+    hipLaunchKernelGGL(select_init_kernel, dim3(1), dim3(256), 0, (hipStream_t)stream, L.st, prefix0, k, shift0,
+                       d_hist);
+    return check_launch("select_init_kernel");
+}
+
+static int sel_round_io(const uint64_t *d_keys, const uint64_t *d_n, const SelWork &L, int round,
+                        const uint64_t *&cur, const uint64_t *&cur_n) {
+    if (round < 0 || round > 5) return set_error(SDP_EINVAL, "sdp_select: round %d", round);
+    cur = round == 0 ? d_keys : L.buf[(round - 1) & 1];
+    cur_n = round == 0 ? d_n : L.cnt[(round - 1) & 1];
+    return 0;
+}
+
+extern "C" int sdp_select_hist(const uint64_t *d_keys, const uint64_t *d_n, int64_t n_cap, int32_t round,
+                               void *d_work, int64_t work_bytes, uint64_t *d_hist, void *stream) {
+    if (work_bytes < sdp_select_kth_workspace_bytes(n_cap)) return set_error(SDP_ECAP, "sdp_select_hist: workspace");
+    const SelWork L = sel_layout(d_work, n_cap);
+    const uint64_t *cur, *cur_n;
+    int rc = sel_round_io(d_keys, d_n, L, round, cur, cur_n);
+    if (rc) return rc;
+    hipLaunchKernelGGL(radix_hist_st_kernel, dim3(512), dim3(256), 0, (hipStream_t)stream, cur, cur_n, L.st, d_hist);
+    return check_launch("radix_hist_st_kernel");
+}
+
+extern "C" int sdp_select_step(const uint64_t *d_keys, const uint64_t *d_n, int64_t n_cap, int32_t round,
+                               int32_t last, void *d_work, int64_t work_bytes, uint64_t *d_hist, uint64_t *d_result,
+                               void *stream) {
+    if (d_result == nullptr || d_hist == nullptr) return set_error(SDP_EINVAL, "sdp_select_step: args");
+    if (work_bytes < sdp_select_kth_workspace_bytes(n_cap)) return set_error(SDP_ECAP, "sdp_select_step: workspace");
+    const SelWork L = sel_layout(d_work, n_cap);
+    const uint64_t *cur, *cur_n;
+    int rc = sel_round_io(d_keys, d_n, L, round, cur, cur_n);
+    if (rc) return rc;
+    hipStream_t s = (hipStream_t)stream;
+    hipLaunchKernelGGL(radix_decide_kernel, dim3(1), dim3(1024), 0, s, d_hist, L.st, last ? nullptr : L.cnt[round & 1],
+                       d_result);
+    if ((rc = check_launch("radix_decide_kernel"))) return rc;
+    if (last) return 0;
+    hipLaunchKernelGGL(radix_filter_st_kernel, dim3(512), dim3(256), 0, s, cur, cur_n, L.st, L.buf[round & 1],
+                       L.cnt[round & 1]);
+    return check_launch("radix_filter_st_kernel");
 }
 
 extern "C" int sdp_sort_small(uint64_t *d_keys, const uint64_t *d_n, void *stream) {

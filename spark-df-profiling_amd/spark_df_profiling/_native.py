@@ -111,6 +111,10 @@ _SIGNATURES = {
     'sdp_sort_small': (ctypes.c_int, [_P, _P, _P]),
     'sdp_select_kth_workspace_bytes': (_I64, [_I64]),
     'sdp_select_kth': (ctypes.c_int, [_P, _P, _I64, _I64, _U64, _U64, _P, _I64, _P, _P]),
+    'sdp_select_rounds': (ctypes.c_int, [_U64, _U64]),
+    'sdp_select_init': (ctypes.c_int, [_I64, _U64, _U64, _P, _I64, _I64, _P, _P]),
+    'sdp_select_hist': (ctypes.c_int, [_P, _P, _I64, _I32, _P, _I64, _P, _P]),
+    'sdp_select_step': (ctypes.c_int, [_P, _P, _I64, _I32, _I32, _P, _I64, _P, _P, _P]),
     'sdp_column_keys': (ctypes.c_int, [_COL, _P, _P, _P]),
     'sdp_pass2': (ctypes.c_int, [_COL, _D, _P, _I32, _I32, _D, _D, _P, _I64, _P, _P, _P]),
     'sdp_table_clear': (ctypes.c_int, [_P, _P, _I64, _I32, _P]),
@@ -143,7 +147,8 @@ _SIGNATURES = {
 
 _VALUE_FUNCS = {'sdp_last_error', 'sdp_version', 'sdp_pass1_workspace_bytes', 'sdp_pass2_workspace_bytes',
                 'sdp_pass1_grid', 'sdp_gram_workspace_bytes', 'sdp_part_rows_per_block', 'sdp_part_bucket_target',
-                'sdp_scan_workspace_bytes', 'sdp_bitmap_workspace_bytes', 'sdp_select_kth_workspace_bytes'}
+                'sdp_scan_workspace_bytes', 'sdp_bitmap_workspace_bytes', 'sdp_select_kth_workspace_bytes',
+                'sdp_select_rounds'}
 _STATUS_FUNCS = set(_SIGNATURES) - _VALUE_FUNCS
 
 _lib = None

@@ -35,6 +35,9 @@ class LocalComm:
     def allreduce_sum(self, t: torch.Tensor) -> torch.Tensor:
         return t
 
+    def allreduce_sum_(self, t: torch.Tensor) -> torch.Tensor:
+        return t
+
     def alltoallv(self, send: torch.Tensor, send_counts: List[int]) -> torch.Tensor:
         assert len(send_counts) == 1
         return send
@@ -80,6 +83,17 @@ class TorchComm:
         x = self._io(t.contiguous()).clone()
         self.dist.all_reduce(x, op=self.dist.ReduceOp.SUM, group=self.group)
         return x.to(t.device)
+
+    def allreduce_sum_(self, t):
+        """In-place sum.  With RCCL the collective is ordered on the current
+        stream and the host does not wait (device-driven radix rounds)."""
+        if self.cpu:
+            x = t.cpu()
+            self.dist.all_reduce(x, op=self.dist.ReduceOp.SUM, group=self.group)
+            t.copy_(x)
+        else:
+            self.dist.all_reduce(t, op=self.dist.ReduceOp.SUM, group=self.group)
+        return t
 
     def alltoallv(self, send, send_counts):
         """send is laid out rank-major (send_counts[r] elements for rank r)."""

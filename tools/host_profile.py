@@ -11,6 +11,8 @@ import time
 sys.path.insert(0, 'spark-df-profiling_amd')
 sys.path.insert(0, '.')
 import torch  # noqa: E402
+from spark_df_profiling import plot  # noqa: E402
+plot.start_pool()
 
 import bench  # noqa: E402
 from spark_df_profiling import describe  # noqa: E402
@@ -33,5 +35,5 @@ torch.cuda.synchronize()
 pr.disable()
 os.makedirs('gpurun_out', exist_ok=True)
 st = pstats.Stats(pr)
-st.sort_stats('cumulative').print_stats(45)
+st.sort_stats('cumulative').print_stats(70)
 st.sort_stats('tottime').print_stats(30)

@@ -7,6 +7,8 @@ Run with one GPU per rank over RCCL, or several ranks sharing one GPU over gloo:
 import os
 import sys
 
+os.environ.setdefault('SDP_PLOT_WORKERS', '0')      # render inline (no pool in this check)
+
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 for p in (ROOT, os.path.join(ROOT, 'spark-df-profiling_amd'), os.path.join(ROOT, 'tests')):
     sys.path.insert(0, p)
@@ -52,7 +54,17 @@ def main():
         start = rank * per
         stop = n if rank == world - 1 else start + per
         shard = full.slice_rows(start, stop)
-        got = describe(shard, comm=comm, plots=False)
+        plots = name == 'numeric'
+        got = describe(shard, comm=comm, plots=plots)
+        if plots:
+            # each rank rendered its own columns; every rank must hold all images
+            v = got['variables']
+            num = v[v['type'] == 'NUM']
+            bad = [c for c in num.index if not str(num.loc[c, 'histogram']).startswith('data:image/png')
+                   or not str(num.loc[c, 'mini_histogram']).startswith('data:image/png')]
+            if bad:
+                failures += 1
+                print('[%s] rank %d missing images for %s' % (name, rank, bad), flush=True)
         if rank == 0:
             import oracle
             want = oracle.describe(t)
@@ -64,7 +76,7 @@ def main():
                 print('[%s] MISMATCH world=%d\n%s' % (name, world, e), flush=True)
     dist.barrier()
     dist.destroy_process_group()
-    if rank == 0 and failures:
+    if failures:
         sys.exit(1)
 
 
