@@ -100,7 +100,7 @@ def describe_1d(engine: Engine, col: DeviceColumn, nrows, bins, k, freq, bundle)
     if col.kind == 'null':
         distinct, count = 0, 0
     elif numeric:
-        p1_pack = engine.numeric_pass1(col)
+        p1_pack = bundle.pop('p1_pack', None) or engine.numeric_pass1(col)
         p1 = p1_pack[0]
         count = p1['count']
         hint = p1['n_valid']
@@ -161,6 +161,12 @@ def describe_1d(engine: Engine, col: DeviceColumn, nrows, bins, k, freq, bundle)
     else:
         res['mode'] = 0
     return res
+
+
+def _is_numeric(col):
+    st = col.spark_type
+    nested = ('array' in st) or ('struct' in st) or ('map' in st) or col.kind == 'nested'
+    return col.kind != 'null' and not nested and (st in INT_TYPES or st in ('float', 'double'))
 
 
 def _numeric_series(st, nrows):
@@ -260,6 +266,11 @@ def describe(df, bins=10, corr_reject=0.9, **kwargs):
         return res, fut
 
     workers = column_workers(engine, kwargs.pop('workers', None))
+    if workers == 1:
+        # pass 1 of every numeric column queued back to back (two readbacks in all)
+        num_cols = [c for c in table.columns if _is_numeric(c)]
+        for col, pack in zip(num_cols, engine.numeric_pass1_batch(num_cols)):
+            bundles[col.name]['p1_pack'] = pack
     if workers > 1:
         done = _describe_concurrent(engine, table.columns, one, workers)
     else:

@@ -218,7 +218,7 @@ class Engine:
         p.shift = 0.0
         return self._to_dev(p), p
 
-    def pass1(self, col: DeviceColumn, plan_dev, plan):
+    def _pass1_launch(self, col: DeviceColumn, plan_dev, plan, res_dev=None):
         n = col.length
         grid = sdp.sdp_pass1_grid(n, col.dtype)
         work = self._bytes(sdp.sdp_pass1_workspace_bytes(n, col.dtype))
@@ -240,13 +240,18 @@ class Engine:
         cap = -(-cap // nat.PASS1_WAVES) + 64 if cap else 0
         cand = self._u64(max(nw, 1) * nseg * max(cap, 1))
         cand_counts = torch.zeros(max(nw, 1) * nseg, dtype=torch.int32, device=self.device)
-        res_dev = self._bytes(ctypes.sizeof(nat.SdpPass1Result))
+        if res_dev is None:
+            res_dev = self._bytes(ctypes.sizeof(nat.SdpPass1Result))
         cs = col.sdp()
         nat.annotate(_label(col), col_read_bytes(col))
         sdp.sdp_pass1(ctypes.byref(cs), ptr(plan_dev), ptr(work), work.numel(), ptr(cand), ptr(cand_counts), cap,
                       ptr(res_dev), self._s())
-        local = self._read(res_dev, nat.SdpPass1Result)
-        return local, {'cand': cand, 'counts': cand_counts, 'nseg': nseg, 'cap': cap}
+        return {'cand': cand, 'counts': cand_counts, 'nseg': nseg, 'cap': cap, 'res_dev': res_dev}
+
+    def pass1(self, col: DeviceColumn, plan_dev, plan):
+        info = self._pass1_launch(col, plan_dev, plan)
+        local = self._read(info['res_dev'], nat.SdpPass1Result)
+        return local, info
 
     def merge_pass1(self, local: nat.SdpPass1Result):
         """All-gather the per-rank pass-1 states and merge them in rank order."""
@@ -477,6 +482,47 @@ class Engine:
         plan_dev, plan = self.plan(col, probs)
         local, cand_info = self.pass1(col, plan_dev, plan)
         return self.merge_pass1(local), plan, cand_info
+
+    def numeric_pass1_batch(self, cols, probs=PROBS):
+        """numeric_pass1 of several columns with the GPU work queued back to
+        back: every column's sample + quantile plan, ONE readback of the plans,
+        every column's pass 1, ONE readback (one all-gather on a sharded table)
+        of the results.  Two host round trips for the whole table instead of two
+        per column; results are identical to numeric_pass1 column by column."""
+        if not cols:
+            return []
+        world = self.comm.world
+        ns = max(1, SAMPLE_TOTAL // world)
+        s = self._s()
+        samples = self._u64(len(cols) * ns)
+        for i, col in enumerate(cols):
+            cs = col.sdp()
+            sdp.sdp_sample_keys(ctypes.byref(cs), ns, ptr(samples[i * ns:]), s)
+        if world > 1:
+            parts = [p.view(len(cols), ns) for p in self.comm.allgather(samples)]
+        pr = self._h2d(np.array(list(probs), dtype=np.float64))
+        psz = ctypes.sizeof(nat.SdpQPlan)
+        plans_dev = self._bytes(len(cols) * psz)
+        for i, col in enumerate(cols):
+            allk = torch.cat([p[i] for p in parts]) if world > 1 else samples[i * ns:(i + 1) * ns]
+            sdp.sdp_quantile_plan(ptr(allk), allk.numel(), ptr(pr), len(probs), int(col.is_float),
+                                  ptr(plans_dev[i * psz:]), s)
+        raw = plans_dev.cpu().numpy().tobytes()
+        plans = [nat.SdpQPlan.from_buffer_copy(raw[i * psz:(i + 1) * psz]) for i in range(len(cols))]
+        rsz = ctypes.sizeof(nat.SdpPass1Result)
+        res_all = self._bytes(len(cols) * rsz)
+        infos = []
+        for i, col in enumerate(cols):
+            infos.append(self._pass1_launch(col, plans_dev[i * psz:], plans[i], res_all[i * rsz:]))
+        if world == 1:
+            raw = res_all.cpu().numpy().tobytes()
+            merged = [merge_pass1_results([nat.SdpPass1Result.from_buffer_copy(raw[i * rsz:(i + 1) * rsz])])
+                      for i in range(len(cols))]
+        else:
+            ranks = [g.cpu().numpy().tobytes() for g in self.comm.allgather(res_all)]
+            merged = [merge_pass1_results([nat.SdpPass1Result.from_buffer_copy(r[i * rsz:(i + 1) * rsz])
+                                           for r in ranks]) for i in range(len(cols))]
+        return [(merged[i], plans[i], infos[i]) for i in range(len(cols))]
 
     def minmax_pass(self, col):
         """count / min / max of a date or timestamp column (describe.py:233)."""
