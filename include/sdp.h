@@ -128,6 +128,11 @@ int sdp_sample_keys(const sdp_column *col, int32_t n_sample, uint64_t *d_sample,
 int sdp_quantile_plan(uint64_t *d_sample, int32_t n_sample, const double *probs,
                       int32_t n_probs, int32_t is_float, sdp_qplan *d_plan,
                       void *stream);
+/* sdp_quantile_plan of n_cols columns in one launch (one workgroup each):
+ * samples [n_cols][n_sample], is_float [n_cols] (device), plans [n_cols]. */
+int sdp_quantile_plan_batch(uint64_t *d_samples, int32_t n_sample, int32_t n_cols,
+                            const double *probs, int32_t n_probs, const int32_t *d_is_float,
+                            sdp_qplan *d_plans, void *stream);
 
 #define SDP_PASS1_WAVES 4     /* waves per pass-1 workgroup = candidate segments per block */
 

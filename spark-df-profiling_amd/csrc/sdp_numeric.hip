@@ -102,10 +102,15 @@ __device__ void block_sort_keys(uint64_t *s, int n) {
     }
 }
 
+// one workgroup per column: column b's sample at sample + b * ns, plan at plan + b
 __global__ void __launch_bounds__(1024) quantile_plan_kernel(uint64_t *sample, int32_t ns,
                                                              const double *probs, int32_t np,
-                                                             int32_t is_float, sdp_qplan *plan) {
+                                                             int32_t is_float, const int32_t *is_float_v,
+                                                             sdp_qplan *plan) {
     __shared__ uint64_t s[SORT_MAX];
+    sample += (int64_t)blockIdx.x * ns;
+    plan += blockIdx.x;
+    if (is_float_v) is_float = is_float_v[blockIdx.x];
     for (int i = threadIdx.x; i < ns; i += blockDim.x) s[i] = sample[i];
     __syncthreads();
     block_sort_keys(s, ns);
@@ -1011,7 +1016,18 @@ extern "C" int sdp_quantile_plan(uint64_t *d_sample, int32_t n_sample, const dou
     if (n_sample < 1 || n_sample > SORT_MAX) return set_error(SDP_EINVAL, "sdp_quantile_plan: n_sample %d", n_sample);
     if (n_probs < 0 || n_probs > SDP_MAX_WINDOWS) return set_error(SDP_EINVAL, "sdp_quantile_plan: n_probs %d", n_probs);
     hipLaunchKernelGGL(quantile_plan_kernel, dim3(1), dim3(1024), 0, (hipStream_t)stream, d_sample, n_sample,
-                       d_probs, n_probs, is_float, d_plan);
+                       d_probs, n_probs, is_float, (const int32_t *)nullptr, d_plan);
+    return check_launch("quantile_plan_kernel");
+}
+
+extern "C" int sdp_quantile_plan_batch(uint64_t *d_samples, int32_t n_sample, int32_t n_cols, const double *d_probs,
+                                       int32_t n_probs, const int32_t *d_is_float, sdp_qplan *d_plans,
+                                       void *stream) {
+    if (n_sample < 1 || n_sample > SORT_MAX) return set_error(SDP_EINVAL, "sdp_quantile_plan_batch: n_sample %d", n_sample);
+    if (n_probs < 0 || n_probs > SDP_MAX_WINDOWS) return set_error(SDP_EINVAL, "sdp_quantile_plan_batch: n_probs %d", n_probs);
+    if (n_cols < 1 || d_is_float == nullptr) return set_error(SDP_EINVAL, "sdp_quantile_plan_batch: n_cols %d", n_cols);
+    hipLaunchKernelGGL(quantile_plan_kernel, dim3(n_cols), dim3(1024), 0, (hipStream_t)stream, d_samples, n_sample,
+                       d_probs, n_probs, 0, d_is_float, d_plans);
     return check_launch("quantile_plan_kernel");
 }
 

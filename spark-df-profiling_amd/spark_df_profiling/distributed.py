@@ -104,15 +104,9 @@ def exchange_bytes_groups(engine, tab):
         payload = col.data[idx]
     else:
         payload = torch.zeros(0, dtype=torch.uint8, device=engine.device)
-    byte_send = []
-    csum = 0
-    lens_list = lens.tolist() if lens.numel() else []
-    pos = 0
-    for r in range(world):
-        b = sum(lens_list[pos:pos + send[r]])
-        byte_send.append(b)
-        pos += send[r]
-        csum += b
+    # bytes per owner summed on the device (a host list of every group's
+    # length would cost seconds at tens of millions of groups)
+    byte_send = torch.zeros(world, dtype=torch.int64, device=engine.device).scatter_add_(0, owner, lens).tolist()
     rlens = comm.alltoallv(lens.contiguous(), send)
     rcnt = comm.alltoallv(cnt.contiguous(), send)
     rbytes = comm.alltoallv(payload.contiguous(), byte_send)

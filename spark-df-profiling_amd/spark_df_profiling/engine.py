@@ -499,14 +499,14 @@ class Engine:
             cs = col.sdp()
             sdp.sdp_sample_keys(ctypes.byref(cs), ns, ptr(samples[i * ns:]), s)
         if world > 1:
-            parts = [p.view(len(cols), ns) for p in self.comm.allgather(samples)]
+            # [cols, world * ns]: column i's pooled sample in rank order
+            samples = torch.cat([p.view(len(cols), ns) for p in self.comm.allgather(samples)], dim=1).contiguous()
         pr = self._h2d(np.array(list(probs), dtype=np.float64))
+        isf = self._h2d(np.array([int(c.is_float) for c in cols], dtype=np.int32))
         psz = ctypes.sizeof(nat.SdpQPlan)
         plans_dev = self._bytes(len(cols) * psz)
-        for i, col in enumerate(cols):
-            allk = torch.cat([p[i] for p in parts]) if world > 1 else samples[i * ns:(i + 1) * ns]
-            sdp.sdp_quantile_plan(ptr(allk), allk.numel(), ptr(pr), len(probs), int(col.is_float),
-                                  ptr(plans_dev[i * psz:]), s)
+        sdp.sdp_quantile_plan_batch(ptr(samples), ns * world, len(cols), ptr(pr), len(probs), ptr(isf),
+                                    ptr(plans_dev), s)
         raw = plans_dev.cpu().numpy().tobytes()
         plans = [nat.SdpQPlan.from_buffer_copy(raw[i * psz:(i + 1) * psz]) for i in range(len(cols))]
         rsz = ctypes.sizeof(nat.SdpPass1Result)
