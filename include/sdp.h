@@ -192,6 +192,9 @@ int sdp_select_step(const uint64_t *d_keys, const uint64_t *d_n, int64_t n_cap, 
                     uint64_t *d_result, void *stream);
 /* Sort <= 16384 keys in place (one workgroup, LDS bitonic). */
 int sdp_sort_small(uint64_t *d_keys, const uint64_t *d_n, void *stream);
+/* n_sets independent in-place sorts of n_each (<= 16384) keys, one launch
+ * (heavy-key samples of all columns). */
+int sdp_sort_small_batch(uint64_t *d_keys, int32_t n_each, int32_t n_sets, void *stream);
 /* Write the order-preserving keys of all na.drop rows (fallback select). */
 int sdp_column_keys(const sdp_column *col, uint64_t *d_out, uint64_t *d_out_n,
                     void *stream);

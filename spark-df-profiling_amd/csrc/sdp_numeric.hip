@@ -746,6 +746,16 @@ __global__ void __launch_bounds__(1024) sort_small_kernel(uint64_t *keys, const 
     for (int i = threadIdx.x; i < n; i += blockDim.x) keys[i] = s[i];
 }
 
+// n_sets independent sorts of n_each keys each (one workgroup per set)
+__global__ void __launch_bounds__(1024) sort_small_batch_kernel(uint64_t *keys, int32_t n_each) {
+    __shared__ uint64_t s[SORT_MAX];
+    keys += (int64_t)blockIdx.x * n_each;
+    for (int i = threadIdx.x; i < n_each; i += blockDim.x) s[i] = keys[i];
+    __syncthreads();
+    block_sort_keys(s, n_each);
+    for (int i = threadIdx.x; i < n_each; i += blockDim.x) keys[i] = s[i];
+}
+
 template <typename T>
 __global__ void column_keys_kernel(sdp_column col, uint64_t *out, uint64_t *out_n) {
     __shared__ uint64_t s_buf[STAGE];
@@ -1209,6 +1219,13 @@ extern "C" int sdp_select_step(const uint64_t *d_keys, const uint64_t *d_n, int6
 extern "C" int sdp_sort_small(uint64_t *d_keys, const uint64_t *d_n, void *stream) {
     hipLaunchKernelGGL(sort_small_kernel, dim3(1), dim3(1024), 0, (hipStream_t)stream, d_keys, d_n);
     return check_launch("sort_small_kernel");
+}
+
+extern "C" int sdp_sort_small_batch(uint64_t *d_keys, int32_t n_each, int32_t n_sets, void *stream) {
+    if (n_each < 1 || n_each > SORT_MAX || n_sets < 1)
+        return set_error(SDP_EINVAL, "sdp_sort_small_batch: n_each %d n_sets %d", n_each, n_sets);
+    hipLaunchKernelGGL(sort_small_batch_kernel, dim3(n_sets), dim3(1024), 0, (hipStream_t)stream, d_keys, n_each);
+    return check_launch("sort_small_batch_kernel");
 }
 
 extern "C" int sdp_column_keys(const sdp_column *col, uint64_t *d_out, uint64_t *d_out_n, void *stream) {

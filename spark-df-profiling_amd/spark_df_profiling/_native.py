@@ -110,6 +110,7 @@ _SIGNATURES = {
     'sdp_radix_hist': (ctypes.c_int, [_P, _P, _U64, _I32, _P, _P]),
     'sdp_radix_filter': (ctypes.c_int, [_P, _P, _U64, _I32, _P, _P, _P]),
     'sdp_sort_small': (ctypes.c_int, [_P, _P, _P]),
+    'sdp_sort_small_batch': (ctypes.c_int, [_P, _I32, _I32, _P]),
     'sdp_select_kth_workspace_bytes': (_I64, [_I64]),
     'sdp_select_kth': (ctypes.c_int, [_P, _P, _I64, _I64, _U64, _U64, _P, _I64, _P, _P]),
     'sdp_select_rounds': (ctypes.c_int, [_U64, _U64]),

@@ -163,6 +163,8 @@ class Engine:
         self.stream = stream
 
     # -- small helpers ----------------------------------------------------------
+    _heavy_pre = None
+
     def _s(self):
         return nat.stream_handle(self.stream)
 
@@ -507,13 +509,39 @@ class Engine:
         plans_dev = self._bytes(len(cols) * psz)
         sdp.sdp_quantile_plan_batch(ptr(samples), ns * world, len(cols), ptr(pr), len(probs), ptr(isf),
                                     ptr(plans_dev), s)
-        raw = plans_dev.cpu().numpy().tobytes()
-        plans = [nat.SdpQPlan.from_buffer_copy(raw[i * psz:(i + 1) * psz]) for i in range(len(cols))]
+        # heavy-key samples of the columns the partitioning path will group
+        # (single rank, >= 64 K rows), sorted on the GPU and read back with the
+        # plans; the host finds the heavy keys while pass 1 runs
+        hcols = [c for c in cols if world == 1 and c.length >= (1 << 16)]
+        hs = None
+        if hcols:
+            hs = self._u64(len(hcols) * PART_SAMPLE)
+            for i, col in enumerate(hcols):
+                cs = col.sdp()
+                sdp.sdp_part_sample(ctypes.byref(cs), None, PART_SAMPLE, ptr(hs[i * PART_SAMPLE:]), None, s)
+            sdp.sdp_sort_small_batch(ptr(hs), PART_SAMPLE, len(hcols), s)
+            raw = torch.cat([plans_dev, hs.view(torch.uint8)]).cpu().numpy()
+        else:
+            raw = plans_dev.cpu().numpy()
+        plans = [nat.SdpQPlan.from_buffer_copy(raw[i * psz:(i + 1) * psz].tobytes()) for i in range(len(cols))]
         rsz = ctypes.sizeof(nat.SdpPass1Result)
         res_all = self._bytes(len(cols) * rsz)
         infos = []
         for i, col in enumerate(cols):
             infos.append(self._pass1_launch(col, plans_dev[i * psz:], plans[i], res_all[i * rsz:]))
+        if hcols:
+            if self._heavy_pre is None:
+                self._heavy_pre = {}
+            hsn = raw[len(cols) * psz:].view(np.uint64).reshape(len(hcols), PART_SAMPLE)
+            for i, col in enumerate(hcols):
+                a = hsn[i]
+                a = a[:int(np.searchsorted(a, np.uint64(U64)))]      # valid rows sort before UINT64_MAX
+                if a.size == 0:
+                    self._heavy_pre[id(col)] = None
+                    continue
+                start = np.flatnonzero(np.concatenate(([True], a[1:] != a[:-1])))
+                cnt = np.diff(np.append(start, a.size))
+                self._heavy_pre[id(col)] = self._heavy_struct(a[start], cnt)
         if world == 1:
             raw = res_all.cpu().numpy().tobytes()
             merged = [merge_pass1_results([nat.SdpPass1Result.from_buffer_copy(raw[i * rsz:(i + 1) * rsz])])
@@ -553,6 +581,8 @@ class Engine:
         outside the partitions (describe.py:251's hot groups).  gather=True
         (fixed keys of a sharded table): the samples of all ranks are pooled,
         so every rank picks the same heavy keys."""
+        if not isb and not gather and self._heavy_pre and id(col) in self._heavy_pre:
+            return self._heavy_pre.pop(id(col))        # sampled with pass 1 (numeric_pass1_batch)
         ns = min(PART_SAMPLE, max(col.length, 1))
         s = self._s()
         h = self._u64(ns)
@@ -575,14 +605,19 @@ class Engine:
         if pos.size == 0:
             return None
         u, first, cnt = np.unique(hn[pos], return_index=True, return_counts=True)
+        return self._heavy_struct(u, cnt, first, pos, keep, isb)
+
+    def _heavy_struct(self, u, cnt, first=None, pos=None, keep=None, isb=False):
+        """Heavy keys (>= HEAVY_MIN sample occurrences, at most HEAVY_MAX by
+        count) from the sample's distinct hashes u (ascending) and counts."""
         sel = np.nonzero(cnt >= HEAVY_MIN)[0]
         if sel.size == 0:
             return None
         if sel.size > nat.HEAVY_MAX:
             sel = sel[np.argsort(-cnt[sel], kind='stable')[:nat.HEAVY_MAX]]
-        rows = pos[first[sel]]
         hv = {'h': self._h2d(u[sel].view(np.int64).copy()), 'n': int(sel.size)}
         if isb:
+            rows = pos[first[sel]]
             idx = self._h2d(rows.astype(np.int64))
             hv['k0'], hv['k1'], hv['meta'] = keep[0][idx].contiguous(), keep[1][idx].contiguous(), \
                 keep[2][idx].contiguous()

@@ -35,6 +35,17 @@ def _worker(rank, world, port, q):
         v = torch.arange(rank + 2, dtype=torch.int64)
         out['allgatherv'] = [x.tolist() for x in comm.allgatherv(v)]
         out['allreduce'] = comm.allreduce_sum(torch.tensor([rank + 1], dtype=torch.int64)).tolist()
+        # in-place all-reduce of a [Q, 2048] digit-histogram block (sharded radix select)
+        h = torch.zeros(3 * 2048, dtype=torch.int64)
+        h[rank * 2048 + 7] = 5
+        h[2 * 2048 + 11] = rank + 1
+        r_ = comm.allreduce_sum_(h)
+        out['allreduce_'] = (r_ is h, int(h[7]), int(h[2048 + 7]), int(h[2 * 2048 + 11]), int(h.sum()))
+        # histogram images: every rank ends with every rank's strings
+        imgs = {'c%d' % rank: ('h%d' % rank, 'm%d' % rank)}
+        for part in comm.allgather_object(dict(imgs)):
+            imgs.update(part)
+        out['images'] = sorted(imgs.items())
         # alltoallv (gloo emulation): rank r sends (r*10 + d) repeated d+1 times to rank d
         send = torch.cat([torch.full((d + 1,), rank * 10 + d, dtype=torch.int64) for d in range(world)])
         out['alltoallv'] = comm.alltoallv(send, [d + 1 for d in range(world)]).tolist()
@@ -77,6 +88,8 @@ def test_two_rank_merges():
         assert o['allgather'] == [[1.0, 0.0], [2.0, 10.0]]
         assert o['allgatherv'] == [[0, 1], [0, 1, 2]]
         assert o['allreduce'] == [3]
+        assert o['allreduce_'] == (True, 5, 5, 3, 13)
+        assert o['images'] == [('c0', ('h0', 'm0')), ('c1', ('h1', 'm1'))]
         want = []
         for src in range(world):
             want += [src * 10 + r] * (r + 1)
