@@ -42,6 +42,8 @@ def main():
         'numeric': datagen.numeric_table(40_000),
         'numeric_big': datagen.numeric_table(300_001, seed=11),
         'categorical': datagen.categorical_table(30_000),
+        # >= 64 K rows per rank: byte columns take the local partitioning path
+        'categorical_big': datagen.categorical_table(240_000, seed=9, card=(100, 100_000)),
         'dates': datagen.date_table(20_000),
         'corr': datagen.corr_table(20_000),
         'legacy': datagen.legacy_table(),
