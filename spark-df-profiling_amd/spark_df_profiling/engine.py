@@ -512,15 +512,24 @@ class Engine:
         # heavy-key samples of the columns the partitioning path will group
         # (single rank, >= 64 K rows), sorted on the GPU and read back with the
         # plans; the host finds the heavy keys while pass 1 runs
-        hcols = [c for c in cols if world == 1 and c.length >= (1 << 16)]
+        # (sharded: every column, PART_SAMPLE / world rows per rank pooled in
+        # rank order, the same keys on every rank -- group_sharded's gather)
+        hcols = [c for c in cols if world > 1 or c.length >= (1 << 16)]
+        hn_each = PART_SAMPLE // world * world
         hs = None
         if hcols:
-            hs = self._u64(len(hcols) * PART_SAMPLE)
+            nsr = hn_each // world
+            hs = self._u64(len(hcols) * nsr)
             for i, col in enumerate(hcols):
+                if col.length == 0:
+                    hs[i * nsr:(i + 1) * nsr].fill_(-1)
+                    continue
                 cs = col.sdp()
-                sdp.sdp_part_sample(ctypes.byref(cs), None, PART_SAMPLE, ptr(hs[i * PART_SAMPLE:]), None, s)
-            sdp.sdp_sort_small_batch(ptr(hs), PART_SAMPLE, len(hcols), s)
-            raw = torch.cat([plans_dev, hs.view(torch.uint8)]).cpu().numpy()
+                sdp.sdp_part_sample(ctypes.byref(cs), None, nsr, ptr(hs[i * nsr:]), None, s)
+            if world > 1:
+                hs = torch.cat([p.view(len(hcols), nsr) for p in self.comm.allgather(hs)], dim=1).contiguous()
+            sdp.sdp_sort_small_batch(ptr(hs), hn_each, len(hcols), s)
+            raw = torch.cat([plans_dev, hs.view(-1).view(torch.uint8)]).cpu().numpy()
         else:
             raw = plans_dev.cpu().numpy()
         plans = [nat.SdpQPlan.from_buffer_copy(raw[i * psz:(i + 1) * psz].tobytes()) for i in range(len(cols))]
@@ -532,7 +541,7 @@ class Engine:
         if hcols:
             if self._heavy_pre is None:
                 self._heavy_pre = {}
-            hsn = raw[len(cols) * psz:].view(np.uint64).reshape(len(hcols), PART_SAMPLE)
+            hsn = raw[len(cols) * psz:].view(np.uint64).reshape(len(hcols), hn_each)
             for i, col in enumerate(hcols):
                 a = hsn[i]
                 a = a[:int(np.searchsorted(a, np.uint64(U64)))]      # valid rows sort before UINT64_MAX
@@ -581,9 +590,11 @@ class Engine:
         outside the partitions (describe.py:251's hot groups).  gather=True
         (fixed keys of a sharded table): the samples of all ranks are pooled,
         so every rank picks the same heavy keys."""
-        if not isb and not gather and self._heavy_pre and id(col) in self._heavy_pre:
+        if not isb and gather == (self.comm.world > 1) and self._heavy_pre and id(col) in self._heavy_pre:
             return self._heavy_pre.pop(id(col))        # sampled with pass 1 (numeric_pass1_batch)
         ns = min(PART_SAMPLE, max(col.length, 1))
+        if gather and self.comm.world > 1:
+            ns = max(1, min(PART_SAMPLE // self.comm.world, col.length))   # pooled: PART_SAMPLE in all
         s = self._s()
         h = self._u64(ns)
         if col.length == 0:
