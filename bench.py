@@ -375,6 +375,7 @@ def main():
 
     raw = {}
     barrier()
+    ms0 = torch.cuda.memory_stats(device)
     rec = nat.start_recording()
     t0 = time.perf_counter()
     for i in range(args.steps):
@@ -382,6 +383,11 @@ def main():
     barrier()
     t1 = time.perf_counter()
     nat.stop_recording()
+    ms1 = torch.cuda.memory_stats(device)
+    # caching-allocator activity inside the timed steps (device mallocs/frees
+    # synchronise; the steady state should have none)
+    alloc = {k: ms1.get(k, 0) - ms0.get(k, 0) for k in ('num_device_alloc', 'num_device_free', 'num_alloc_retries')}
+    alloc['peak_reserved_gb'] = round(ms1.get('reserved_bytes.all.peak', 0) / 1e9, 1)
     elapsed = t1 - t0
     if comm is not None:
         el = torch.tensor([elapsed], dtype=torch.float64, device=device)
@@ -404,6 +410,7 @@ def main():
         'roofline': rl,
         'per_kernel': per_kernel,
         'resident_gb_per_gpu': round(table_bytes(table) / 1e9, 2),
+        'allocator': alloc,
         'gen_s': round(t_gen, 1),
     }
     if world == 1 and not args.no_cpu_baseline:

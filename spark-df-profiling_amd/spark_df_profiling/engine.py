@@ -309,6 +309,9 @@ class Engine:
 
     def resolve_quantiles(self, col, p1: dict, plan, cand_info, probs=PROBS):
         """Order statistics for each requested probability (describe.py:203-208)."""
+        return self._quantiles_finish(self._quantiles_launch(col, p1, plan, cand_info, probs))
+
+    def _quantiles_launch(self, col, p1: dict, plan, cand_info, probs=PROBS):
         n = p1['count']
         is_int = not col.is_float
         nw = plan.n_windows
@@ -352,9 +355,9 @@ class Engine:
                 queued.append((r, arr, arr_n, arr.numel(), r, 0, EMPTY64))
                 key = 'queued'
             values[r] = key
+        res = None
         if queued and self.comm.world > 1:
-            for (r, *_), key in zip(queued, self._select_sharded(queued)):
-                values[r] = key
+            res = self._select_sharded(queued)
         elif queued:
             # every select of the column runs back to back on the stream; one readback
             cap = max(q[3] for q in queued)
@@ -363,8 +366,17 @@ class Engine:
             for i, (r, arr, arr_n, ncap, kk, lo, hi) in enumerate(queued):
                 sdp.sdp_select_kth(ptr(arr), ptr(arr_n), ncap, int(kk), _u(lo), _u(hi), ptr(work), work.numel(),
                                    ptr(res[i:]), self._s())
-            for (r, *_), key in zip(queued, self._host_u64(res)):
+        # dense / fallback arrays stay referenced until the results are read
+        return {'queued': queued, 'res': res, 'values': values, 'needed': needed, 'is_int': is_int,
+                'probs': probs, 'fallback': fallback, 'dense': dense}
+
+    def _quantiles_finish(self, st):
+        values, needed, is_int = st['values'], st['needed'], st['is_int']
+        if st['queued']:
+            keys = self._host_u64(st['res'])
+            for (r, *_), key in zip(st['queued'], keys):
                 values[r] = key
+        probs, fallback = st['probs'], st['fallback']
         out = {}
         for p in probs:
             pos, lo_r, hi_r = needed[p]
@@ -408,7 +420,7 @@ class Engine:
                 if rd < rounds[i]:
                     sdp.sdp_select_step(ptr(arr), ptr(arr_n), ncap, rd, int(rd == rounds[i] - 1),
                                         ptr(works[i][0]), works[i][1], ptr(hist[i * 2048:]), ptr(res[i:]), s)
-        return self._host_u64(res)
+        return res
 
     def _compact(self, cand_info, w):
         nseg, cap = cand_info['nseg'], cand_info['cap']

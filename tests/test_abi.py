@@ -82,3 +82,15 @@ def test_part_argument_checks_without_gpu():
         _native.sdp.sdp_scan_u32(None, 0, None, None, 0, None)
     assert _native.sdp.sdp_part_rows_per_block(10 ** 9, 0) % 4096 == 0
     assert _native.sdp.sdp_part_bucket_target(1, 1) == 2048
+
+
+def test_select_rounds_host_arithmetic():
+    """sdp_select_rounds (host-only): 11-bit radix rounds a select over
+    [lo, hi] needs -- every rank of a sharded select runs exactly this many
+    hist / all-reduce / step rounds."""
+    from spark_df_profiling._native import sdp
+    assert sdp.sdp_select_rounds(5, 5) == 1
+    assert sdp.sdp_select_rounds(0, 2047) == 1
+    assert sdp.sdp_select_rounds(0, 2048) == 2
+    assert sdp.sdp_select_rounds(1 << 40, (1 << 40) + 5) == 1
+    assert sdp.sdp_select_rounds(0, (1 << 64) - 1) == 6
