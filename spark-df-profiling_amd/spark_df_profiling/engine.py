@@ -164,6 +164,7 @@ class Engine:
 
     # -- small helpers ----------------------------------------------------------
     _heavy_pre = None
+    _near_unique = frozenset()
 
     def _s(self):
         return nat.stream_handle(self.stream)
@@ -553,6 +554,7 @@ class Engine:
         if hcols:
             if self._heavy_pre is None:
                 self._heavy_pre = {}
+                self._near_unique = set()
             hsn = raw[len(cols) * psz:].view(np.uint64).reshape(len(hcols), hn_each)
             for i, col in enumerate(hcols):
                 a = hsn[i]
@@ -563,6 +565,8 @@ class Engine:
                 start = np.flatnonzero(np.concatenate(([True], a[1:] != a[:-1])))
                 cnt = np.diff(np.append(start, a.size))
                 self._heavy_pre[id(col)] = self._heavy_struct(a[start], cnt)
+                if start.size >= 0.9 * a.size:
+                    self._near_unique.add(id(col))
         if world == 1:
             raw = res_all.cpu().numpy().tobytes()
             merged = [merge_pass1_results([nat.SdpPass1Result.from_buffer_copy(raw[i * rsz:(i + 1) * rsz])])
@@ -733,7 +737,9 @@ class Engine:
             out_key, out_cnt = self._u64(max(nrec, 1)), self._u64(max(nrec, 1))
         if nrec:
             nat.annotate('bytes' if isb else ('u64/counts' if with_counts else 'u64'), nrec * recw)
-            sdp.sdp_part_dedup(ctypes.byref(rf), int(isb), bref, ptr(starts), nfinal, int(with_counts) | (2 if large else 0),
+            direct = 4 if (not isb and not with_counts and not large and id(col) in self._near_unique) else 0
+            sdp.sdp_part_dedup(ctypes.byref(rf), int(isb), bref, ptr(starts), nfinal,
+                               int(with_counts) | (2 if large else 0) | direct,
                                ptr(out_key), ptr(out_cnt), ptr(ngroups), ptr(stats), s)
         both = self._host_u64(torch.cat([stats, hcnt[:hv['n']]]) if hv else stats)   # one readback
         st, hc = both[:68], both[68:]
@@ -860,7 +866,8 @@ class Engine:
             starts = o2[torch.from_numpy(sidx).to(self.device)].contiguous()
             ngroups = torch.zeros(nmy * nb2, dtype=torch.int32, device=self.device)
             nat.annotate('u64', nrecv * 8)
-            sdp.sdp_part_dedup(ctypes.byref(rf), 0, None, ptr(starts), nmy * nb2, 0, None, None, ptr(ngroups),
+            sdp.sdp_part_dedup(ctypes.byref(rf), 0, None, ptr(starts), nmy * nb2,
+                               4 if id(col) in self._near_unique else 0, None, None, ptr(ngroups),
                                ptr(stats), s)
         st = stats.clone()
         st[4] = st[4:68].sum()
