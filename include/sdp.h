@@ -176,12 +176,13 @@ int sdp_select_kth(const uint64_t *d_keys, const uint64_t *d_n, int64_t n_cap, i
                    uint64_t lo_key, uint64_t hi_key, void *d_work, int64_t work_bytes,
                    uint64_t *d_result, void *stream);
 /* The same select for a row-sharded table, one radix round per call: every
- * rank calls sdp_select_init once, then for round r = 0 .. rounds-1
- * sdp_select_hist (local digit histogram into d_hist[2048]), an all-reduce
- * (sum) of d_hist by the caller on the same stream, and sdp_select_step
- * (digit from the summed histogram; filter of the local keys unless last).
- * rounds = sdp_select_rounds(lo_key, hi_key).  No host round trip per round.
- * Workspace: sdp_select_kth_workspace_bytes(n_cap). */
+ * rank calls sdp_select_init and sdp_select_hist (round 0's local digit
+ * histogram into d_hist[2048]) once, then for round r = 0 .. rounds-1 an
+ * all-reduce (sum) of d_hist by the caller on the same stream and
+ * sdp_select_step (digit from the summed histogram; unless last, the local
+ * keys are filtered and counted by the next digit into d_hist, i.e. the
+ * histogram of round r + 1).  rounds = sdp_select_rounds(lo_key, hi_key).  No
+ * host round trip per round.  Workspace: sdp_select_kth_workspace_bytes(n_cap). */
 int sdp_select_rounds(uint64_t lo_key, uint64_t hi_key);
 int sdp_select_init(int64_t k, uint64_t lo_key, uint64_t hi_key, void *d_work, int64_t work_bytes,
                     int64_t n_cap, uint64_t *d_hist, void *stream);

@@ -737,6 +737,41 @@ __global__ void radix_filter_st_kernel(const uint64_t *keys, const uint64_t *n_p
     }
 }
 
+// filter of one round fused with the next round's digit histogram: the keys
+// that survive (prefix match after radix_decide_kernel moved the state on)
+// are compacted AND counted by their next digit, so a round costs one pass over
+// its candidates and two launches (decide, filter+hist) instead of three.
+__global__ void radix_filter_hist_st_kernel(const uint64_t *keys, const uint64_t *n_ptr, const SelState *st,
+                                            uint64_t *out, uint64_t *out_n, uint64_t *hist) {
+    if (st->done) return;
+    __shared__ uint64_t s_buf[STAGE];
+    __shared__ uint32_t s_cnt;
+    __shared__ uint64_t s_gbase;
+    __shared__ uint32_t h[2048];
+    for (int i = threadIdx.x; i < 2048; i += blockDim.x) h[i] = 0;
+    if (threadIdx.x == 0) s_cnt = 0;
+    __syncthreads();
+    Stager sg{s_buf, &s_cnt, &s_gbase};
+    const uint64_t n = *n_ptr, prefix = st->prefix;
+    const int shift = st->shift, top = shift + 11;
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    const uint64_t iters = (n + stride - 1) / stride;
+    for (uint64_t it = 0; it < iters; ++it) {
+        const uint64_t i = it * stride + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+        uint64_t k = 0;
+        bool keep = false;
+        if (i < n) {
+            k = keys[i];
+            keep = top >= 64 ? true : ((k >> top) == prefix);
+            if (keep) atomicAdd(&h[(k >> shift) & 2047u], 1u);
+        }
+        stage_push(sg, keep, k, out, (unsigned long long *)out_n, it + 1 == iters);
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < 2048; i += blockDim.x)
+        if (h[i]) atomicAdd((unsigned long long *)&hist[i], (unsigned long long)h[i]);
+}
+
 __global__ void __launch_bounds__(1024) sort_small_kernel(uint64_t *keys, const uint64_t *n_ptr) {
     __shared__ uint64_t s[SORT_MAX];
     const int n = (int)min((uint64_t)SORT_MAX, *n_ptr);
@@ -1144,15 +1179,15 @@ extern "C" int sdp_select_kth(const uint64_t *d_keys, const uint64_t *d_n, int64
     int rc = check_launch("select_init_kernel");
     if (rc) return rc;
     const uint64_t *cur = d_keys, *cur_n = d_n;
+    hipLaunchKernelGGL(radix_hist_st_kernel, dim3(512), dim3(256), 0, s, cur, cur_n, L.st, L.hist);
     for (int shift = shift0, r = 0;; shift -= 11, ++r) {
-        hipLaunchKernelGGL(radix_hist_st_kernel, dim3(512), dim3(256), 0, s, cur, cur_n, L.st, L.hist);
         hipLaunchKernelGGL(radix_decide_kernel, dim3(1), dim3(1024), 0, s, L.hist, L.st,
                            shift ? L.cnt[r & 1] : nullptr, d_result);
         if ((rc = check_launch("radix_decide_kernel"))) return rc;
         if (shift == 0) break;
-        hipLaunchKernelGGL(radix_filter_st_kernel, dim3(512), dim3(256), 0, s, cur, cur_n, L.st, L.buf[r & 1],
-                           L.cnt[r & 1]);
-        if ((rc = check_launch("radix_filter_st_kernel"))) return rc;
+        hipLaunchKernelGGL(radix_filter_hist_st_kernel, dim3(512), dim3(256), 0, s, cur, cur_n, L.st, L.buf[r & 1],
+                           L.cnt[r & 1], L.hist);
+        if ((rc = check_launch("radix_filter_hist_st_kernel"))) return rc;
         cur = L.buf[r & 1];
         cur_n = L.cnt[r & 1];
     }
@@ -1211,9 +1246,11 @@ extern "C" int sdp_select_step(const uint64_t *d_keys, const uint64_t *d_n, int6
                        d_result);
     if ((rc = check_launch("radix_decide_kernel"))) return rc;
     if (last) return 0;
-    hipLaunchKernelGGL(radix_filter_st_kernel, dim3(512), dim3(256), 0, s, cur, cur_n, L.st, L.buf[round & 1],
-                       L.cnt[round & 1]);
-    return check_launch("radix_filter_st_kernel");
+    // survivors compacted and counted by the next digit: d_hist then holds the
+    // local histogram of round + 1 (the caller all-reduces it before the next step)
+    hipLaunchKernelGGL(radix_filter_hist_st_kernel, dim3(512), dim3(256), 0, s, cur, cur_n, L.st, L.buf[round & 1],
+                       L.cnt[round & 1], d_hist);
+    return check_launch("radix_filter_hist_st_kernel");
 }
 
 extern "C" int sdp_sort_small(uint64_t *d_keys, const uint64_t *d_n, void *stream) {

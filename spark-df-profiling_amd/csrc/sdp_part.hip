@@ -700,27 +700,27 @@ __global__ void __launch_bounds__(CT) part_count_recs_kernel(const uint64_t *in_
     }
 }
 
-template <bool BYTES, int FTILE = S_TILE>
+template <bool BYTES>
 struct RecsLds {
     uint32_t hist[MAXB];
     uint32_t off[MAXB];
     uint64_t cur[MAXB];
-    uint64_t k0[BYTES ? B_S_TILE : FTILE];
+    uint64_t k0[BYTES ? B_S_TILE : S_TILE];
     uint64_t k1[BYTES ? B_S_TILE : 1];
     uint64_t meta[BYTES ? B_S_TILE : 1];
     uint16_t bkt[BYTES ? B_S_TILE : 1];     // fixed keys: the bucket is recomputed from the key
     uint32_t wsum[ST / WAVE];
 };
 
-template <bool BYTES, int FRPT = S_RPT>
+template <bool BYTES>
 __global__ void __launch_bounds__(ST) part_scatter_recs_kernel(const uint64_t *in_k0, const uint64_t *in_k1,
                                                                const uint64_t *in_meta, const Chunk *chunks,
                                                                int64_t nchunks, int b1, int b2, const uint64_t *offs,
                                                                uint64_t *out_k0, uint64_t *out_k1,
                                                                uint64_t *out_meta) {
-    constexpr int RPT = BYTES ? B_S_RPT : FRPT;
+    constexpr int RPT = BYTES ? B_S_RPT : S_RPT;
     constexpr int TILE = ST * RPT;
-    __shared__ RecsLds<BYTES, ST * FRPT> s;
+    __shared__ RecsLds<BYTES> s;
     const int t = threadIdx.x;
     const int nb = 1 << b2;
     const int shift = 64 - b1 - b2;

@@ -411,11 +411,11 @@ class Engine:
             sdp.sdp_select_init(int(kk), _u(lo), _u(hi), ptr(work), wb, ncap, ptr(hist[i * 2048:]), s)
             works.append((work, wb))
             rounds.append(sdp.sdp_select_rounds(_u(lo), _u(hi)))
+        for i, (r, arr, arr_n, ncap, kk, lo, hi) in enumerate(queued):
+            sdp.sdp_select_hist(ptr(arr), ptr(arr_n), ncap, 0, ptr(works[i][0]), works[i][1],
+                                ptr(hist[i * 2048:]), s)
         for rd in range(max(rounds)):
-            for i, (r, arr, arr_n, ncap, kk, lo, hi) in enumerate(queued):
-                if rd < rounds[i]:
-                    sdp.sdp_select_hist(ptr(arr), ptr(arr_n), ncap, rd, ptr(works[i][0]), works[i][1],
-                                        ptr(hist[i * 2048:]), s)
+            # (each step's filter leaves the next round's local histogram in hist)
             self.comm.allreduce_sum_(hist)
             for i, (r, arr, arr_n, ncap, kk, lo, hi) in enumerate(queued):
                 if rd < rounds[i]:
