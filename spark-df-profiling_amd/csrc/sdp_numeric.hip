@@ -655,7 +655,19 @@ __global__ void radix_hist_st_kernel(const uint64_t *keys, const uint64_t *n_ptr
     __syncthreads();
     const uint64_t n = *n_ptr, prefix = st->prefix;
     const int shift = st->shift, top = shift + 11;
-    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    // four independent loads in flight per thread before the LDS atomics
+    constexpr int R = 4;
+    for (; i + (R - 1) * stride < n; i += R * stride) {
+        uint64_t k[R];
+#pragma unroll
+        for (int r = 0; r < R; ++r) k[r] = keys[i + r * stride];
+#pragma unroll
+        for (int r = 0; r < R; ++r)
+            if (top >= 64 || (k[r] >> top) == prefix) atomicAdd(&h[(k[r] >> shift) & 2047u], 1u);
+    }
+    for (; i < n; i += stride) {
         const uint64_t k = keys[i];
         if (top >= 64 || (k >> top) == prefix) atomicAdd(&h[(k >> shift) & 2047u], 1u);
     }
