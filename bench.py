@@ -39,6 +39,7 @@ sys.path.insert(0, os.path.join(ROOT, 'spark-df-profiling_amd'))
 
 METRIC = 'profile rows/sec (whole node) + % HBM roofline, 1B-row x16 col at 1/2/4/8 GPUs'
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md:36 (spec)
+FP64_MFMA_PEAK_TFS = 78.6      # AMD spec for MI355X fp64 matrix (not in the local guide)
 NULL_P = 0.05
 SEED = 20261015
 
@@ -168,6 +169,40 @@ def make_c3_shard(rows_total, rank, world, device):
     return DeviceTable(cols, n)
 
 
+C5_COLS = 512
+C5_FACTORS = 4
+
+
+def make_c5_shard(rows_total, rank, world, device, ncols=C5_COLS):
+    """`rows_total` x `ncols` fp32, no nulls.  Each column is
+    a low-rank shared factor plus unit noise, x_j = F a_j + e_j with F ~ N(0,1)
+    (rows x 4) and loadings a_j ~ U(-1.5, 1.5)^4, so the Pearson matrix spans
+    (-1, 1); generated column by column in HBM from fixed seeds."""
+    from spark_df_profiling import _native as nat
+    from spark_df_profiling.columns import DeviceColumn, DeviceTable
+    per = rows_total // world
+    start = rank * per
+    n = per if rank < world - 1 else rows_total - start
+    g = _gen(SEED + 777 * 1000 + rank, device)
+    F = torch.randn(n, C5_FACTORS, generator=g, device=device, dtype=torch.float32)
+    gl = torch.Generator()
+    gl.manual_seed(SEED + 778)
+    L = ((torch.rand(C5_FACTORS, ncols, generator=gl, dtype=torch.float64) * 3.0 - 1.5)
+         .to(torch.float32).to(device))
+    cols = []
+    for j in range(ncols):
+        gj = _gen(SEED + (1000 + j) * 1000 + rank, device)
+        v = torch.randn(n, generator=gj, device=device, dtype=torch.float32)
+        v.add_(F @ L[:, j])
+        c = DeviceColumn('c%03d' % j, 'float', n, 'fixed', nat.F32)
+        c.values = v
+        c.validity = None
+        cols.append(c)
+    del F
+    torch.cuda.synchronize()
+    return DeviceTable(cols, n)
+
+
 def table_bytes(table):
     """Resident bytes of the shard (values, offsets, string bytes, validity)."""
     b = 0
@@ -226,25 +261,32 @@ def label_kernels(label):
     return []
 
 
-def pmc_traffic(label):
-    """HBM bytes per launch of the kernel(s) behind `label`, from the newest
-    committed PMC summary (profiles/*_traffic.json, tools/gpu_traffic.sh:
-    rocprofv3 FETCH_SIZE and WRITE_SIZE passes over this bench), or None."""
-    import glob
-    files = sorted(glob.glob(os.path.join(ROOT, 'profiles', '*_traffic.json')), key=os.path.getmtime)
-    if not files:
+# PMC traffic summary the bench reads `roofline.traffic` from, chosen by name
+# (never by file mtime, which a git checkout scrambles): the newest committed
+# summary of the default workload (tools/gpu_traffic.sh -> tools/traffic_summary.py).
+TRAFFIC_SUMMARY = {'c3': 'profiles/r01_bench1g_final_traffic.json', 'c5': None}
+
+
+def pmc_traffic(label, path):
+    """HBM bytes per launch of the kernel(s) behind `label` from the PMC
+    summary at `path` (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE passes over this
+    bench), or (None, None)."""
+    if not path:
         return None, None
-    with open(files[-1]) as fh:
+    full = path if os.path.isabs(path) else os.path.join(ROOT, path)
+    if not os.path.exists(full):
+        return None, None
+    with open(full) as fh:
         summ = json.load(fh)
     pre = label_kernels(label)
     hits = [v for k, v in summ['kernels'].items() if any(k.startswith(p) for p in pre)]
     if not hits:
         return None, None
     n = sum(v['dispatches'] for v in hits)
-    return sum(v['traffic_bytes'] * v['dispatches'] for v in hits) / n, os.path.basename(files[-1])
+    return sum(v['traffic_bytes'] * v['dispatches'] for v in hits) / n, path
 
 
-def roofline(rec, steps, step_s, prof_bytes):
+def roofline(rec, steps, step_s, prof_bytes, traffic_path=None):
     """Dominant kernel (entry point + label) by total HIP-event time -> achieved
     GB/s = its algorithmic bytes per launch / its mean launch duration."""
     torch.cuda.synchronize()
@@ -258,13 +300,13 @@ def roofline(rec, steps, step_s, prof_bytes):
     per_launch = nbytes[dom] / nl[dom]
     achieved = per_launch / (avg_ms * 1e-3) / 1e9
     prof_gbs = prof_bytes / step_s / 1e9
-    traffic, tsrc = pmc_traffic(dom)
+    traffic, tsrc = pmc_traffic(dom, traffic_path)
     out = {'bound': 'hbm', 'kernel': dom, 'achieved': round(achieved, 1), 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
            'frac': round(achieved / HBM_PEAK_GBS, 4),
            'traffic': int(traffic) if traffic is not None else None,
            'traffic_unit': 'bytes per launch (PMC FETCH_SIZE x2 + WRITE_SIZE)',
            'traffic_over_alg': round(traffic / per_launch, 3) if traffic is not None else None,
-           'traffic_source': ('profiles/' + tsrc) if tsrc else None,
+           'traffic_source': tsrc,
            'launches_per_step': nl[dom] // steps, 'avg_launch_ms': round(avg_ms, 4),
            'alg_bytes_per_launch': int(per_launch),
            'share_of_step': round(tot[dom] / steps / (step_s * 1e3), 3),
@@ -315,18 +357,44 @@ def cpu_baseline(sample_rows, device):
                       '(CPU restatement, not reference Spark: no pyspark/JVM in the image), %.1f s' % (sample_rows, dt)}
 
 
+def gram_roofline(rec, steps, ncols, n_rows):
+    """C5: the Pearson Gram on the fp64 matrix cores.  F_alg = n C (C + 1)
+    flop per launch (symmetric X^T X, one multiply-add per
+    unique entry) over the launch's average HIP-event duration."""
+    torch.cuda.synchronize()
+    ev = rec.get('sdp_gram', [])
+    if not ev:
+        return None
+    ms = sum(a.elapsed_time(b) for a, b, _ in ev) / len(ev)
+    flop = float(n_rows) * ncols * (ncols + 1)
+    tfs = flop / (ms * 1e-3) / 1e12
+    alg_bytes = sum(x for _, _, x in ev if x is not None) / len(ev)
+    return {'bound': 'mfma', 'kernel': 'sdp_gram (gram_wide_kernel + gram_reduce_kernel<128>, v_mfma_f64_16x16x4f64)',
+            'achieved': round(tfs, 2), 'peak': FP64_MFMA_PEAK_TFS, 'unit': 'TFLOP/s',
+            'frac': round(tfs / FP64_MFMA_PEAK_TFS, 4), 'traffic': None,
+            'flop_per_launch': flop, 'avg_launch_ms': round(ms, 4), 'launches_per_step': len(ev) // steps,
+            'hbm_alg_bytes_per_launch': int(alg_bytes),
+            'hbm_achieved_gbs': round(alg_bytes / (ms * 1e-3) / 1e9, 1)}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('--gpus', type=int, default=1)
     ap.add_argument('--steps', type=int, default=3)
     ap.add_argument('--warmup', type=int, default=1)
-    ap.add_argument('--rows', type=int, default=10 ** 9)
+    ap.add_argument('--workload', choices=('c3', 'c5'), default='c3',
+                    help='c3: 1e9 x 16 mixed (the metric); c5: 1e7 x 512 fp32 (Pearson on MFMA)')
+    ap.add_argument('--rows', type=int, default=None)
     ap.add_argument('--cpu-sample-rows', type=int, default=1 << 20)
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--no-plots', action='store_true')
+    ap.add_argument('--traffic', default=None, help='PMC traffic summary (default: TRAFFIC_SUMMARY[workload])')
     ap.add_argument('--workers', type=int, default=None,
                     help='columns profiled concurrently per GPU (default: SDP_COLUMN_WORKERS or 1)')
     args = ap.parse_args()
+    if args.rows is None:
+        args.rows = 10 ** 9 if args.workload == 'c3' else 10 ** 7
+    traffic_path = args.traffic if args.traffic is not None else TRAFFIC_SUMMARY.get(args.workload)
 
     if not args.no_plots:
         # histogram rendering workers (spawned before this process touches the GPU)
@@ -357,7 +425,10 @@ def main():
     from spark_df_profiling.engine import Engine
 
     t_gen = time.perf_counter()
-    table = make_c3_shard(args.rows, rank, world, device)
+    if args.workload == 'c3':
+        table = make_c3_shard(args.rows, rank, world, device)
+    else:
+        table = make_c5_shard(args.rows, rank, world, device)
     t_gen = time.perf_counter() - t_gen
 
     column_workers_used = column_workers(Engine(device=device, comm=comm), args.workers)
@@ -393,19 +464,29 @@ def main():
         el = torch.tensor([elapsed], dtype=torch.float64, device=device)
         elapsed = float(torch.stack(comm.allgather(el)).max().item())
     step_s = elapsed / args.steps
-    rl, per_kernel = roofline(rec, args.steps, step_s, profile_alg_bytes(table, raw))
+    rl, per_kernel = roofline(rec, args.steps, step_s, profile_alg_bytes(table, raw), traffic_path)
+    ncols = len(table.columns)
+    if args.workload == 'c5':
+        hbm_rl = rl
+        rl = gram_roofline(rec, args.steps, ncols, table.num_rows)
+        rl['hbm_dominant'] = {k: hbm_rl[k] for k in ('kernel', 'achieved', 'frac', 'avg_launch_ms')}
+        rl['whole_profile'] = hbm_rl['whole_profile']
 
     if rank != 0:
         return
+    if args.workload == 'c3':
+        workload = ('C3: %d rows x 16 mixed columns (6 f64, 4 i64, 2 f32, 3 utf8, 1 date32), 5%% nulls, '
+                    'row-sharded' % args.rows)
+    else:
+        workload = ('C5: %d rows x %d fp32 columns (low-rank factor + noise, no nulls), full describe() '
+                    'with the Pearson matrix on fp64 MFMA' % (args.rows, ncols))
     out = {
         'metric': METRIC, 'value': round(args.rows * args.steps / elapsed, 1), 'unit': 'rows/s',
         'n_gpus': world, 'steps': args.steps, 'warmup': args.warmup,
         'ms_per_step': round(1e3 * elapsed / args.steps, 2), 'higher_is_better': True, 'scaling': 'strong',
         'vs_baseline': None, 'dtype': 'f64', 'data': 'synthetic (torch, seeded, generated in HBM)',
-        'config': {'workload': 'C3: %d rows x 16 mixed columns (6 f64, 4 i64, 2 f32, 3 utf8, 1 date32), '
-                               '5%% nulls, row-sharded' % args.rows,
-                   'rows': args.rows, 'columns': 16, 'parallelism': 'row-shard x%d' % world,
-                   'plots': not args.no_plots,
+        'config': {'workload': workload, 'rows': args.rows, 'columns': ncols,
+                   'parallelism': 'row-shard x%d' % world, 'plots': not args.no_plots,
                    'column_workers': column_workers_used},
         'roofline': rl,
         'per_kernel': per_kernel,
@@ -413,7 +494,7 @@ def main():
         'allocator': alloc,
         'gen_s': round(t_gen, 1),
     }
-    if world == 1 and not args.no_cpu_baseline:
+    if world == 1 and not args.no_cpu_baseline and args.workload == 'c3':
         del table
         torch.cuda.empty_cache()
         out['cpu_baseline'] = cpu_baseline(args.cpu_sample_rows, device)

@@ -106,6 +106,28 @@ def _fsum(a):
     return math.fsum(a.tolist())
 
 
+_CHUNK = 1 << 16
+
+
+def _sum(a, fast=False):
+    """Exact sum (math.fsum) or, in the vectorised mode, numpy's pairwise sum
+    of 64 K-element chunks added exactly: error <= ~16 eps * sum|a|, far inside
+    the 1e-9 relative parity bound for every statistic built from it."""
+    if not fast:
+        return _fsum(a)
+    a = np.asarray(a, dtype=np.float64)
+    if a.size == 0:
+        return 0.0
+    if a.size <= _CHUNK:
+        return float(np.sum(a))
+    m = a.size // _CHUNK * _CHUNK
+    parts = np.sum(a[:m].reshape(-1, _CHUNK), axis=1).tolist()
+    parts.append(float(np.sum(a[m:])))
+    if not all(math.isfinite(x) for x in parts):
+        return float(np.sum(parts))
+    return math.fsum(parts)
+
+
 def _spark_gt(x, t):
     """Spark `x > t` with NaN ordered above every number (A.8)."""
     x = np.asarray(x, dtype=np.float64)
@@ -192,9 +214,11 @@ def hist_counts(xs, edges):
     return out
 
 
-def spark_percentile_exact(sorted_x, p):
-    """Spark `percentile` (A.4), used for int columns (describe.py:203-204)."""
-    n = len(sorted_x)
+def spark_percentile_exact(sorted_x, p, n=None):
+    """Spark `percentile` (A.4), used for int columns (describe.py:203-204).
+    `sorted_x` is the sorted column or a {rank: value} map of the two ranks
+    this p needs (then n is the column length)."""
+    n = len(sorted_x) if n is None else n
     position = (n - 1) * p
     lower = math.floor(position)
     higher = math.ceil(position)
@@ -216,7 +240,18 @@ def spark_percentile_approx_rank(n, p, relative_error=1e-4):
     return min(max(int(math.ceil(p * n)), 1), n)
 
 
-def numeric_stats(values, valid, is_int, nrows, bins, k):
+def _order_stats(x, ranks, fast):
+    """{rank: value} of 0-based order statistics of x (stable sort, or an
+    introselect partition at the needed ranks in the vectorised mode)."""
+    ranks = sorted(set(int(r) for r in ranks))
+    if not fast:
+        sx = np.sort(x, kind='stable')
+        return {r: sx[r] for r in ranks}
+    px = np.partition(x, ranks)
+    return {r: px[r] for r in ranks}
+
+
+def numeric_stats(values, valid, is_int, nrows, bins, k, fast=False):
     """All of describe_numeric_1d (describe.py:192-229) except the PNGs.
 
     Returns an OrderedDict in the reference's key order plus '_hist' (counts,
@@ -232,18 +267,20 @@ def numeric_stats(values, valid, is_int, nrows, bins, k):
     st = OrderedDict()
     # mean/min/max/variance/kurtosis/std/skewness/sum (:193-201)
     if is_int:
-        mean = _fsum(xs) / n
+        mean = _sum(xs, fast) / n
         mn, mx = float(xs_int.min()), float(xs_int.max())
         total = float(np.sum(xs_int, dtype=np.int64))          # LongType wraps (A.2)
     else:
-        mean = _fsum(xs) / n
+        mean = _sum(xs, fast) / n
         mn, mx = float(xs.min()), float(xs.max())
-        total = _fsum(xs)
+        total = _sum(xs, fast)
     d = xs - mean
-    c = _fsum(d)
-    m2 = _fsum(d * d) - c * c / n
-    m3 = _fsum(d * d * d) - 3.0 * c * _fsum(d * d) / n + 2.0 * c ** 3 / n ** 2
-    m4 = _fsum(d ** 4) - 4.0 * c * _fsum(d ** 3) / n + 6.0 * c * c * _fsum(d * d) / n ** 2 - 3.0 * c ** 4 / n ** 3
+    d2 = d * d
+    c, s2, s3, s4 = _sum(d, fast), _sum(d2, fast), _sum(d2 * d, fast), _sum(d2 * d2, fast)
+    del d2
+    m2 = s2 - c * c / n
+    m3 = s3 - 3.0 * c * s2 / n + 2.0 * c ** 3 / n ** 2
+    m4 = s4 - 4.0 * c * s3 / n + 6.0 * c * c * s2 / n ** 2 - 3.0 * c ** 4 / n ** 3
     variance = float('nan') if n == 1 else m2 / (n - 1.0)
     std = float('nan') if n == 1 else math.sqrt(max(variance, 0.0))
     skew = float('nan') if m2 == 0 else math.sqrt(n) * m3 / math.sqrt(m2 * m2 * m2)
@@ -257,11 +294,16 @@ def numeric_stats(values, valid, is_int, nrows, bins, k):
     st['skewness'] = skew
     st['sum'] = total
     # percentiles (:203-208)
-    sx = np.sort(xs_int if is_int else xs, kind='stable')
+    probs = [0.05, 0.25, 0.5, 0.75, 0.95]
+    if is_int:
+        need = [r for p in probs for r in (math.floor((n - 1) * p), math.ceil((n - 1) * p))]
+    else:
+        need = [spark_percentile_approx_rank(n, p) - 1 for p in probs]
+    sx = _order_stats(xs_int if is_int else xs, need, fast)
     qs = {}
-    for p in [0.05, 0.25, 0.5, 0.75, 0.95]:
+    for p in probs:
         if is_int:
-            q = spark_percentile_exact(sx, p)
+            q = spark_percentile_exact(sx, p, n)
         else:
             q = float(sx[spark_percentile_approx_rank(n, p) - 1])
         qs[p] = q
@@ -273,7 +315,7 @@ def numeric_stats(values, valid, is_int, nrows, bins, k):
         st['iqr'] = np.float64(q3) - np.float64(q1)
         st['cv'] = np.float64(std) / float(mean)
         # mad (:215-218): *mean* absolute deviation around the Spark mean
-        st['mad'] = np.float64(_fsum(np.abs(xs - mean))) / float(n)
+        st['mad'] = np.float64(_sum(np.abs(xs - mean), fast)) / float(n)
     st['type'] = 'NUM'
     # zeros (:220-221) over the full column (null excluded, NaN != 0, -0.0 == 0)
     vd = values[valid].astype(np.float64)
@@ -340,23 +382,53 @@ def _sort_key(v):
     return v
 
 
-def categorical_stats(arr, spark_t):
+def _value_counts_fast(arr, spark_t, k=50):
+    """(first k groups by (count desc, key asc), number of non-null rows,
+    number of groups) through Arrow's hash aggregation (exact counts); only
+    the groups at or above the k-th largest count are sorted by key."""
+    import pyarrow.compute as pc
+    a = arr.drop_null() if arr.null_count else arr
+    if pa.types.is_dictionary(a.type):
+        a = a.dictionary_decode()
+    vc = pc.value_counts(a)
+    keys = vc.field('values')
+    cnt = np.asarray(vc.field('counts').to_numpy(zero_copy_only=False), dtype=np.int64)
+    G = len(cnt)
+    if G > k:
+        thr = np.partition(cnt, G - k)[G - k]
+        sel = np.nonzero(cnt >= thr)[0]
+    else:
+        sel = np.arange(G)
+    sk = keys.take(pa.array(sel, pa.int64()))
+    vals = _py_values(sk, spark_t).tolist()
+    groups = sorted(zip(vals, cnt[sel].tolist()), key=lambda kv: (-kv[1], _sort_key(kv[0])))[:k]
+    return groups, len(a), G
+
+
+def categorical_stats(arr, spark_t, fast=False):
     """describe_categorical_1d (describe.py:250-271).  Group order: count desc,
     then key asc (the defined tie-break; the reference's orderBy is unstable)."""
+    if fast:
+        top50, nvals, ngroups = _value_counts_fast(arr, spark_t, 50)
+        return _categorical_series(top50, nvals, ngroups)
     idx = _nonnull_values(arr, spark_t)
     vals = _py_values(arr.take(pa.array(idx, pa.int64())), spark_t)
     counts = {}
     for x in vals.tolist():
         counts[x] = counts.get(x, 0) + 1
     groups = sorted(counts.items(), key=lambda kv: (-kv[1], _sort_key(kv[0])))
+    return _categorical_series(groups[:50], len(vals), len(groups))
+
+
+def _categorical_series(top50, nvals, ngroups):
+    groups = top50
     st = OrderedDict()
     st['top'] = groups[0][0]
     st['freq'] = np.int64(groups[0][1])
-    top50 = groups[:50]
     top_keys = [g[0] for g in top50]
     top_counts = [g[1] for g in top50]
-    others_count = len(vals) - sum(top_counts)
-    others_distinct = len(groups) - len(top50)
+    others_count = nvals - sum(top_counts)
+    others_distinct = ngroups - len(top50)
     vc = pd.Series(top_counts + [others_count, others_distinct],
                    index=pd.Index(top_keys + ['***Other Values***', '***Other Values Distinct Count***'],
                                   dtype=object),
@@ -366,10 +438,15 @@ def categorical_stats(arr, spark_t):
     return st
 
 
-def date_stats(arr, spark_t, distinct_count, freq):
+def date_stats(arr, spark_t, distinct_count, freq, fast=False):
     """describe_date_1d (describe.py:232-247)."""
-    idx = _nonnull_values(arr, spark_t)
-    vals = _py_values(arr.take(pa.array(idx, pa.int64())), spark_t)
+    if fast:
+        import pyarrow.compute as pc
+        mm = pc.min_max(arr)
+        vals = _py_values(pa.array([mm['min'].as_py(), mm['max'].as_py()], arr.type), spark_t)
+    else:
+        idx = _nonnull_values(arr, spark_t)
+        vals = _py_values(arr.take(pa.array(idx, pa.int64())), spark_t)
     mn, mx = min(vals), max(vals)
     st = OrderedDict()
     if isinstance(mx, pd.Timestamp):
@@ -388,7 +465,9 @@ def date_stats(arr, spark_t, distinct_count, freq):
 # describe_1d (describe.py:136-189)
 # ----------------------------------------------------------------------------
 
-def _distinct_count(arr, spark_t):
+def _distinct_count(arr, spark_t, fast=False):
+    if fast and spark_t != 'null':
+        return _distinct_count_fast(arr, spark_t)
     valid = _valid_mask(arr)
     if spark_t in _INT_TYPES:
         return int(np.unique(_numeric_values(arr, spark_t)[valid]).size)
@@ -400,10 +479,25 @@ def _distinct_count(arr, spark_t):
     return len(set(_sort_key(x) for x in vals.tolist()))
 
 
-def describe_1d(arr, spark_t, nrows, bins, k, freq, raw):
+def _distinct_count_fast(arr, spark_t):
+    """countDistinct: numeric keys by an in-place sort and a count of key
+    changes, other types by Arrow's hash kernel -- the semantics of the exact
+    count above."""
+    valid = _valid_mask(arr)
+    if spark_t in _INT_TYPES or spark_t in ('float', 'double'):
+        v = _numeric_values(arr, spark_t)[valid]
+        k = v if spark_t in _INT_TYPES else _canon_float_keys(v)
+        k.sort()
+        return int(k.size and 1 + np.count_nonzero(k[1:] != k[:-1]))
+    import pyarrow.compute as pc
+    a = arr.dictionary_decode() if pa.types.is_dictionary(arr.type) else arr
+    return int(pc.count_distinct(a, mode='only_valid').as_py())
+
+
+def describe_1d(arr, spark_t, nrows, bins, k, freq, raw, fast=False):
     if ('array' in spark_t) or ('struct' in spark_t) or ('map' in spark_t):
         raise NotImplementedError('Column {c} is of type {t} and cannot be analyzed'.format(c=raw['name'], t=spark_t))
-    distinct = _distinct_count(arr, spark_t)
+    distinct = _distinct_count(arr, spark_t, fast)
     valid = _valid_mask(arr) if spark_t != 'null' else np.zeros(len(arr), bool)
     if spark_t in ('float', 'double'):
         cnt = int(np.sum(valid & ~np.isnan(_numeric_values(arr, spark_t))))
@@ -430,18 +524,18 @@ def describe_1d(arr, spark_t, nrows, bins, k, freq, raw):
                               else pd.Series([], dtype=object).value_counts())
     elif spark_t in _INT_TYPES or spark_t in ('float', 'double'):
         is_int = spark_t in _INT_TYPES
-        st = numeric_stats(_numeric_values(arr, spark_t), valid, is_int, nrows, bins, k)
+        st = numeric_stats(_numeric_values(arr, spark_t), valid, is_int, nrows, bins, k, fast)
         raw['hist'] = st.pop('_hist')
         raw['thresholds'] = st.pop('_thresholds')
         st['histogram'] = None            # filled by the caller (PNG renderer or None)
         st['mini_histogram'] = None
     elif spark_t in _DATE_TYPES:
-        st = date_stats(arr, spark_t, distinct, freq.upper())
+        st = date_stats(arr, spark_t, distinct, freq.upper(), fast)
     elif bool(res['is_unique']):
         st = OrderedDict([('type', 'UNIQUE')])
         st['value_counts'] = _first_values_series(arr, spark_t, 50)
     else:
-        st = categorical_stats(arr, spark_t)
+        st = categorical_stats(arr, spark_t, fast)
     res.update(st)
     if res['type'] == 'CAT' and res['n_missing'] > 0:          # :169-170
         res['distinct_count'] += 1
@@ -462,7 +556,7 @@ def describe_1d(arr, spark_t, nrows, bins, k, freq, raw):
 # corr_matrix (utils.py:20-36) and describe (describe.py:66-133)
 # ----------------------------------------------------------------------------
 
-def corr_matrix(table, columns):
+def corr_matrix(table, columns, fast=False):
     """Pearson on rows with no null/NaN in any of `columns` (utils.py:27-31)."""
     keep = np.ones(table.num_rows, bool)
     mats = []
@@ -477,7 +571,7 @@ def corr_matrix(table, columns):
     C = len(columns)
     out = np.full((C, C), np.nan)
     if n > 0:
-        means = np.array([_fsum(X[:, j]) / n for j in range(C)])
+        means = np.array([_sum(X[:, j], fast) / n for j in range(C)])
         Xc = X - means
         G = Xc.T @ Xc
         with np.errstate(all='ignore'):
@@ -498,7 +592,16 @@ def profile_raw(table, bins=10, corr_reject=0.9, **kwargs):
     return _describe_with_raw(table, bins, corr_reject, None, **kwargs)
 
 
-def _describe_with_raw(table, bins, corr_reject, plot, **kwargs):
+def _describe_column(args):
+    """describe_1d of one column (picklable unit of work for describe_fast's
+    process pool)."""
+    arr, t, n, bins, k, freq, name, fast = args
+    raw = {'name': name, 'spark_type': t}
+    s = describe_1d(arr, t, n, bins, k, freq, raw, fast)
+    return s, raw
+
+
+def _describe_with_raw(table, bins, corr_reject, plot, fast=False, pool=None, **kwargs):
     if isinstance(table, pa.RecordBatch):
         table = pa.Table.from_batches([table])
     if not isinstance(table, pa.Table):
@@ -510,11 +613,12 @@ def _describe_with_raw(table, bins, corr_reject, plot, **kwargs):
     k_vals, t_freq = kwargs.get('k_vals') or {}, kwargs.get('t_freq') or {}
     ldesc = OrderedDict()
     raws = OrderedDict()
+    jobs = []
     for name in table.column_names:
         arr = _column(table, name)
-        t = spark_type_of(arr.type)
-        raw = {'name': name, 'spark_type': t}
-        s = describe_1d(arr, t, n, bins, k_vals.get(name, 2), t_freq.get(name, 'D'), raw)
+        jobs.append((arr, spark_type_of(arr.type), n, bins, k_vals.get(name, 2), t_freq.get(name, 'D'), name, fast))
+    results = list(pool.map(_describe_column, jobs)) if pool is not None else [_describe_column(j) for j in jobs]
+    for name, (s, raw) in zip(table.column_names, results):
         if 'histogram' in s and plot is not None:
             h = raw['hist']
             frame = pd.DataFrame({'bin_id': np.arange(len(h['counts'])), 'count': h['counts'],
@@ -528,7 +632,7 @@ def _describe_with_raw(table, bins, corr_reject, plot, **kwargs):
     if corr_reject is not None:
         computable = [c for c in ldesc if ldesc[c]['type'] == 'NUM']
         if len(computable) > 0:
-            corr = corr_matrix(table, computable)
+            corr = corr_matrix(table, computable, fast)
             for x, corr_x in corr.iterrows():
                 for y, cv in corr_x.items():
                     if x == y:

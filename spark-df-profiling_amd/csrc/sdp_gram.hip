@@ -321,6 +321,200 @@ __global__ void __launch_bounds__(G_BLOCK) gram_kernel(const GramCol *cols, int 
     }
 }
 
+// ---- wide tables (C > 64): 128 x 128 output tiles staged through LDS ---------
+//
+// One 512-thread workgroup owns output tile (ti, tj) (ti <= tj, 128 columns
+// each) for one row chunk.  Per k-step of GW_KR = 32 rows the workgroup stages
+// both column panels ONCE into LDS as shifted, masked fp64 ((x - K) or 0 for a
+// dropped row), so the dtype conversion is paid once per element per tile
+// instead of once per wave; every wave then runs its MFMAs from LDS.  Wave w
+// owns the 64 x 32 quadrant (qa = w >> 2, qb = w & 3) of the tile: 8
+// accumulators, no cross-wave reduction (each wave writes its quadrant of the
+// chunk partial).  On a diagonal tile the two quadrants wholly below the
+// diagonal are skipped (the reduce mirrors the upper triangle).  The next
+// k-step's raw loads are issued before the MFMA phase, so HBM latency hides
+// behind the matrix work.  Blocks are mapped XCD-major: the tiles of one row
+// chunk run on one XCD and share its L2 for the column reads.
+//
+// LDS panel layout [col][row] with a pitch of 34 doubles (68 dwords = 4 mod 64
+// banks): an MFMA operand read (lane (q, cl) -> col 16a + cl, row 4kk + q)
+// touches 64 distinct banks per 32-lane group.
+constexpr int GW_TILE = 128;
+constexpr int GW_WAVES = 8;
+constexpr int GW_BLOCK = GW_WAVES * WAVE;
+constexpr int GW_KR = 32;                              // rows per k-step
+constexpr int GW_PITCH = 34;                           // doubles per column (32 rows + pad)
+constexpr int GW_SLOTS = 2 * GW_TILE * (GW_KR / 4) / GW_BLOCK;   // (col, 4-row quad) per thread: 4
+
+struct GwRaw {
+    u32x4 lo, hi;
+};
+
+__device__ __forceinline__ void gw_load(const GramCol &gc, int64_t r, int64_t n, GwRaw &x) {
+    if (gc.dtype == 0) return;
+    const char *base = (const char *)gc.p + r * gc.width;
+    if (r + 4 <= n) {
+        switch (gc.width) {
+        case 8: {
+            const __attribute__((address_space(1))) u32x4 *b = (const __attribute__((address_space(1))) u32x4 *)base;
+            x.lo = b[0];
+            x.hi = b[1];
+        } break;
+        case 4: x.lo = *(const __attribute__((address_space(1))) u32x4 *)base; break;
+        case 2: {
+            typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+            const u32x2 v = *(const __attribute__((address_space(1))) u32x2 *)base;
+            x.lo[0] = v[0];
+            x.lo[1] = v[1];
+        } break;
+        default: x.lo[0] = *(const __attribute__((address_space(1))) uint32_t *)base;
+        }
+        return;
+    }
+    // column end: element-wise into the same byte image (beyond n -> zero bytes)
+    uint32_t w[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    for (int m = 0; m < 4 && r + m < n; ++m) {
+        const unsigned char *e = (const unsigned char *)base + m * gc.width;
+        for (int b = 0; b < gc.width; ++b) w[(m * gc.width + b) >> 2] |= (uint32_t)e[b] << (8 * ((m * gc.width + b) & 3));
+    }
+    x.lo = u32x4{w[0], w[1], w[2], w[3]};
+    x.hi = u32x4{w[4], w[5], w[6], w[7]};
+}
+
+__global__ void __launch_bounds__(GW_BLOCK, 2) gram_wide_kernel(const GramCol *cols, int ncols, const double *shift,
+                                                              const uint32_t *keep, int64_t n, int side, int T,
+                                                              int S, int64_t rows_per_chunk, double *part_g,
+                                                              double *part_cs, double *part_n) {
+    __shared__ double pa[GW_TILE * GW_PITCH];
+    __shared__ double pb[GW_TILE * GW_PITCH];
+    // XCD-major logical block id: consecutive ids (same chunk, different tiles) on one XCD
+    const int G = S * T;
+    const int G8 = (G + 7) / 8;
+    const int L = (int)(blockIdx.x % 8) * G8 + (int)(blockIdx.x / 8);
+    if (L >= G) return;
+    const int s = L / T, t = L % T;
+    int ti = 0, rem = t;
+    while (rem >= side - ti) { rem -= side - ti; ++ti; }
+    const int tj = ti + rem;
+    const bool diag = ti == tj;
+    const int tid = threadIdx.x, lane = lane_id(), wid = tid / WAVE;
+    const int q = lane >> 4, cl = lane & 15;
+    const int qa = wid >> 2, qb = wid & 3;
+    // on a diagonal tile, quadrants with every column index j < every row index i are skipped
+    const bool work = !diag || (32 * qb + 31 >= 64 * qa);
+
+    // staging slots of this thread: (panel column c in [0, 256), quad in [0, 8))
+    GramCol sc[GW_SLOTS];
+    double sk[GW_SLOTS];
+    int squad[GW_SLOTS];
+    bool sact[GW_SLOTS];
+#pragma unroll
+    for (int i = 0; i < GW_SLOTS; ++i) {
+        const int p = tid + GW_BLOCK * i;
+        const int c = p >> 3;
+        squad[i] = p & 7;
+        const bool in_b = c >= GW_TILE;
+        const int gc = (in_b ? tj : ti) * GW_TILE + (c & (GW_TILE - 1));
+        sact[i] = !(diag && in_b);
+        const bool v = sact[i] && gc < ncols;
+        sc[i] = v ? cols[gc] : GramCol{nullptr, 0, 0};
+        sk[i] = v ? shift[gc] : 0.0;
+    }
+    double csum[GW_SLOTS];
+#pragma unroll
+    for (int i = 0; i < GW_SLOTS; ++i) csum[i] = 0.0;
+    double nkeep = 0.0;
+
+    d4 acc[4][2];
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+#pragma unroll
+        for (int b = 0; b < 2; ++b) acc[a][b] = d4{0.0, 0.0, 0.0, 0.0};
+
+    const int64_t c0 = (int64_t)s * rows_per_chunk;
+    const int64_t c1 = min(n, c0 + rows_per_chunk);
+    GwRaw raw[GW_SLOTS];
+    auto issue = [&](int64_t r0) {
+#pragma unroll
+        for (int i = 0; i < GW_SLOTS; ++i) {
+            raw[i].lo = u32x4{0, 0, 0, 0};
+            raw[i].hi = u32x4{0, 0, 0, 0};
+            if (sact[i]) gw_load(sc[i], r0 + 4 * squad[i], n, raw[i]);
+        }
+    };
+    if (c0 < c1) issue(c0);
+    const double *opb = diag ? pa : pb;
+    for (int64_t r0 = c0; r0 < c1; r0 += GW_KR) {
+        const uint32_t kw = keep[r0 >> 5];            // chunks start on 32-row boundaries
+        lds_barrier();                                 // the previous k-step's MFMA reads are done
+#pragma unroll
+        for (int i = 0; i < GW_SLOTS; ++i) {
+            if (!sact[i]) continue;
+            const int p = tid + GW_BLOCK * i;
+            const int c = p >> 3;
+            const uint32_t kb = (kw >> (4 * squad[i])) & 0xFu;
+            double x[4];
+            if (common_dtype(sc[i].dtype))
+                conv4_common(sc[i].width == 8, sc[i].dtype == SDP_F64 || sc[i].dtype == SDP_F32,
+                             Raw4{raw[i].lo, raw[i].hi}, x);
+            else
+                conv4(sc[i].dtype, Raw4{raw[i].lo, raw[i].hi}, x);
+            double y[4];
+#pragma unroll
+            for (int m = 0; m < 4; ++m) y[m] = ((kb >> m) & 1u) ? x[m] - sk[i] : 0.0;
+            if (diag) csum[i] += (y[0] + y[1]) + (y[2] + y[3]);
+            double *dst = (c < GW_TILE ? pa : pb) + (c & (GW_TILE - 1)) * GW_PITCH + 4 * squad[i];
+            *(d4 *)dst = d4{y[0], y[1], y[2], y[3]};
+        }
+        if (diag && ti == 0 && tid == 0) nkeep += (double)__popc(kw);
+        if (r0 + GW_KR < c1) issue(r0 + GW_KR);       // next k-step's loads fly during the MFMAs
+        lds_barrier();
+        if (work) {
+#pragma unroll
+            for (int kk = 0; kk < GW_KR / 4; ++kk) {
+                double va[4], vb[2];
+#pragma unroll
+                for (int a = 0; a < 4; ++a) va[a] = pa[(64 * qa + 16 * a + cl) * GW_PITCH + 4 * kk + q];
+#pragma unroll
+                for (int b = 0; b < 2; ++b) vb[b] = opb[(32 * qb + 16 * b + cl) * GW_PITCH + 4 * kk + q];
+#pragma unroll
+                for (int a = 0; a < 4; ++a)
+#pragma unroll
+                    for (int b = 0; b < 2; ++b)
+                        acc[a][b] = __builtin_amdgcn_mfma_f64_16x16x4f64(va[a], vb[b], acc[a][b], 0, 0, 0);
+            }
+        }
+    }
+
+    // this wave's quadrant of the chunk partial
+    double *pg = part_g + (int64_t)L * GW_TILE * GW_TILE;
+    if (work) {
+#pragma unroll
+        for (int a = 0; a < 4; ++a)
+#pragma unroll
+            for (int b = 0; b < 2; ++b)
+#pragma unroll
+                for (int rr = 0; rr < 4; ++rr) {
+                    const int i = 64 * qa + 16 * a + q + 4 * rr, j = 32 * qb + 16 * b + cl;
+                    pg[i * GW_TILE + j] = acc[a][b][rr];
+                }
+    }
+    if (diag) {
+        // column sums: the 8 quads of a column are 8 consecutive lanes
+#pragma unroll
+        for (int i = 0; i < GW_SLOTS; ++i) {
+            double v = csum[i];
+            v += __shfl_xor(v, 1, WAVE);
+            v += __shfl_xor(v, 2, WAVE);
+            v += __shfl_xor(v, 4, WAVE);
+            const int p = tid + GW_BLOCK * i;
+            const int c = p >> 3;
+            if (sact[i] && (p & 7) == 0) part_cs[((int64_t)s * side + ti) * GW_TILE + c] = v;
+        }
+        if (ti == 0 && tid == 0) part_n[s] = nkeep;
+    }
+}
+
 // Sum of the S chunk partials of every output entry.  A block owns R_EB
 // entries of one tile; each entry's S partials are split into R_P contiguous
 // parts summed by separate threads, and the parts are added in part order
@@ -357,7 +551,9 @@ __global__ void __launch_bounds__(R_EB * R_P) gram_reduce_kernel(const double *p
     const double v = sum_parts(part_g + (int64_t)t * TILE * TILE + e, (int64_t)T * TILE * TILE, S, red);
     if (p == 0) {
         const int i = ti * TILE + e / TILE, j = tj * TILE + e % TILE;
-        if (i < ncols && j < ncols) {
+        // diagonal tiles: the upper triangle (the wide kernel leaves the lower
+        // quadrants unwritten; the narrow kernels' are bitwise mirrors)
+        if (i < ncols && j < ncols && (ti != tj || i <= j)) {
             G[(int64_t)i * ncols + j] = v;
             G[(int64_t)j * ncols + i] = v;
         }
@@ -379,6 +575,23 @@ struct GramGeom {
 
 static GramGeom gram_geom(int64_t n, int ncols) {
     GramGeom g;
+    if (ncols > 64) {
+        // wide kernel: ~2048 workgroups (4 rounds of 2 per CU), chunks of whole k-steps
+        g.tile = GW_TILE;
+        g.side = (ncols + GW_TILE - 1) / GW_TILE;
+        g.T = g.side * (g.side + 1) / 2;
+        int64_t S = (2048 + g.T - 1) / g.T;
+        const int64_t max_s = (n + 4095) / 4096;
+        if (S > max_s) S = max_s;
+        if (S < 1) S = 1;
+        int64_t rpc = (n + S - 1) / S;
+        rpc = (rpc + GW_KR - 1) / GW_KR * GW_KR;
+        if (rpc < GW_KR) rpc = GW_KR;
+        g.S = (int)((n + rpc - 1) / rpc);
+        if (g.S < 1) g.S = 1;
+        g.rows_per_chunk = rpc;
+        return g;
+    }
     g.tile = ncols <= 16 ? 16 : (ncols <= 32 ? 32 : 64);
     g.side = (ncols + g.tile - 1) / g.tile;
     g.T = g.side * (g.side + 1) / 2;
@@ -477,6 +690,17 @@ extern "C" int sdp_gram(const sdp_column *cols, int32_t ncols, const uint32_t *d
     if (e == hipSuccess) e = hipStreamSynchronize(s);
     free(h);
     if (e != hipSuccess) return set_error(SDP_EHIP, "sdp_gram: %s", hipGetErrorString(e));
+    if (g.tile == GW_TILE) {
+        const int G = g.S * g.T;
+        const dim3 wgrid((unsigned)((G + 7) / 8 * 8));
+        hipLaunchKernelGGL(gram_wide_kernel, wgrid, dim3(GW_BLOCK), 0, s, d_cols, ncols, d_shift, d_keep, n, g.side,
+                           g.T, g.S, g.rows_per_chunk, pg, pcs, pn);
+        int rcw = check_launch("gram_wide_kernel");
+        if (rcw) return rcw;
+        hipLaunchKernelGGL(gram_reduce_kernel<GW_TILE>, dim3(g.T * (GW_TILE * GW_TILE / R_EB)), dim3(R_EB * R_P), 0, s,
+                           pg, pcs, pn, ncols, g.side, g.T, g.S, d_gram, d_colsum, d_n);
+        return check_launch("gram_reduce_kernel");
+    }
     const dim3 grid((unsigned)(g.S * g.T));
     switch (g.tile) {
     case 16:

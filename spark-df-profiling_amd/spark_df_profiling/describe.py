@@ -49,14 +49,30 @@ def as_device_table(df, device=None) -> DeviceTable:
     if isinstance(df, (str, os.PathLike)) and str(df).endswith('.parquet'):
         # the reference's inputs come from spark.read.parquet (examples/Demo.ipynb:63)
         return DeviceTable.from_parquet(str(df), device=device)
-    # Spark DataFrame (pyspark optional): collect as Arrow, never row by row
-    to_arrow = getattr(df, 'toArrow', None) or getattr(df, '_collect_as_arrow', None)
-    if to_arrow is not None and type(df).__module__.startswith('pyspark'):
-        got = to_arrow()
-        if isinstance(got, list):
-            got = pa.Table.from_batches(got)
-        return DeviceTable.from_arrow(got, device)
+    if type(df).__module__.startswith('pyspark'):
+        return DeviceTable.from_arrow(spark_to_arrow(df), device)
     raise TypeError('df must be of type pyspark.sql.DataFrame, pyarrow.Table, a .parquet path or DeviceTable')
+
+
+def spark_to_arrow(df):
+    """A Spark DataFrame (pyspark is optional: only its duck type is used)
+    collected to the driver as Arrow, never row by row -- the counterpart of
+    the reference's per-statistic Spark jobs (describe.py:71-283) is one
+    columnar collect followed by HBM-resident passes:
+      Spark >= 4.0   df.toArrow()                       -> pyarrow.Table
+      Spark 2.3-3.x  df._collect_as_arrow()             -> [RecordBatch]
+      otherwise      df.toPandas() (Arrow-accelerated when
+                     spark.sql.execution.arrow.enabled) -> pyarrow.Table"""
+    to_arrow = getattr(df, 'toArrow', None) or getattr(df, '_collect_as_arrow', None)
+    if to_arrow is not None:
+        got = to_arrow()
+        if isinstance(got, (list, tuple)):
+            got = pa.Table.from_batches(list(got)) if got else pa.table({})
+        return got
+    to_pandas = getattr(df, 'toPandas', None)
+    if to_pandas is None:
+        raise TypeError('Spark DataFrame without toArrow/_collect_as_arrow/toPandas')
+    return pa.Table.from_pandas(to_pandas(), preserve_index=False)
 
 
 def _series(values, col: DeviceColumn) -> pd.Series:

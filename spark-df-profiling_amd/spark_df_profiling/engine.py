@@ -44,6 +44,16 @@ U64 = (1 << 64) - 1
 PART_SAMPLE = 16384          # rows sampled for heavy keys (sdp_part_sample)
 HEAVY_MIN = 3                # sample occurrences that make a key heavy
 PART_CHUNK = 65536           # level-2 records per workgroup chunk
+CAND_FULL_BUDGET = 1 << 30   # bytes of room-for-every-row candidate slots per pass-1 batch
+
+# Test knob for the quantile edge paths (never set in production):
+#   'overflow' -- one candidate slot per wave segment, so every window that
+#                 receives candidates overflows (w_overflow) and its ranks take
+#                 the exact whole-column select;
+#   'miss'     -- every planned window is narrowed to its lower bound, so ranks
+#                 outside the bound's ties miss the windows and fall back.
+import os as _os
+DEBUG_QUANTILE = _os.environ.get('SDP_DEBUG_QUANTILE', '')
 
 
 def _u(x):
@@ -221,11 +231,19 @@ class Engine:
         p.shift = 0.0
         return self._to_dev(p), p
 
-    def _pass1_launch(self, col: DeviceColumn, plan_dev, plan, res_dev=None):
+    def _pass1_launch(self, col: DeviceColumn, plan_dev, plan, res_dev=None, budget=None):
+        """Launch pass 1 of one column.  `budget` (a one-element list of bytes
+        left) is shared by the columns of one batch: every column's candidate
+        slots stay alive until its quantiles are resolved, so the room-for-
+        every-row sizing below is granted only while the batch's total stays
+        under CAND_FULL_BUDGET; past it (wide tables: 512 columns x 1e7 rows
+        would need ~350 GB) slots are sized from the sample estimate, whose
+        rare overflow falls back to the exact whole-column select."""
         n = col.length
         grid = sdp.sdp_pass1_grid(n, col.dtype)
         work = self._bytes(sdp.sdp_pass1_workspace_bytes(n, col.dtype))
         nw = plan.n_windows
+        nseg = grid * nat.PASS1_WAVES                    # wave-private candidate segments per window
         cap = 0
         if nw:
             rows_pb = n / max(grid, 1)
@@ -235,12 +253,20 @@ class Engine:
                 cap = max(cap, int(2.0 * exp + 6.0 * math.sqrt(exp) + 64))
             # a block's rows come from whole grid-strided tiles; at small n a window
             # can sit inside one tile (sorted data), so give every block room for
-            # all its rows (<= 2^24 rows: at most 5 x 128 MiB of slots)
+            # all its rows when the batch can afford it
             tile_rows = 256 * 4 * (16 // nat.ELEM_SIZE[col.dtype])
             full = int(math.ceil(n / max(grid, 1) / tile_rows + 1)) * tile_rows
-            cap = full if n <= (1 << 24) else min(cap, full)
-        nseg = grid * nat.PASS1_WAVES                    # wave-private candidate segments per window
+            full_bytes = nw * nseg * (-(-full // nat.PASS1_WAVES) + 64) * 8
+            if budget is None:
+                budget = [CAND_FULL_BUDGET]
+            if n <= (1 << 24) and full_bytes <= budget[0]:
+                cap = full
+                budget[0] -= full_bytes
+            else:
+                cap = min(cap, full)
         cap = -(-cap // nat.PASS1_WAVES) + 64 if cap else 0
+        if nw and DEBUG_QUANTILE == 'overflow':
+            cap = 1                                       # every busy segment overflows
         cand = self._u64(max(nw, 1) * nseg * max(cap, 1))
         cand_counts = torch.zeros(max(nw, 1) * nseg, dtype=torch.int32, device=self.device)
         if res_dev is None:
@@ -546,11 +572,17 @@ class Engine:
         else:
             raw = plans_dev.cpu().numpy()
         plans = [nat.SdpQPlan.from_buffer_copy(raw[i * psz:(i + 1) * psz].tobytes()) for i in range(len(cols))]
+        if DEBUG_QUANTILE == 'miss':
+            for i, p in enumerate(plans):
+                for w in range(p.n_windows):
+                    p.hi[w] = p.lo[w]
+                plans_dev[i * psz:(i + 1) * psz] = self._to_dev(p)
         rsz = ctypes.sizeof(nat.SdpPass1Result)
         res_all = self._bytes(len(cols) * rsz)
         infos = []
+        budget = [CAND_FULL_BUDGET]
         for i, col in enumerate(cols):
-            infos.append(self._pass1_launch(col, plans_dev[i * psz:], plans[i], res_all[i * rsz:]))
+            infos.append(self._pass1_launch(col, plans_dev[i * psz:], plans[i], res_all[i * rsz:], budget))
         if hcols:
             if self._heavy_pre is None:
                 self._heavy_pre = {}

@@ -124,6 +124,7 @@ def render_one(kind, counts, edges, width):
 # ----------------------------------------------------------------------------
 
 _POOL = None
+_POOL_LOCK = threading.Lock()      # column worker threads may submit concurrently
 
 
 def _warm():
@@ -135,6 +136,11 @@ def start_pool(workers=None):
     """Start (once) the spawn-context worker pool and wait until every worker
     has imported matplotlib.  Call early (before heavy GPU allocation) to keep
     the one-time start-up out of the first describe()."""
+    with _POOL_LOCK:
+        return _start_pool_locked(workers)
+
+
+def _start_pool_locked(workers):
     global _POOL
     if _POOL is not None:
         return _POOL
@@ -166,9 +172,10 @@ def start_pool(workers=None):
 
 def shutdown_pool():
     global _POOL
-    if _POOL is not None:
-        _POOL.shutdown(wait=True, cancel_futures=True)
-        _POOL = None
+    with _POOL_LOCK:
+        if _POOL is not None:
+            _POOL.shutdown(wait=True, cancel_futures=True)
+            _POOL = None
 
 
 class _PairFuture:

@@ -13,6 +13,8 @@ overview (dataset info, type counts, warnings) and the sample table.
 
 from __future__ import annotations
 
+import os
+
 import html as _html
 
 import pandas as pd
@@ -258,9 +260,9 @@ def _sample_frame(df, n):
         return pa.Table.from_batches([df]).slice(0, n).to_pandas()
     if isinstance(df, DeviceTable):
         return pd.DataFrame({c.name: [] for c in df.columns})
-    if isinstance(df, str) and df.endswith('.parquet'):
+    if isinstance(df, (str, os.PathLike)) and str(df).endswith('.parquet'):
         import pyarrow.parquet as pq
-        pf = pq.ParquetFile(df)
+        pf = pq.ParquetFile(str(df))
         return pa.Table.from_batches([next(pf.iter_batches(batch_size=max(n, 1)))]).slice(0, n).to_pandas() \
             if pf.metadata.num_rows else pd.DataFrame()
     limit = getattr(df, 'limit', None)

@@ -150,3 +150,85 @@ def demo_like_table(n, seed=20261015):
         'source': pa.array(['NASA'] * n),
         'year': pa.array(days.astype(np.int32), type=pa.date32(), mask=_mask(g, n, 0.007)),
     })
+
+
+# ----------------------------------------------------------------------------
+# BASELINE.json configurations, numpy PCG64 from fixed seeds.
+# C1 is demo_like_table above; C3 is generated in HBM by bench.make_c3_shard.
+# ----------------------------------------------------------------------------
+
+C_SEED = 20261015
+
+
+def c2_table(n, seed=C_SEED):
+    """C2: n x 8 fp64, no nulls -- N(0,1), N(1e9,1) (cancellation stress),
+    lognormal(0,1), U(-1e6,1e6), exp(1), Student-t(3), 1 % exact zeros + N(0,1),
+    bimodal."""
+    g = rng(seed)
+    z = g.standard_normal(n)
+    z[g.random(n) < 0.01] = 0.0
+    bi = np.where(g.random(n) < 0.3, g.normal(-5.0, 1.0, n), g.normal(4.0, 0.5, n))
+    cols = {
+        'norm': g.standard_normal(n),
+        'shifted_1e9': 1e9 + g.standard_normal(n),
+        'lognormal': g.lognormal(0.0, 1.0, n),
+        'uniform_1e6': g.uniform(-1e6, 1e6, n),
+        'exp': g.exponential(1.0, n),
+        'student_t3': g.standard_t(3, n),
+        'zeros_1pct': z,
+        'bimodal': bi,
+    }
+    return pa.table({k: pa.array(v) for k, v in cols.items()})
+
+
+def bounded_zipf(g, n, s, card):
+    """Continuous power-law inverse CDF on [1, card+1) -> labels 0..card-1
+    (the same law bench.py draws its zipf columns from)."""
+    u = g.random(n)
+    a = 1.0 - s
+    x = np.power(1.0 - u * (1.0 - (card + 1.0) ** a), 1.0 / a)
+    return np.clip(np.floor(x).astype(np.int64) - 1, 0, card - 1)
+
+
+def mix64_np(x):
+    x = np.asarray(x, dtype=np.uint64).copy()
+    with np.errstate(over='ignore'):
+        x ^= x >> np.uint64(30)
+        x *= np.uint64(0xBF58476D1CE4E5B9)
+        x ^= x >> np.uint64(27)
+        x *= np.uint64(0x94D049BB133111EB)
+        x ^= x >> np.uint64(31)
+    return x
+
+
+def hex16_strings(keys):
+    """utf8 array of the 16 lower-case hex digits of each u64 key."""
+    keys = np.asarray(keys, dtype=np.uint64)
+    n = keys.size
+    shifts = np.arange(60, -4, -4, dtype=np.uint64)
+    nib = ((keys[:, None] >> shifts[None, :]) & np.uint64(15)).astype(np.uint8)
+    data = np.frombuffer(b'0123456789abcdef', dtype=np.uint8)[nib].reshape(-1)
+    offsets = (np.arange(n + 1, dtype=np.int32) * 16)
+    return pa.StringArray.from_buffers(n, pa.py_buffer(offsets.tobytes()), pa.py_buffer(data.tobytes()))
+
+
+def c4_table(n, seed=C_SEED + 4, labels=5 * 10 ** 8):
+    """C4: int64 U[0, 2^32) (near-unique) and utf8 16-byte hex ids drawn
+    zipf(1.05) over `labels` labels (exact distinct + top-50), plus the NUM
+    column the reference needs for table stats (describe.py:108)."""
+    g = rng(seed)
+    ints = g.integers(0, 2 ** 32, n, dtype=np.int64)
+    lab = bounded_zipf(g, n, 1.05, labels)
+    return pa.table({'u32_range_i64': pa.array(ints), 'hex_id': hex16_strings(mix64_np(lab))})
+
+
+def c5_table(n, ncols=512, seed=C_SEED + 5, factors=4):
+    """C5: n x ncols fp32, no nulls: x_j = F a_j + e_j, F ~ N(0,1) (n x 4),
+    loadings a_j ~ U(-1.5, 1.5)^4, so the Pearson matrix spans (-1, 1)."""
+    g = rng(seed)
+    F = g.standard_normal((n, factors))
+    L = g.uniform(-1.5, 1.5, (factors, ncols))
+    cols = {}
+    for j in range(ncols):
+        cols['c%03d' % j] = pa.array((F @ L[:, j] + g.standard_normal(n)).astype(np.float32))
+    return pa.table(cols)

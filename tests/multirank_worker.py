@@ -2,14 +2,16 @@
 
 Run with one GPU per rank over RCCL, or several ranks sharing one GPU over gloo:
     python -m torch.distributed.run --nproc-per-node 2 --master-addr 127.0.0.1 \\
-        --master-port 29511 tools/multirank_check.py [nccl|gloo]
+        --master-port 29511 tests/multirank_worker.py [nccl|gloo] [table,...]
+tests/test_gpu_multirank.py runs it (2 gloo ranks on the one GPU of the box),
+started by conftest.py before the test process initialises the GPU.
 """
 import os
 import sys
 
 os.environ.setdefault('SDP_PLOT_WORKERS', '0')      # render inline (no pool in this check)
 
-ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))  # repo root
 for p in (ROOT, os.path.join(ROOT, 'spark-df-profiling_amd'), os.path.join(ROOT, 'tests')):
     sys.path.insert(0, p)
 
@@ -48,8 +50,11 @@ def main():
         'corr': datagen.corr_table(20_000),
         'legacy': datagen.legacy_table(),
     }
+    only = sys.argv[2].split(',') if len(sys.argv) > 2 else None
     failures = 0
     for name, t in tables.items():
+        if only and name not in only:
+            continue
         full = DeviceTable.from_arrow(t, dev)
         n = t.num_rows
         per = (n // world) // 16 * 16
@@ -78,6 +83,8 @@ def main():
                 print('[%s] MISMATCH world=%d\n%s' % (name, world, e), flush=True)
     dist.barrier()
     dist.destroy_process_group()
+    if rank == 0:
+        print('MULTIRANK %s failures=%d' % ('OK' if not failures else 'FAILED', failures), flush=True)
     if failures:
         sys.exit(1)
 

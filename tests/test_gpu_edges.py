@@ -1,0 +1,111 @@
+"""Edge paths of the GPU engine that the ordinary tables never reach:
+
+* the quantile window-miss and candidate-slot-overflow fallbacks
+  (engine._quantiles_launch -> exact whole-column select), forced by the
+  SDP_DEBUG_QUANTILE knob, against the oracle;
+* determinism: two describe() runs of one table are bitwise
+  equal in every output;
+* a duck-typed Spark DataFrame (toArrow / limit().toPandas()) through
+  describe() and ProfileReport (reference __init__.py:61-68).
+Needs an MI355X.
+"""
+
+import math
+
+import numpy as np
+import pandas as pd
+import pyarrow as pa
+import pytest
+
+import datagen
+from compare import assert_describe_equal
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize('mode', ['overflow', 'miss'])
+def test_quantile_fallback(monkeypatch, mode):
+    import oracle
+    from spark_df_profiling import describe, engine
+    monkeypatch.setattr(engine, 'DEBUG_QUANTILE', mode)
+    t = datagen.numeric_table(200_003, seed=17)
+    raw = {}
+    got = describe(t, raw=raw, plots=False)
+    want = oracle.describe(t)
+    assert_describe_equal(got, want)
+    used = [name for name, b in raw['columns'].items() if 'numeric' in b and b['numeric'].fallback_used]
+    assert used, 'the knob must route quantiles through the fallback'
+
+
+def _bitwise_equal(a, b):
+    if isinstance(a, pd.Series) or isinstance(b, pd.Series):
+        return (isinstance(a, pd.Series) and isinstance(b, pd.Series) and list(a.index) == list(b.index)
+                and all(_bitwise_equal(x, y) for x, y in zip(a.tolist(), b.tolist())))
+    if isinstance(a, (float, np.floating)) and isinstance(b, (float, np.floating)):
+        return np.float64(a).tobytes() == np.float64(b).tobytes() or (math.isnan(a) and math.isnan(b))
+    return type(a) == type(b) and a == b
+
+
+def test_determinism_bitwise():
+    from spark_df_profiling import describe
+    for t in (datagen.numeric_table(300_007, seed=23), datagen.categorical_table(120_000, seed=29),
+              datagen.corr_table(100_000, seed=31)):
+        r1, r2 = {}, {}
+        a = describe(t, plots=False, raw=r1)
+        b = describe(t, plots=False, raw=r2)
+        assert a['table'] == b['table'] or all(_bitwise_equal(a['table'][k], b['table'][k]) for k in a['table'])
+        va, vb = a['variables'], b['variables']
+        assert list(va.index) == list(vb.index) and list(va.columns) == list(vb.columns)
+        for name in va.index:
+            for k in va.columns:
+                assert _bitwise_equal(va.loc[name, k], vb.loc[name, k]), (name, k, va.loc[name, k], vb.loc[name, k])
+        for k in a['freq']:
+            assert _bitwise_equal(a['freq'][k], b['freq'][k]), k
+        if r1['corr'] is not None:
+            assert r1['corr'].to_numpy().tobytes() == r2['corr'].to_numpy().tobytes()
+
+
+class _FakeSparkFrame:
+    """The part of pyspark.sql.DataFrame the boundary touches: toArrow()
+    (Spark >= 4; _collect_as_arrow() on 3.x) and limit(n).toPandas()."""
+
+    def __init__(self, table):
+        self._t = table
+
+    def toArrow(self):
+        return self._t
+
+    def limit(self, n):
+        return _FakeSparkFrame(self._t.slice(0, n))
+
+    def toPandas(self):
+        return self._t.to_pandas()
+
+
+_FakeSparkFrame.__module__ = 'pyspark.sql.dataframe'
+
+
+class _FakeSparkFrame3(_FakeSparkFrame):
+    toArrow = None
+
+    def _collect_as_arrow(self):
+        return self._t.to_batches(max_chunksize=4096)
+
+
+_FakeSparkFrame3.__module__ = 'pyspark.sql.dataframe'
+
+
+def test_spark_like_input(tmp_path):
+    import oracle
+    from spark_df_profiling import ProfileReport, describe
+    t = datagen.demo_like_table(20_000)
+    want = oracle.describe(t)
+    assert_describe_equal(describe(_FakeSparkFrame(t), plots=False), want)
+    assert_describe_equal(describe(_FakeSparkFrame3(t), plots=False), want)
+    rep = ProfileReport(_FakeSparkFrame(t))
+    out = tmp_path / 'spark_like.html'
+    rep.to_file(str(out))
+    html = out.read_text(encoding='utf8')
+    assert 'data:image/png' in html and 'reclat_city' in html
+    with pytest.raises(TypeError):
+        describe(object())

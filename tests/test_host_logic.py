@@ -117,3 +117,29 @@ def test_corr_from_gram():
     rho = corr_from_gram(Xc.T @ Xc, Xc.sum(0), len(X))
     assert np.allclose(rho, np.corrcoef(X.T), rtol=1e-12, atol=1e-12)
     assert np.isnan(corr_from_gram(np.zeros((2, 2)), np.zeros(2), 0)).all()
+
+
+def test_spark_to_arrow_duck_types():
+    """describe.spark_to_arrow on Spark-like objects of each collect style
+    (no GPU: the Arrow table is returned before any upload)."""
+    import pyarrow as pa
+    from spark_df_profiling.describe import spark_to_arrow
+    t = pa.table({'a': pa.array([1, 2, None]), 's': pa.array(['x', None, 'z'])})
+
+    class S4:
+        def toArrow(self):
+            return t
+
+    class S3:
+        def _collect_as_arrow(self):
+            return t.to_batches(max_chunksize=2)
+
+    class S2:
+        def toPandas(self):
+            return t.to_pandas()
+
+    assert spark_to_arrow(S4()).equals(t)
+    assert spark_to_arrow(S3()).equals(t)
+    got = spark_to_arrow(S2())
+    assert got.column('s').to_pylist() == ['x', None, 'z']
+    assert got.column('a').to_pylist()[:2] == [1.0, 2.0]

@@ -6,7 +6,7 @@ cd "$GRAFT_REPO_ROOT"; mkdir -p gpurun_out
 export TMPDIR=/tmp
 for w in 2 3; do
   timeout -k 10 400 python -u -m torch.distributed.run --nproc-per-node $w --master-addr 127.0.0.1 --master-port 2951$w \
-     tools/multirank_check.py gloo > gpurun_out/mr_$w.log 2>&1 || { echo "world $w failed"; tail -30 gpurun_out/mr_$w.log; exit 1; }
+     tests/multirank_worker.py gloo > gpurun_out/mr_$w.log 2>&1 || { echo "world $w failed"; tail -30 gpurun_out/mr_$w.log; exit 1; }
   grep -E "OK|MISMATCH|missing" gpurun_out/mr_$w.log
 done
 [ "${TESTS:-1}" = 1 ] || exit 0
