@@ -32,10 +32,23 @@ def start_pool(workers):
     global _POOL, _POOL_N
     if _POOL is None and workers > 1:
         import multiprocessing as mp
+        import sys
         from concurrent.futures import ProcessPoolExecutor
         _POOL = ProcessPoolExecutor(max_workers=workers, mp_context=mp.get_context('spawn'))
         _POOL_N = workers
-        list(_POOL.map(_warm, range(workers)))
+        # spawn re-imports the parent's __main__ in every child unless it cannot
+        # find it; hide it while the workers start (they need only this package)
+        main = sys.modules.get('__main__')
+        saved = {a: getattr(main, a) for a in ('__file__', '__spec__') if main is not None and hasattr(main, a)}
+        try:
+            if '__file__' in saved:
+                del main.__file__
+            if '__spec__' in saved:
+                main.__spec__ = None
+            list(_POOL.map(_warm, range(2 * workers)))
+        finally:
+            for a, v in saved.items():
+                setattr(main, a, v)
     return _POOL
 
 

@@ -330,10 +330,12 @@ __global__ void __launch_bounds__(G_BLOCK) gram_kernel(const GramCol *cols, int 
 // instead of once per wave; every wave then runs its MFMAs from LDS.  Wave w
 // owns the 64 x 32 quadrant (qa = w >> 2, qb = w & 3) of the tile: 8
 // accumulators, no cross-wave reduction (each wave writes its quadrant of the
-// chunk partial).  On a diagonal tile the two quadrants wholly below the
-// diagonal are skipped (the reduce mirrors the upper triangle).  The next
+// chunk partial).  On a diagonal tile the waves share out the 36 upper-
+// triangle 16x16 blocks instead (GW_DIAG_BLK; the reduce mirrors them).  The next
 // k-step's raw loads are issued before the MFMA phase, so HBM latency hides
-// behind the matrix work.  Blocks are mapped XCD-major: the tiles of one row
+// behind the matrix work (v2: double-buffered panels, each slot's
+// convert/store and its next load interleaved between MFMA groups, one
+// barrier per k-step).  Blocks are mapped XCD-major: the tiles of one row
 // chunk run on one XCD and share its L2 for the column reads.
 //
 // LDS panel layout [col][row] with a pitch of 34 doubles (68 dwords = 4 mod 64
@@ -349,6 +351,14 @@ constexpr int GW_SLOTS = 2 * GW_TILE * (GW_KR / 4) / GW_BLOCK;   // (col, 4-row 
 struct GwRaw {
     u32x4 lo, hi;
 };
+
+// Diagonal tiles: the 36 16x16 blocks (bi <= bj) of the upper triangle dealt
+// round-robin to the 8 waves (5 or 4 each), so no SIMD carries more than ~10
+// blocks per k-step against 16 on an off-diagonal tile.  Entry = bi * 8 + bj.
+__constant__ uint8_t GW_DIAG_BLK[GW_WAVES][5] = {
+    {0, 9, 19, 30, 47}, {1, 10, 20, 31, 54}, {2, 11, 21, 36, 55}, {3, 12, 22, 37, 63},
+    {4, 13, 23, 38, 0}, {5, 14, 27, 39, 0}, {6, 15, 28, 45, 0}, {7, 18, 29, 46, 0}};
+__constant__ uint8_t GW_DIAG_N[GW_WAVES] = {5, 5, 5, 5, 4, 4, 4, 4};
 
 __device__ __forceinline__ void gw_load(const GramCol &gc, int64_t r, int64_t n, GwRaw &x) {
     if (gc.dtype == 0) return;
@@ -381,114 +391,181 @@ __device__ __forceinline__ void gw_load(const GramCol &gc, int64_t r, int64_t n,
     x.hi = u32x4{w[4], w[5], w[6], w[7]};
 }
 
-__global__ void __launch_bounds__(GW_BLOCK, 2) gram_wide_kernel(const GramCol *cols, int ncols, const double *shift,
-                                                              const uint32_t *keep, int64_t n, int side, int T,
-                                                              int S, int64_t rows_per_chunk, double *part_g,
-                                                              double *part_cs, double *part_n) {
-    __shared__ double pa[GW_TILE * GW_PITCH];
-    __shared__ double pb[GW_TILE * GW_PITCH];
-    // XCD-major logical block id: consecutive ids (same chunk, different tiles) on one XCD
-    const int G = S * T;
-    const int G8 = (G + 7) / 8;
-    const int L = (int)(blockIdx.x % 8) * G8 + (int)(blockIdx.x / 8);
-    if (L >= G) return;
+// KIND: GW_GENERIC (any dtype mix, element-wise tail), GW_F32 / GW_F64 (every
+// column of the tile has that dtype and the chunk holds no ragged tail: the
+// staging is branch-free -- row addresses are clamped into the column and the
+// rows past n are zeroed by their keep bits, absent columns read column 0 and
+// are zeroed by their slot mask -- so the k-loop stays one basic block and the
+// compiler can hoist the next group's LDS operand reads over the MFMAs).
+constexpr int GW_GENERIC = 0, GW_F32 = 1, GW_F64 = 2;
+
+template <bool DIAG, int KIND>
+__device__ __forceinline__ void gram_wide_unit(int L, const GramCol *cols, int ncols, const double *shift,
+                                               const uint32_t *keep, int64_t n, int side, int T,
+                                               int64_t rows_per_chunk, double *part_g, double *part_cs,
+                                               double *part_n, double (*pa)[GW_TILE * GW_PITCH],
+                                               double (*pb)[GW_TILE * GW_PITCH]) {
     const int s = L / T, t = L % T;
     int ti = 0, rem = t;
     while (rem >= side - ti) { rem -= side - ti; ++ti; }
     const int tj = ti + rem;
-    const bool diag = ti == tj;
-    const int tid = threadIdx.x, lane = lane_id(), wid = tid / WAVE;
+    constexpr bool diag = DIAG;
+    const int tid = threadIdx.x, lane = lane_id();
+    const int wid = __builtin_amdgcn_readfirstlane(tid / WAVE);
     const int q = lane >> 4, cl = lane & 15;
     const int qa = wid >> 2, qb = wid & 3;
-    // on a diagonal tile, quadrants with every column index j < every row index i are skipped
-    const bool work = !diag || (32 * qb + 31 >= 64 * qa);
+    constexpr int NSLOT = DIAG ? GW_SLOTS / 2 : GW_SLOTS;    // diagonal tiles stage panel A only
+    const int squad = tid & 7;                         // the same quad in every slot
 
-    // staging slots of this thread: (panel column c in [0, 256), quad in [0, 8))
-    GramCol sc[GW_SLOTS];
-    double sk[GW_SLOTS];
-    int squad[GW_SLOTS];
-    bool sact[GW_SLOTS];
+    GramCol sc[NSLOT];
+    double sk[NSLOT];
+    uint32_t smask[NSLOT];                             // 0xF for a real column, 0 for padding
 #pragma unroll
-    for (int i = 0; i < GW_SLOTS; ++i) {
-        const int p = tid + GW_BLOCK * i;
-        const int c = p >> 3;
-        squad[i] = p & 7;
-        const bool in_b = c >= GW_TILE;
-        const int gc = (in_b ? tj : ti) * GW_TILE + (c & (GW_TILE - 1));
-        sact[i] = !(diag && in_b);
-        const bool v = sact[i] && gc < ncols;
-        sc[i] = v ? cols[gc] : GramCol{nullptr, 0, 0};
+    for (int i = 0; i < NSLOT; ++i) {
+        const int c = (tid + GW_BLOCK * i) >> 3;
+        const int gc = (c >= GW_TILE ? tj : ti) * GW_TILE + (c & (GW_TILE - 1));
+        const bool v = gc < ncols;
+        sc[i] = v ? cols[gc] : (KIND == GW_GENERIC ? GramCol{nullptr, 0, 0} : cols[0]);
         sk[i] = v ? shift[gc] : 0.0;
+        smask[i] = v ? 0xFu : 0u;
     }
-    double csum[GW_SLOTS];
+    double csum[NSLOT];
 #pragma unroll
-    for (int i = 0; i < GW_SLOTS; ++i) csum[i] = 0.0;
+    for (int i = 0; i < NSLOT; ++i) csum[i] = 0.0;
     double nkeep = 0.0;
 
-    d4 acc[4][2];
+    // off-diagonal: acc[2a + b] is block (a, b) of the 64 x 32 quadrant;
+    // diagonal: acc[j] is block GW_DIAG_BLK[wid][j] of the tile
+    constexpr int NACC = DIAG ? 5 : 8;
+    d4 acc[NACC];
 #pragma unroll
-    for (int a = 0; a < 4; ++a)
+    for (int a = 0; a < NACC; ++a) acc[a] = d4{0.0, 0.0, 0.0, 0.0};
+    const int dn = diag ? (int)GW_DIAG_N[wid] : 0;
+    int dbi[5], dbj[5];
 #pragma unroll
-        for (int b = 0; b < 2; ++b) acc[a][b] = d4{0.0, 0.0, 0.0, 0.0};
+    for (int j = 0; j < 5; ++j) {
+        const int blk = diag ? (int)GW_DIAG_BLK[wid][j] : 0;
+        dbi[j] = blk >> 3;
+        dbj[j] = blk & 7;
+    }
 
     const int64_t c0 = (int64_t)s * rows_per_chunk;
     const int64_t c1 = min(n, c0 + rows_per_chunk);
-    GwRaw raw[GW_SLOTS];
-    auto issue = [&](int64_t r0) {
-#pragma unroll
-        for (int i = 0; i < GW_SLOTS; ++i) {
+    const int64_t rlast = (n & ~(int64_t)3) - 4;       // last whole 4-row group (fast kinds: n >= 4)
+    GwRaw raw[NSLOT];
+    auto load_slot = [&](int i, int64_t r0) {
+        const int64_t r = r0 + 4 * squad;
+        if (KIND == GW_F32) {
+            const int64_t rc = r < rlast ? r : rlast;
+            raw[i].lo = *(const __attribute__((address_space(1))) u32x4 *)((const char *)sc[i].p + rc * 4);
+        } else if (KIND == GW_F64) {
+            const int64_t rc = r < rlast ? r : rlast;
+            const __attribute__((address_space(1))) u32x4 *b =
+                (const __attribute__((address_space(1))) u32x4 *)((const char *)sc[i].p + rc * 8);
+            raw[i].lo = b[0];
+            raw[i].hi = b[1];
+        } else {
             raw[i].lo = u32x4{0, 0, 0, 0};
             raw[i].hi = u32x4{0, 0, 0, 0};
-            if (sact[i]) gw_load(sc[i], r0 + 4 * squad[i], n, raw[i]);
+            gw_load(sc[i], r, n, raw[i]);
         }
     };
-    if (c0 < c1) issue(c0);
-    const double *opb = diag ? pa : pb;
-    for (int64_t r0 = c0; r0 < c1; r0 += GW_KR) {
-        const uint32_t kw = keep[r0 >> 5];            // chunks start on 32-row boundaries
-        lds_barrier();                                 // the previous k-step's MFMA reads are done
+    // converts slot i (rows of the k-step whose keep word is kw) into buffer `buf`
+    auto stage_slot = [&](int i, uint32_t kw, int buf) {
+        const int c = (tid + GW_BLOCK * i) >> 3;
+        const uint32_t kb = (kw >> (4 * squad)) & smask[i];
+        double x[4];
+        if (KIND == GW_F32) {
 #pragma unroll
-        for (int i = 0; i < GW_SLOTS; ++i) {
-            if (!sact[i]) continue;
-            const int p = tid + GW_BLOCK * i;
-            const int c = p >> 3;
-            const uint32_t kb = (kw >> (4 * squad[i])) & 0xFu;
-            double x[4];
-            if (common_dtype(sc[i].dtype))
-                conv4_common(sc[i].width == 8, sc[i].dtype == SDP_F64 || sc[i].dtype == SDP_F32,
-                             Raw4{raw[i].lo, raw[i].hi}, x);
-            else
-                conv4(sc[i].dtype, Raw4{raw[i].lo, raw[i].hi}, x);
-            double y[4];
-#pragma unroll
-            for (int m = 0; m < 4; ++m) y[m] = ((kb >> m) & 1u) ? x[m] - sk[i] : 0.0;
-            if (diag) csum[i] += (y[0] + y[1]) + (y[2] + y[3]);
-            double *dst = (c < GW_TILE ? pa : pb) + (c & (GW_TILE - 1)) * GW_PITCH + 4 * squad[i];
-            *(d4 *)dst = d4{y[0], y[1], y[2], y[3]};
+            for (int m = 0; m < 4; ++m) x[m] = (double)__uint_as_float(raw[i].lo[m]);
+        } else if (KIND == GW_F64) {
+            x[0] = __longlong_as_double((long long)(((uint64_t)raw[i].lo[1] << 32) | raw[i].lo[0]));
+            x[1] = __longlong_as_double((long long)(((uint64_t)raw[i].lo[3] << 32) | raw[i].lo[2]));
+            x[2] = __longlong_as_double((long long)(((uint64_t)raw[i].hi[1] << 32) | raw[i].hi[0]));
+            x[3] = __longlong_as_double((long long)(((uint64_t)raw[i].hi[3] << 32) | raw[i].hi[2]));
+        } else if (common_dtype(sc[i].dtype)) {
+            conv4_common(sc[i].width == 8, sc[i].dtype == SDP_F64 || sc[i].dtype == SDP_F32,
+                         Raw4{raw[i].lo, raw[i].hi}, x);
+        } else {
+            conv4(sc[i].dtype, Raw4{raw[i].lo, raw[i].hi}, x);
         }
-        if (diag && ti == 0 && tid == 0) nkeep += (double)__popc(kw);
-        if (r0 + GW_KR < c1) issue(r0 + GW_KR);       // next k-step's loads fly during the MFMAs
+        double y[4];
+#pragma unroll
+        for (int m = 0; m < 4; ++m) y[m] = ((kb >> m) & 1u) ? x[m] - sk[i] : 0.0;
+        if (diag) csum[i] += (y[0] + y[1]) + (y[2] + y[3]);
+        double *dst = (c < GW_TILE ? pa[buf] : pb[buf]) + (c & (GW_TILE - 1)) * GW_PITCH + 4 * squad;
+        *(d4 *)dst = d4{y[0], y[1], y[2], y[3]};
+    };
+    // MFMA operands of 4-row group kk out of buffer `buf`
+    auto read_ops = [&](int buf, int kk, double (&va)[4], double (&vb)[4]) {
+        const double *A = pa[buf];
+        const double *B = diag ? pa[buf] : pb[buf];
+        if (!diag) {
+#pragma unroll
+            for (int a = 0; a < 4; ++a) va[a] = A[(64 * qa + 16 * a + cl) * GW_PITCH + 4 * kk + q];
+#pragma unroll
+            for (int b = 0; b < 2; ++b) vb[b] = B[(32 * qb + 16 * b + cl) * GW_PITCH + 4 * kk + q];
+        }
+    };
+
+    if (c0 < c1) {
+        // prologue: k-step 0 staged, k-step 1 in flight
+        const uint32_t kw0 = keep[c0 >> 5];
+#pragma unroll
+        for (int i = 0; i < NSLOT; ++i) load_slot(i, c0);
+#pragma unroll
+        for (int i = 0; i < NSLOT; ++i) {
+            stage_slot(i, kw0, 0);
+            if (c0 + GW_KR < c1) load_slot(i, c0 + GW_KR);
+        }
+        if (diag && ti == 0 && tid == 0) nkeep += (double)__popc(kw0);
         lds_barrier();
-        if (work) {
+    }
+    int cur = 0;
+    for (int64_t r0 = c0; r0 < c1; r0 += GW_KR) {
+        const bool has1 = r0 + GW_KR < c1, has2 = r0 + 2 * GW_KR < c1;
+        const uint32_t kw1 = has1 ? keep[(r0 + GW_KR) >> 5] : 0u;
+        double va[2][4], vb[2][4];
+        read_ops(cur, 0, va[0], vb[0]);
 #pragma unroll
-            for (int kk = 0; kk < GW_KR / 4; ++kk) {
-                double va[4], vb[2];
-#pragma unroll
-                for (int a = 0; a < 4; ++a) va[a] = pa[(64 * qa + 16 * a + cl) * GW_PITCH + 4 * kk + q];
-#pragma unroll
-                for (int b = 0; b < 2; ++b) vb[b] = opb[(32 * qb + 16 * b + cl) * GW_PITCH + 4 * kk + q];
+        for (int kk = 0; kk < GW_KR / 4; ++kk) {
+            if (kk + 1 < GW_KR / 4) read_ops(cur, kk + 1, va[(kk + 1) & 1], vb[(kk + 1) & 1]);
+            if (!diag) {
 #pragma unroll
                 for (int a = 0; a < 4; ++a)
 #pragma unroll
                     for (int b = 0; b < 2; ++b)
-                        acc[a][b] = __builtin_amdgcn_mfma_f64_16x16x4f64(va[a], vb[b], acc[a][b], 0, 0, 0);
+                        acc[2 * a + b] = __builtin_amdgcn_mfma_f64_16x16x4f64(va[kk & 1][a], vb[kk & 1][b],
+                                                                              acc[2 * a + b], 0, 0, 0);
+            } else {
+                const double *A = pa[cur];
+#pragma unroll
+                for (int j = 0; j < NACC; ++j) {
+                    if (j < dn) {                      // wave-uniform
+                        const double x = A[(16 * dbi[j] + cl) * GW_PITCH + 4 * kk + q];
+                        const double y = A[(16 * dbj[j] + cl) * GW_PITCH + 4 * kk + q];
+                        acc[j] = __builtin_amdgcn_mfma_f64_16x16x4f64(x, y, acc[j], 0, 0, 0);
+                    }
+                }
+            }
+            // between MFMA groups: convert one slot of the next k-step, then
+            // reuse its registers for the k-step after that (a full k-step of
+            // matrix work before they are needed)
+            constexpr int EVERY = (GW_KR / 4) / NSLOT;
+            if ((kk % EVERY) == EVERY - 1 && has1) {
+                const int i = kk / EVERY;
+                stage_slot(i, kw1, cur ^ 1);
+                if (has2) load_slot(i, r0 + 2 * GW_KR);
             }
         }
+        if (has1 && diag && ti == 0 && tid == 0) nkeep += (double)__popc(kw1);
+        lds_barrier();                                 // next buffer written, this one read by all waves
+        cur ^= 1;
     }
 
-    // this wave's quadrant of the chunk partial
+    // this wave's blocks of the chunk partial
     double *pg = part_g + (int64_t)L * GW_TILE * GW_TILE;
-    if (work) {
+    if (!diag) {
 #pragma unroll
         for (int a = 0; a < 4; ++a)
 #pragma unroll
@@ -496,22 +573,83 @@ __global__ void __launch_bounds__(GW_BLOCK, 2) gram_wide_kernel(const GramCol *c
 #pragma unroll
                 for (int rr = 0; rr < 4; ++rr) {
                     const int i = 64 * qa + 16 * a + q + 4 * rr, j = 32 * qb + 16 * b + cl;
-                    pg[i * GW_TILE + j] = acc[a][b][rr];
+                    pg[i * GW_TILE + j] = acc[2 * a + b][rr];
                 }
-    }
-    if (diag) {
+    } else {
+#pragma unroll
+        for (int jb = 0; jb < NACC; ++jb)
+            if (jb < dn) {
+#pragma unroll
+                for (int rr = 0; rr < 4; ++rr) {
+                    const int i = 16 * dbi[jb] + q + 4 * rr, j = 16 * dbj[jb] + cl;
+                    pg[i * GW_TILE + j] = acc[jb][rr];
+                }
+            }
         // column sums: the 8 quads of a column are 8 consecutive lanes
 #pragma unroll
-        for (int i = 0; i < GW_SLOTS; ++i) {
+        for (int i = 0; i < NSLOT; ++i) {
             double v = csum[i];
             v += __shfl_xor(v, 1, WAVE);
             v += __shfl_xor(v, 2, WAVE);
             v += __shfl_xor(v, 4, WAVE);
-            const int p = tid + GW_BLOCK * i;
-            const int c = p >> 3;
-            if (sact[i] && (p & 7) == 0) part_cs[((int64_t)s * side + ti) * GW_TILE + c] = v;
+            const int c = (tid + GW_BLOCK * i) >> 3;
+            if (squad == 0) part_cs[((int64_t)s * side + ti) * GW_TILE + c] = v;
         }
         if (ti == 0 && tid == 0) part_n[s] = nkeep;
+    }
+}
+
+// Persistent workgroups (one per CU, 136 KiB of LDS each) pull units -- one
+// (row chunk, tile) pair each, chunk-major so that concurrently running units
+// share their rows in the L2/Infinity Cache -- from an atomic counter until
+// none is left.  Units are ~1/16 of a workgroup's share, so the diagonal tiles'
+// lighter units and the tail balance out; each unit writes its own partial,
+// so the result does not depend on which workgroup ran it.
+__global__ void __launch_bounds__(GW_BLOCK, 2) gram_wide_kernel(const GramCol *cols, int ncols, const double *shift,
+                                                              const uint32_t *keep, int64_t n, int side, int T,
+                                                              int S, int64_t rows_per_chunk, double *part_g,
+                                                              double *part_cs, double *part_n,
+                                                              unsigned int *next_unit) {
+    __shared__ double pa[2][GW_TILE * GW_PITCH];
+    __shared__ double pb[2][GW_TILE * GW_PITCH];
+    __shared__ int s_unit;
+    const int U = S * T;
+    for (;;) {
+        if (threadIdx.x == 0) s_unit = (int)atomicAdd(next_unit, 1u);
+        __syncthreads();
+        const int L = s_unit;
+        __syncthreads();                           // everyone has read s_unit before it is rewritten
+        if (L >= U) return;
+        int ti = 0, rem = L % T;                   // diagonal tiles take their own instantiation
+        while (rem >= side - ti) { rem -= side - ti; ++ti; }
+        const int tj = ti + rem;
+        // uniform dtype kind of the tile's columns (padding columns count as any kind)
+        int f32 = 1, f64 = 1;
+        for (int c = threadIdx.x; c < 2 * GW_TILE; c += GW_BLOCK) {
+            const int gc = (c >= GW_TILE ? tj : ti) * GW_TILE + (c & (GW_TILE - 1));
+            if (gc < ncols) {
+                f32 &= cols[gc].dtype == SDP_F32;
+                f64 &= cols[gc].dtype == SDP_F64;
+            }
+        }
+        f32 = __syncthreads_and(f32);
+        f64 = __syncthreads_and(f64);
+        const int64_t c1 = min(n, (int64_t)(L / T) * rows_per_chunk + rows_per_chunk);
+        const bool whole = n >= 4 && c1 <= (n & ~(int64_t)3);   // no ragged tail rows in this chunk
+        const int kind = whole && f32 ? GW_F32 : (whole && f64 ? GW_F64 : GW_GENERIC);
+#define GW_CALL(D, K) gram_wide_unit<D, K>(L, cols, ncols, shift, keep, n, side, T, rows_per_chunk, part_g, part_cs, \
+                                          part_n, pa, pb)
+        if (rem == 0) {
+            if (kind == GW_F32) GW_CALL(true, GW_F32);
+            else if (kind == GW_F64) GW_CALL(true, GW_F64);
+            else GW_CALL(true, GW_GENERIC);
+        } else {
+            if (kind == GW_F32) GW_CALL(false, GW_F32);
+            else if (kind == GW_F64) GW_CALL(false, GW_F64);
+            else GW_CALL(false, GW_GENERIC);
+        }
+#undef GW_CALL
+        __syncthreads();                           // the unit's LDS reads are done before the next unit stages
     }
 }
 
@@ -576,11 +714,12 @@ struct GramGeom {
 static GramGeom gram_geom(int64_t n, int ncols) {
     GramGeom g;
     if (ncols > 64) {
-        // wide kernel: ~2048 workgroups (4 rounds of 2 per CU), chunks of whole k-steps
+        // wide kernel: ~4096 (chunk, tile) units pulled by 256 persistent
+        // workgroups, chunks of whole k-steps
         g.tile = GW_TILE;
         g.side = (ncols + GW_TILE - 1) / GW_TILE;
         g.T = g.side * (g.side + 1) / 2;
-        int64_t S = (2048 + g.T - 1) / g.T;
+        int64_t S = (4096 + g.T - 1) / g.T;
         const int64_t max_s = (n + 4095) / 4096;
         if (S > max_s) S = max_s;
         if (S < 1) S = 1;
@@ -635,6 +774,7 @@ extern "C" int64_t sdp_gram_workspace_bytes(int64_t length, int32_t ncols) {
     b += align256((int64_t)g.S * g.side * g.tile * sizeof(double));
     b += align256((int64_t)g.S * sizeof(double));
     b += align256((int64_t)ncols * sizeof(MaskCol));
+    b += 256;                                       // wide kernel's unit counter
     return b;
 }
 
@@ -691,10 +831,16 @@ extern "C" int sdp_gram(const sdp_column *cols, int32_t ncols, const uint32_t *d
     free(h);
     if (e != hipSuccess) return set_error(SDP_EHIP, "sdp_gram: %s", hipGetErrorString(e));
     if (g.tile == GW_TILE) {
+        // unit counter: the last 256 bytes of the workspace
+        unsigned int *ctr = (unsigned int *)((char *)d_work + sdp_gram_workspace_bytes(n, ncols) - 256);
+        hipError_t me = hipMemsetAsync(ctr, 0, sizeof(unsigned int), s);
+        if (me != hipSuccess) return set_error(SDP_EHIP, "sdp_gram: %s", hipGetErrorString(me));
+        int dev = 0, cus = 256;
+        if (hipGetDevice(&dev) == hipSuccess) hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
         const int G = g.S * g.T;
-        const dim3 wgrid((unsigned)((G + 7) / 8 * 8));
-        hipLaunchKernelGGL(gram_wide_kernel, wgrid, dim3(GW_BLOCK), 0, s, d_cols, ncols, d_shift, d_keep, n, g.side,
-                           g.T, g.S, g.rows_per_chunk, pg, pcs, pn);
+        const int wg = cus < G ? cus : G;
+        hipLaunchKernelGGL(gram_wide_kernel, dim3((unsigned)wg), dim3(GW_BLOCK), 0, s, d_cols, ncols, d_shift, d_keep,
+                           n, g.side, g.T, g.S, g.rows_per_chunk, pg, pcs, pn, ctr);
         int rcw = check_launch("gram_wide_kernel");
         if (rcw) return rcw;
         hipLaunchKernelGGL(gram_reduce_kernel<GW_TILE>, dim3(g.T * (GW_TILE * GW_TILE / R_EB)), dim3(R_EB * R_P), 0, s,

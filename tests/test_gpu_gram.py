@@ -13,12 +13,12 @@ pytestmark = pytest.mark.gpu
 DTYPES = [np.float64, np.int64, np.float32, np.int32, np.int16, np.uint8, np.uint32, np.float64]
 
 
-def _table(n, ncols, seed):
+def _table(n, ncols, seed, dtypes=DTYPES):
     g = np.random.default_rng(seed)
     cols, host = {}, []
     base = g.standard_normal(n)
     for c in range(ncols):
-        dt = DTYPES[c % len(DTYPES)]
+        dt = dtypes[c % len(dtypes)]
         x = 40 * (0.5 * base + g.standard_normal(n)) + (c % 5) * 7
         if np.issubdtype(dt, np.unsignedinteger):
             x = np.clip(np.abs(x), 0, 250)
@@ -33,12 +33,22 @@ def _table(n, ncols, seed):
     return pa.table(cols), np.stack(host, axis=1)
 
 
-@pytest.mark.parametrize('n,ncols', [(5003, 12), (4099, 21), (3001, 40), (2053, 70), (1, 3), (37, 17)])
-def test_gram_matches_numpy(n, ncols):
+# > 64 columns take the wide kernel (128-column tiles): diagonal and
+# off-diagonal tiles x {all f32, all f64, mixed} staging paths, padding
+# columns of a partial last tile, chunks with a ragged tail (n % 4 != 0),
+# several row chunks per tile.
+WIDE = [(2053, 70, None), (20011, 200, None), (40000, 160, 'f32'), (9999, 130, 'f32'), (30002, 257, 'f64'),
+        (7, 129, 'f64'), (3, 300, None)]
+
+
+@pytest.mark.parametrize('n,ncols,kind', [(5003, 12, None), (4099, 21, None), (3001, 40, None), (1, 3, None),
+                                          (37, 17, None)] + WIDE)
+def test_gram_matches_numpy(n, ncols, kind):
     import torch
     from spark_df_profiling.columns import DeviceTable
     from spark_df_profiling.engine import Engine
-    tab, X = _table(n, ncols, seed=n + ncols)
+    dtypes = {None: DTYPES, 'f32': [np.float32], 'f64': [np.float64]}[kind]
+    tab, X = _table(n, ncols, seed=n + ncols, dtypes=dtypes)
     dt = DeviceTable.from_arrow(tab, torch.device('cuda'))
     cols = [dt.column(c) for c in tab.column_names]
     keep = ~np.isnan(X).any(axis=1)
