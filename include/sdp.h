@@ -196,6 +196,45 @@ int sdp_sort_small(uint64_t *d_keys, const uint64_t *d_n, void *stream);
 /* n_sets independent in-place sorts of n_each (<= 16384) keys, one launch
  * (heavy-key samples of all columns). */
 int sdp_sort_small_batch(uint64_t *d_keys, int32_t n_each, int32_t n_sets, void *stream);
+/* Batched selects: Q independent k-th-key selects (each as sdp_select_kth:
+ * keys in [lo_key, hi_key], workspace sdp_select_kth_workspace_bytes(n_cap) at
+ * d_work, result written to *d_result) queued with ~2 launches per radix
+ * round for all of them -- the per-quantile Spark jobs of describe.py:203-208
+ * for every numeric column at once.  d_tasks is a DEVICE array of Q tasks;
+ * d_hist holds Q x 2048 u64 digit histograms.  rounds = the max over tasks of
+ * sdp_select_rounds(lo, hi).  Row-sharded callers use the split form:
+ * sdp_select_batch_init (round 0's local histograms), then per round r an
+ * all-reduce of d_hist followed by sdp_select_batch_step(r, last). */
+typedef struct sdp_select_task {
+    const uint64_t *d_keys;
+    const uint64_t *d_n;               /* device count of keys (<= n_cap)           */
+    int64_t         n_cap;
+    int64_t         k;                 /* 0-based rank                              */
+    uint64_t        lo_key, hi_key;
+    void           *d_work;
+    uint64_t       *d_result;
+} sdp_select_task;
+
+int sdp_select_batch(const sdp_select_task *d_tasks, int32_t q, int32_t rounds, uint64_t *d_hist, void *stream);
+int sdp_select_batch_init(const sdp_select_task *d_tasks, int32_t q, uint64_t *d_hist, void *stream);
+int sdp_select_batch_step(const sdp_select_task *d_tasks, int32_t q, int32_t round, int32_t last, uint64_t *d_hist,
+                          void *stream);
+
+/* Batched sdp_compact_candidates: task i copies the d_counts[s] keys of each
+ * of its nseg wave segments (cap slots apart in d_cand) densely to d_out and
+ * their total to *d_out_count (d_offsets_work: nseg u64). */
+typedef struct sdp_compact_task {
+    const uint64_t *d_cand;
+    const uint32_t *d_counts;
+    int64_t         nseg;
+    int64_t         cap;
+    uint64_t       *d_offsets_work;
+    uint64_t       *d_out;
+    uint64_t       *d_out_count;
+} sdp_compact_task;
+
+int sdp_compact_batch(const sdp_compact_task *d_tasks, int32_t q, int64_t max_nseg, void *stream);
+
 /* Write the order-preserving keys of all na.drop rows (fallback select). */
 int sdp_column_keys(const sdp_column *col, uint64_t *d_out, uint64_t *d_out_n,
                     void *stream);

@@ -836,7 +836,7 @@ extern "C" int sdp_gram(const sdp_column *cols, int32_t ncols, const uint32_t *d
         hipError_t me = hipMemsetAsync(ctr, 0, sizeof(unsigned int), s);
         if (me != hipSuccess) return set_error(SDP_EHIP, "sdp_gram: %s", hipGetErrorString(me));
         int dev = 0, cus = 256;
-        if (hipGetDevice(&dev) == hipSuccess) hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+        if (hipGetDevice(&dev) == hipSuccess && hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) cus = 256;
         const int G = g.S * g.T;
         const int wg = cus < G ? cus : G;
         hipLaunchKernelGGL(gram_wide_kernel, dim3((unsigned)wg), dim3(GW_BLOCK), 0, s, d_cols, ncols, d_shift, d_keep,

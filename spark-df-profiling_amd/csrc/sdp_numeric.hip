@@ -1265,6 +1265,253 @@ extern "C" int sdp_select_step(const uint64_t *d_keys, const uint64_t *d_n, int6
     return check_launch("radix_filter_hist_st_kernel");
 }
 
+// ---- batched selects: every order statistic of every column of a table -------------
+// One launch per stage for all Q tasks (blockIdx.y = task), so the selects of a
+// whole table cost ~2 launches per radix round instead of ~2 per round per
+// select (512 columns x 5 quantiles = 2560 selects in C5).  Task i keeps the
+// workspace layout of sdp_select_kth in tasks[i].d_work and its round-r digit
+// histogram at d_hist + 2048 i (the array a sharded caller all-reduces).
+static __device__ __forceinline__ SelState *task_state(const sdp_select_task &t) { return (SelState *)t.d_work; }
+static __device__ __forceinline__ int64_t sel_align_d(int64_t x) { return (x + 255) / 256 * 256; }
+static __device__ __forceinline__ void task_io(const sdp_select_task &t, int round, const uint64_t *&cur,
+                                               const uint64_t *&cur_n, uint64_t *&out, uint64_t *&out_n) {
+    char *w = (char *)t.d_work + sel_align_d(sizeof(SelState)) + sel_align_d(2048 * 8);
+    uint64_t *cnt0 = (uint64_t *)w, *cnt1 = (uint64_t *)(w + sel_align_d(8));
+    w += 2 * sel_align_d(8);
+    uint64_t *buf0 = (uint64_t *)w;
+    uint64_t *buf1 = (uint64_t *)(w + sel_align_d(8 * (t.n_cap > 0 ? t.n_cap : 1)));
+    cur = round == 0 ? t.d_keys : ((round - 1) & 1 ? buf1 : buf0);
+    cur_n = round == 0 ? t.d_n : ((round - 1) & 1 ? cnt1 : cnt0);
+    out = (round & 1) ? buf1 : buf0;
+    out_n = (round & 1) ? cnt1 : cnt0;
+}
+
+__global__ void select_init_batch_kernel(const sdp_select_task *tasks, uint64_t *hist) {
+    const sdp_select_task t = tasks[blockIdx.x];
+    SelState *st = task_state(t);
+    if (threadIdx.x == 0) {
+        const uint64_t x = t.lo_key ^ t.hi_key;
+        const int shift0 = x ? ((63 - __clzll((long long)x)) / 11) * 11 : 0;
+        st->prefix = shift0 + 11 < 64 ? (t.lo_key >> (shift0 + 11)) : 0ull;
+        st->k = t.k;
+        st->shift = shift0;
+        st->done = 0;
+        st->result = EMPTY64;
+    }
+    uint64_t *h = hist + (int64_t)blockIdx.x * 2048;
+    for (int i = threadIdx.x; i < 2048; i += blockDim.x) h[i] = 0;
+}
+
+__global__ void radix_hist_batch_kernel(const sdp_select_task *tasks, int round, uint64_t *hist) {
+    const sdp_select_task t = tasks[blockIdx.y];
+    const SelState *st = task_state(t);
+    if (st->done) return;
+    const uint64_t *keys, *n_ptr;
+    uint64_t *o, *on;
+    task_io(t, round, keys, n_ptr, o, on);
+    __shared__ uint32_t h[2048];
+    for (int i = threadIdx.x; i < 2048; i += blockDim.x) h[i] = 0;
+    __syncthreads();
+    const uint64_t n = *n_ptr, prefix = st->prefix;
+    const int shift = st->shift, top = shift + 11;
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    constexpr int R = 4;
+    for (; i + (R - 1) * stride < n; i += R * stride) {
+        uint64_t k[R];
+#pragma unroll
+        for (int r = 0; r < R; ++r) k[r] = keys[i + r * stride];
+#pragma unroll
+        for (int r = 0; r < R; ++r)
+            if (top >= 64 || (k[r] >> top) == prefix) atomicAdd(&h[(k[r] >> shift) & 2047u], 1u);
+    }
+    for (; i < n; i += stride) {
+        const uint64_t k = keys[i];
+        if (top >= 64 || (k >> top) == prefix) atomicAdd(&h[(k >> shift) & 2047u], 1u);
+    }
+    __syncthreads();
+    uint64_t *gh = hist + (int64_t)blockIdx.y * 2048;
+    for (int i = threadIdx.x; i < 2048; i += blockDim.x)
+        if (h[i]) atomicAdd((unsigned long long *)&gh[i], (unsigned long long)h[i]);
+}
+
+__global__ void __launch_bounds__(1024) radix_decide_batch_kernel(const sdp_select_task *tasks, int round,
+                                                                  uint64_t *hist) {
+    const sdp_select_task t = tasks[blockIdx.x];
+    const uint64_t *c, *cn;
+    uint64_t *o, *on;
+    task_io(t, round, c, cn, o, on);
+    // (the decide body of the single-select path; a task that finished in an
+    // earlier round returns at once)
+    SelState *st = task_state(t);
+    if (st->done) return;
+    uint64_t *hh = hist + (int64_t)blockIdx.x * 2048;
+    __shared__ uint64_t sm[1024];
+    __shared__ int s_j;
+    __shared__ uint64_t s_before;
+    const int th = threadIdx.x;
+    const uint64_t a = hh[2 * th], b = hh[2 * th + 1];
+    sm[th] = a + b;
+    if (th == 0) { s_j = -1; s_before = 0; }
+    __syncthreads();
+    for (int off = 1; off < 1024; off <<= 1) {
+        const uint64_t v = th >= off ? sm[th - off] : 0;
+        __syncthreads();
+        sm[th] += v;
+        __syncthreads();
+    }
+    const uint64_t k = (uint64_t)st->k;
+    const uint64_t excl = sm[th] - a - b;
+    if (excl <= k && k < sm[th]) {
+        s_j = k < excl + a ? 2 * th : 2 * th + 1;
+        s_before = k < excl + a ? excl : excl + a;
+    }
+    __syncthreads();
+    hh[2 * th] = 0;
+    hh[2 * th + 1] = 0;
+    if (th == 0) {
+        if (s_j < 0) {
+            st->done = 1;
+            st->result = EMPTY64;
+            *t.d_result = EMPTY64;
+        } else {
+            st->k = (int64_t)(k - s_before);
+            st->prefix = (st->shift + 11 >= 64 ? 0ull : (st->prefix << 11)) | (uint64_t)s_j;
+            if (st->shift == 0) {
+                st->done = 1;
+                st->result = st->prefix;
+                *t.d_result = st->prefix;
+            } else {
+                st->shift -= 11;
+            }
+        }
+        *on = 0;                                   // the next round's survivor count
+    }
+}
+
+__global__ void radix_filter_hist_batch_kernel(const sdp_select_task *tasks, int round, uint64_t *hist) {
+    const sdp_select_task t = tasks[blockIdx.y];
+    const SelState *st = task_state(t);
+    if (st->done) return;
+    const uint64_t *keys, *n_ptr;
+    uint64_t *out, *out_n;
+    task_io(t, round, keys, n_ptr, out, out_n);
+    __shared__ uint64_t s_buf[STAGE];
+    __shared__ uint32_t s_cnt;
+    __shared__ uint64_t s_gbase;
+    __shared__ uint32_t h[2048];
+    for (int i = threadIdx.x; i < 2048; i += blockDim.x) h[i] = 0;
+    if (threadIdx.x == 0) s_cnt = 0;
+    __syncthreads();
+    Stager sg{s_buf, &s_cnt, &s_gbase};
+    const uint64_t n = *n_ptr, prefix = st->prefix;
+    const int shift = st->shift, top = shift + 11;
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    const uint64_t iters = (n + stride - 1) / stride;
+    for (uint64_t it = 0; it < iters; ++it) {
+        const uint64_t i = it * stride + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+        uint64_t k = 0;
+        bool keep = false;
+        if (i < n) {
+            k = keys[i];
+            keep = top >= 64 ? true : ((k >> top) == prefix);
+            if (keep) atomicAdd(&h[(k >> shift) & 2047u], 1u);
+        }
+        stage_push(sg, keep, k, out, (unsigned long long *)out_n, it + 1 == iters);
+    }
+    __syncthreads();
+    uint64_t *gh = hist + (int64_t)blockIdx.y * 2048;
+    for (int i = threadIdx.x; i < 2048; i += blockDim.x)
+        if (h[i]) atomicAdd((unsigned long long *)&gh[i], (unsigned long long)h[i]);
+}
+
+// Batched candidate compaction: task i scans its segment counts (one
+// workgroup) and copies its segments (grid.x workgroups) -- two launches for
+// every window of every column.
+__global__ void __launch_bounds__(1024) scan_counts_batch_kernel(const sdp_compact_task *tasks) {
+    const sdp_compact_task t = tasks[blockIdx.x];
+    __shared__ uint64_t sm[1024];
+    __shared__ uint64_t carry;
+    if (threadIdx.x == 0) carry = 0;
+    __syncthreads();
+    for (int64_t base = 0; base < t.nseg; base += 1024) {
+        const int64_t i = base + threadIdx.x;
+        const uint64_t v = i < t.nseg ? t.d_counts[i] : 0;
+        sm[threadIdx.x] = v;
+        __syncthreads();
+        for (int o = 1; o < 1024; o <<= 1) {
+            const uint64_t x = threadIdx.x >= o ? sm[threadIdx.x - o] : 0;
+            __syncthreads();
+            sm[threadIdx.x] += x;
+            __syncthreads();
+        }
+        if (i < t.nseg) t.d_offsets_work[i] = carry + sm[threadIdx.x] - v;
+        __syncthreads();
+        if (threadIdx.x == 1023) carry += sm[1023];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) *t.d_out_count = carry;
+}
+
+__global__ void copy_segments_batch_kernel(const sdp_compact_task *tasks) {
+    const sdp_compact_task t = tasks[blockIdx.y];
+    for (int64_t b = blockIdx.x; b < t.nseg; b += gridDim.x) {
+        const uint32_t c = t.d_counts[b];
+        const uint64_t base = t.d_offsets_work[b];
+        const uint64_t *src = t.d_cand + b * t.cap;
+        for (uint32_t i = threadIdx.x; i < c; i += blockDim.x) t.d_out[base + i] = src[i];
+    }
+}
+
+static int select_batch_blocks(int32_t q) {
+    int hb = (2048 + q - 1) / q;
+    return hb < 16 ? 16 : (hb > 512 ? 512 : hb);
+}
+
+extern "C" int sdp_compact_batch(const sdp_compact_task *d_tasks, int32_t q, int64_t max_nseg, void *stream) {
+    if (q < 1 || max_nseg < 1) return set_error(SDP_EINVAL, "sdp_compact_batch: q %d max_nseg %lld", q,
+                                                 (long long)max_nseg);
+    hipStream_t s = (hipStream_t)stream;
+    hipLaunchKernelGGL(scan_counts_batch_kernel, dim3((unsigned)q), dim3(1024), 0, s, d_tasks);
+    int rc = check_launch("scan_counts_batch_kernel");
+    if (rc) return rc;
+    const int64_t gx = max_nseg < 1024 ? max_nseg : 1024;
+    hipLaunchKernelGGL(copy_segments_batch_kernel, dim3((unsigned)gx, (unsigned)q), dim3(256), 0, s, d_tasks);
+    return check_launch("copy_segments_batch_kernel");
+}
+
+extern "C" int sdp_select_batch_init(const sdp_select_task *d_tasks, int32_t q, uint64_t *d_hist, void *stream) {
+    if (q < 1 || d_hist == nullptr) return set_error(SDP_EINVAL, "sdp_select_batch_init: q %d", q);
+    hipStream_t s = (hipStream_t)stream;
+    hipLaunchKernelGGL(select_init_batch_kernel, dim3((unsigned)q), dim3(256), 0, s, d_tasks, d_hist);
+    int rc = check_launch("select_init_batch_kernel");
+    if (rc) return rc;
+    hipLaunchKernelGGL(radix_hist_batch_kernel, dim3((unsigned)select_batch_blocks(q), (unsigned)q), dim3(256), 0, s,
+                       d_tasks, 0, d_hist);
+    return check_launch("radix_hist_batch_kernel");
+}
+
+extern "C" int sdp_select_batch_step(const sdp_select_task *d_tasks, int32_t q, int32_t round, int32_t last,
+                                     uint64_t *d_hist, void *stream) {
+    if (q < 1 || round < 0 || round > 5 || d_hist == nullptr)
+        return set_error(SDP_EINVAL, "sdp_select_batch_step: q %d round %d", q, round);
+    hipStream_t s = (hipStream_t)stream;
+    hipLaunchKernelGGL(radix_decide_batch_kernel, dim3((unsigned)q), dim3(1024), 0, s, d_tasks, round, d_hist);
+    int rc = check_launch("radix_decide_batch_kernel");
+    if (rc || last) return rc;
+    hipLaunchKernelGGL(radix_filter_hist_batch_kernel, dim3((unsigned)select_batch_blocks(q), (unsigned)q), dim3(256),
+                       0, s, d_tasks, round, d_hist);
+    return check_launch("radix_filter_hist_batch_kernel");
+}
+
+extern "C" int sdp_select_batch(const sdp_select_task *d_tasks, int32_t q, int32_t rounds, uint64_t *d_hist,
+                                void *stream) {
+    if (rounds < 1 || rounds > 6) return set_error(SDP_EINVAL, "sdp_select_batch: rounds %d", rounds);
+    int rc = sdp_select_batch_init(d_tasks, q, d_hist, stream);
+    for (int r = 0; r < rounds && !rc; ++r) rc = sdp_select_batch_step(d_tasks, q, r, r == rounds - 1, d_hist, stream);
+    return rc;
+}
+
 extern "C" int sdp_sort_small(uint64_t *d_keys, const uint64_t *d_n, void *stream) {
     hipLaunchKernelGGL(sort_small_kernel, dim3(1), dim3(1024), 0, (hipStream_t)stream, d_keys, d_n);
     return check_launch("sort_small_kernel");

@@ -80,6 +80,18 @@ class SdpPass1Result(ctypes.Structure):
                 ('w_overflow', ctypes.c_uint32), ('_pad', ctypes.c_uint32)]
 
 
+class SdpSelectTask(ctypes.Structure):
+    _fields_ = [('d_keys', ctypes.c_void_p), ('d_n', ctypes.c_void_p), ('n_cap', ctypes.c_int64),
+                ('k', ctypes.c_int64), ('lo_key', ctypes.c_uint64), ('hi_key', ctypes.c_uint64),
+                ('d_work', ctypes.c_void_p), ('d_result', ctypes.c_void_p)]
+
+
+class SdpCompactTask(ctypes.Structure):
+    _fields_ = [('d_cand', ctypes.c_void_p), ('d_counts', ctypes.c_void_p), ('nseg', ctypes.c_int64),
+                ('cap', ctypes.c_int64), ('d_offsets_work', ctypes.c_void_p), ('d_out', ctypes.c_void_p),
+                ('d_out_count', ctypes.c_void_p)]
+
+
 class SdpPass2Result(ctypes.Structure):
     _fields_ = [('abs_dev_sum', ctypes.c_double), ('n_high', ctypes.c_uint64), ('n_low', ctypes.c_uint64),
                 ('n_unbinned', ctypes.c_uint64)]
@@ -118,6 +130,10 @@ _SIGNATURES = {
     'sdp_select_hist': (ctypes.c_int, [_P, _P, _I64, _I32, _P, _I64, _P, _P]),
     'sdp_select_step': (ctypes.c_int, [_P, _P, _I64, _I32, _I32, _P, _I64, _P, _P, _P]),
     'sdp_column_keys': (ctypes.c_int, [_COL, _P, _P, _P]),
+    'sdp_select_batch': (ctypes.c_int, [_P, _I32, _I32, _P, _P]),
+    'sdp_select_batch_init': (ctypes.c_int, [_P, _I32, _P, _P]),
+    'sdp_select_batch_step': (ctypes.c_int, [_P, _I32, _I32, _I32, _P, _P]),
+    'sdp_compact_batch': (ctypes.c_int, [_P, _I32, _I64, _P]),
     'sdp_pass2': (ctypes.c_int, [_COL, _D, _P, _I32, _I32, _D, _D, _P, _I64, _P, _P, _P]),
     'sdp_table_clear': (ctypes.c_int, [_P, _P, _I64, _I32, _P]),
     'sdp_hash_u64': (ctypes.c_int, [_COL, _P, _P, _P, _I64, _I32, _P, _P]),

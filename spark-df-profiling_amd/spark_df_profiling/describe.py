@@ -155,7 +155,11 @@ def describe_1d(engine: Engine, col: DeviceColumn, nrows, bins, k, freq, bundle)
         stats = OrderedDict([('type', 'CONST')])
         stats['value_counts'] = _value_counts_first(engine, col, 1)
     elif numeric:
-        st = engine.numeric_stats(col, bins=bins, k=k, p1_pack=p1_pack)
+        st = bundle.pop('numeric_pre', None)
+        if st is None:
+            st = engine.numeric_stats(col, bins=bins, k=k, p1_pack=p1_pack)
+        elif st.error is not None:
+            raise st.error                     # e.g. describe.py:46 with bins=1
         bundle['numeric'] = st
         stats = _numeric_series(st, nrows)
     elif spark_t in DATE_TYPES:
@@ -177,6 +181,13 @@ def describe_1d(engine: Engine, col: DeviceColumn, nrows, bins, k, freq, bundle)
     else:
         res['mode'] = 0
     return res
+
+
+def _const_numeric(st):
+    """describe_1d's CONST test (distinct <= 1, describe.py:156) from pass-1
+    alone: no non-null value, or one value and no NaN (NaN is a distinct
+    value of its own for countDistinct)."""
+    return st.count == 0 or (st.min == st.max and st.n_nan == 0)
 
 
 def _is_numeric(col):
@@ -273,20 +284,36 @@ def describe(df, bins=10, corr_reject=0.9, **kwargs):
     world, rank = engine.comm.world, engine.comm.rank
     owner = {col.name: i % world for i, col in enumerate(table.columns)}
 
+    early_plots = {}
+
     def one(eng, col):
         res = describe_1d(eng, col, n, bins, k_vals.get(col.name, 2), t_freq.get(col.name, 'D'), bundles[col.name])
         # rendered by worker processes while the next columns' kernels run; on
         # a sharded table each rank renders the columns it owns (index % world)
         mine = owner[col.name] == rank
-        fut = _submit_plot(bundles[col.name]['numeric']) if plots and res['type'] == 'NUM' and mine else None
+        fut = early_plots.pop(col.name, None)
+        if fut is None and plots and res['type'] == 'NUM' and mine:
+            fut = _submit_plot(bundles[col.name]['numeric'])
+        if res['type'] != 'NUM':
+            fut = None
         return res, fut
 
     workers = column_workers(engine, kwargs.pop('workers', None))
     if workers == 1:
-        # pass 1 of every numeric column queued back to back (two readbacks in all)
+        # whole-table stages: pass 1 of every numeric column (two readbacks),
+        # then every column's order statistics and pass 2 (two more) -- the
+        # per-column loop below only counts distincts and assembles
         num_cols = [c for c in table.columns if _is_numeric(c)]
-        for col, pack in zip(num_cols, engine.numeric_pass1_batch(num_cols)):
+        packs = engine.numeric_pass1_batch(num_cols)
+        stats = engine.numeric_stats_batch(num_cols, packs, bins, [k_vals.get(c.name, 2) for c in num_cols])
+        for col, pack, st in zip(num_cols, packs, stats):
             bundles[col.name]['p1_pack'] = pack
+            if st is not None:
+                bundles[col.name]['numeric_pre'] = st
+                # the histogram images render while the distinct counts run; a
+                # column that turns out CONST (one distinct value) is never NUM
+                if plots and st.error is None and owner[col.name] == rank and not _const_numeric(st):
+                    early_plots[col.name] = _submit_plot(st)
     if workers > 1:
         done = _describe_concurrent(engine, table.columns, one, workers)
     else:

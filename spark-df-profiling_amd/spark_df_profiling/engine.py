@@ -162,6 +162,7 @@ class NumericStats:
     low_idx: int = 0
     thresholds: tuple = ()
     fallback_used: bool = False
+    error: Optional[Exception] = None      # raised when describe_1d reaches the column
 
 
 class Engine:
@@ -518,6 +519,237 @@ class Engine:
         st.low_idx = r2['n_low']
         st.thresholds = (hi_t, lo_t)
         return st
+
+    # ==========================================================================
+    # whole-table batches: every numeric column's order statistics, then every
+    # column's pass 2, each with ONE host readback (one collective set when
+    # sharded) instead of one or more per column
+    # ==========================================================================
+    def _queue_column_selects(self, col, p1, plan, cand_info, probs, compact, selects):
+        """Decide, for each rank a column needs (describe.py:203-208), whether a
+        window bound resolves it from pass-1's counts or a select must run (in
+        a window's compacted candidates, or -- missed window / slot overflow --
+        over all the column's keys).  Appends compaction and select tasks; the
+        returned state is finished by _finish_column_quantiles."""
+        n = p1['count']
+        is_int = not col.is_float
+        needed = {}
+        for p in probs:
+            if is_int:
+                pos = (n - 1) * p
+                needed[p] = (pos, math.floor(pos), math.ceil(pos))
+            else:
+                needed[p] = (None, spark_percentile_approx_rank(n, p) - 1, None)
+        ranks = sorted({r for v in needed.values() for r in (v[1], v[2]) if r is not None})
+        values, dense, fallback = {}, {}, None
+        for r in ranks:
+            key = None
+            for w in range(plan.n_windows):
+                size = p1['w_eq_lo'][w] + p1['w_in'][w] + p1['w_eq_hi'][w]
+                below = n - p1['w_gt'][w] - size
+                if below <= r < below + size:
+                    rr = r - below
+                    lo, hi = plan.lo[w], plan.hi[w]
+                    if rr < p1['w_eq_lo'][w]:
+                        key = lo
+                    elif rr < p1['w_eq_lo'][w] + p1['w_in'][w]:
+                        if (p1['w_overflow'] >> w) & 1:
+                            break
+                        if w not in dense:
+                            # dense copy sized by the window's (global) inside count
+                            cap = max(1, int(p1['w_in'][w]))
+                            out, out_n = self._u64(cap), self._u64(1, zero=True)
+                            nseg, slot = cand_info['nseg'], cand_info['cap']
+                            compact.append((cand_info['cand'][w * nseg * slot:], cand_info['counts'][w * nseg:],
+                                            nseg, slot, self._u64(nseg), out, out_n))
+                            dense[w] = (out, out_n, cap)
+                        out, out_n, cap = dense[w]
+                        selects.append([r, out, out_n, cap, rr - p1['w_eq_lo'][w], lo, hi, cap])
+                        key = 'queued'
+                    else:
+                        key = hi
+                    break
+            if key is None:                                    # window missed: exact fallback
+                if fallback is None:
+                    fallback = self._all_keys(col)
+                arr, arr_n = fallback
+                # (the last field sizes the workspace budget identically on every rank)
+                selects.append([r, arr, arr_n, arr.numel(), r, 0, EMPTY64, max(1, int(p1['n_valid']))])
+                key = 'queued'
+            values[r] = key
+        return {'values': values, 'needed': needed, 'is_int': is_int, 'probs': probs, 'fallback': fallback,
+                'dense': dense}
+
+    SELECT_BATCH_BYTES = 24 << 30          # select workspaces alive at once (flushed in groups)
+
+    def quantiles_batch(self, items, probs=PROBS):
+        """[(col, p1, plan, cand_info)] -> [(quantiles, fallback_used)] with
+        the candidate compactions of every window in two launches, the selects
+        of every column in ~2 launches per radix round (sdp_select_batch; one
+        all-reduce per round for ALL columns when sharded) and one readback."""
+        s = self._s()
+        states, sel_owner, compact, selects = [], [], [], []
+        for i, (col, p1, plan, cand_info) in enumerate(items):
+            before = len(selects)
+            states.append(self._queue_column_selects(col, p1, plan, cand_info, probs, compact, selects))
+            sel_owner += [i] * (len(selects) - before)
+        keep = []
+        if compact:
+            tasks = (nat.SdpCompactTask * len(compact))()
+            for j, (cand, cnt, nseg, slot, offw, out, out_n) in enumerate(compact):
+                tasks[j] = nat.SdpCompactTask(cand.data_ptr(), cnt.data_ptr(), nseg, slot, offw.data_ptr(),
+                                              out.data_ptr(), out_n.data_ptr())
+            d_tasks = self._h2d(np.frombuffer(bytearray(bytes(tasks)), dtype=np.uint8))
+            sdp.sdp_compact_batch(ptr(d_tasks), len(compact), max(c[2] for c in compact), s)
+            keep.append((d_tasks, compact))
+        res = self._u64(max(1, len(selects)))
+        world = self.comm.world
+        j0 = 0
+        while j0 < len(selects):
+            # a group of selects whose workspaces fit the budget (at least one)
+            j1, tot = j0, 0
+            while j1 < len(selects):
+                wb = int(sdp.sdp_select_kth_workspace_bytes(int(selects[j1][7])))
+                if j1 > j0 and tot + wb > self.SELECT_BATCH_BYTES:
+                    break
+                tot += (wb + 255) // 256 * 256
+                j1 += 1
+            q = j1 - j0
+            tot = sum((int(sdp.sdp_select_kth_workspace_bytes(int(x[3]))) + 255) // 256 * 256 for x in selects[j0:j1])
+            work = self._bytes(tot)
+            tasks = (nat.SdpSelectTask * q)()
+            off, rounds = 0, 1
+            for t, (r, arr, arr_n, ncap, kk, lo, hi, _) in enumerate(selects[j0:j1]):
+                wb = int(sdp.sdp_select_kth_workspace_bytes(int(ncap)))
+                tasks[t] = nat.SdpSelectTask(arr.data_ptr(), arr_n.data_ptr(), int(ncap), int(kk), _u(lo), _u(hi),
+                                             work.data_ptr() + off, res.data_ptr() + 8 * (j0 + t))
+                off += (wb + 255) // 256 * 256
+                rounds = max(rounds, int(sdp.sdp_select_rounds(_u(lo), _u(hi))))
+            d_tasks = self._h2d(np.frombuffer(bytearray(bytes(tasks)), dtype=np.uint8))
+            hist = self._u64(q * 2048)
+            if world == 1:
+                sdp.sdp_select_batch(ptr(d_tasks), q, rounds, ptr(hist), s)
+            else:
+                sdp.sdp_select_batch_init(ptr(d_tasks), q, ptr(hist), s)
+                for rd in range(rounds):
+                    self.comm.allreduce_sum_(hist)
+                    sdp.sdp_select_batch_step(ptr(d_tasks), q, rd, int(rd == rounds - 1), ptr(hist), s)
+            keep.append((d_tasks, work, hist))
+            j0 = j1
+        keys = self._host_u64(res) if selects else []          # the one readback
+        del keep
+        out = []
+        for i, st in enumerate(states):
+            for j, owner in enumerate(sel_owner):
+                if owner == i:
+                    st['values'][selects[j][0]] = keys[j]
+            out.append(self._finish_column_quantiles(st))
+        return out
+
+    @staticmethod
+    def _finish_column_quantiles(st):
+        values, needed, is_int = st['values'], st['needed'], st['is_int']
+        out = {}
+        for p in st['probs']:
+            pos, lo_r, hi_r = needed[p]
+            if is_int:
+                lk, hk = key_to_int(values[lo_r]), key_to_int(values[hi_r])
+                if hi_r == lo_r or hk == lk:
+                    out[p] = float(lk)
+                else:       # Spark Percentile linear interpolation (A.4)
+                    out[p] = (hi_r - pos) * float(lk) + (pos - lo_r) * float(hk)
+            else:
+                out[p] = key_to_float(values[lo_r])
+        return out, st['fallback'] is not None
+
+    def pass2_batch(self, items):
+        """[(col, mean, edges, hi_t, lo_t)] -> [pass-2 dict] (see pass2), all
+        launched back to back and read back once (sharded: one all-reduce of
+        every column's counts and bins, one all-gather of the mad partials)."""
+        if not items:
+            return []
+        s = self._s()
+        rsz = ctypes.sizeof(nat.SdpPass2Result)
+        outs = []
+        for col, mean, edges, hi_t, lo_t in items:
+            bins = len(edges)
+            e = self._h2d(np.array([float(x) for x in edges], dtype=np.float64))
+            mono = all(math.isfinite(float(x)) for x in edges) and all(
+                float(edges[i]) <= float(edges[i + 1]) for i in range(bins - 1))
+            work = self._bytes(sdp.sdp_pass2_workspace_bytes(col.length, col.dtype, bins))
+            res = self._bytes(rsz)
+            hist = self._u64(bins)
+            cs = col.sdp()
+            nat.annotate(_label(col), col_read_bytes(col))
+            sdp.sdp_pass2(ctypes.byref(cs), float(mean), ptr(e), bins, int(mono), float(hi_t), float(lo_t), ptr(work),
+                          work.numel(), ptr(res), ptr(hist), s)
+            outs.append((res, hist, e, work))
+        if self.comm.world == 1:
+            raw = torch.cat([t for res, hist, _, _ in outs for t in (res[:rsz], hist.view(torch.uint8))]).cpu().numpy()
+            result, off = [], 0
+            for (res, hist, _, _) in outs:
+                r = nat.SdpPass2Result.from_buffer_copy(raw[off:off + rsz].tobytes())
+                off += rsz
+                hb = hist.numel() * 8
+                result.append({'abs_dev_sum': float(r.abs_dev_sum), 'n_high': int(r.n_high), 'n_low': int(r.n_low),
+                               'n_unbinned': int(r.n_unbinned),
+                               'hist': raw[off:off + hb].view(np.int64).astype(np.int64)})
+                off += hb
+            return result
+        # sharded: counts and bins summed exactly; abs-dev partials gathered, summed in rank order
+        parts = [torch.cat([res[:rsz].view(torch.int64)[1:4], hist]) for res, hist, _, _ in outs]
+        summed = self.comm.allreduce_sum(torch.cat(parts)).cpu().numpy()
+        mads = torch.stack([res[:8].view(torch.float64)[0] for res, _, _, _ in outs])
+        allm = torch.stack(self.comm.allgather(mads)).cpu().numpy()        # [world, ncols]
+        result, off = [], 0
+        for i, (res, hist, _, _) in enumerate(outs):
+            v = summed[off:off + 3 + hist.numel()]
+            off += 3 + hist.numel()
+            result.append({'abs_dev_sum': math.fsum(float(x) for x in allm[:, i]), 'n_high': int(v[0]),
+                           'n_low': int(v[1]), 'n_unbinned': int(v[2]), 'hist': v[3:].astype(np.int64)})
+        return result
+
+    def numeric_stats_batch(self, cols, packs, bins=10, ks=None, probs=PROBS):
+        """numeric_stats of every column (None for a column with no non-null
+        value) with two host readbacks in all.  A bins value the reference
+        rejects (describe.py:46 with bins=1) is recorded per column and raised
+        when describe_1d reaches that column, as the reference would."""
+        ks = ks or [2] * len(cols)
+        live = [i for i, pk in enumerate(packs) if pk[0]['count'] > 0]
+        qres = self.quantiles_batch([(cols[i], packs[i][0], packs[i][1], packs[i][2]) for i in live], probs)
+        for i in live:                       # candidate slots are no longer needed
+            packs[i][2]['cand'] = None
+        stats = [None] * len(cols)
+        p2_items, p2_idx = [], []
+        for i, (qs, fb) in zip(live, qres):
+            col, p1 = cols[i], packs[i][0]
+            mom = moments(p1, not col.is_float)
+            st = NumericStats(count=p1['count'], n_valid=p1['n_valid'], n_nan=p1['n_nan'], n_zero=p1['n_zero'],
+                              **mom)
+            st.quantiles = qs
+            st.fallback_used = fb
+            q1, q3 = qs[0.25], qs[0.75]
+            k = ks[i]
+            hi_t = q3 + k * (q3 - q1)                          # describe.py:222
+            lo_t = q1 - k * (q3 - q1)                          # describe.py:223
+            st.thresholds = (hi_t, lo_t)
+            try:
+                edges, width = hist_edges(st.min, st.max, bins)    # describe.py:226 -> :40-45
+            except IndexError as e:
+                st.error = e
+                stats[i] = st
+                continue
+            st.edges, st.width = edges, width
+            p2_items.append((col, st.mean, edges, hi_t, lo_t))
+            p2_idx.append(i)
+            stats[i] = st
+        for i, r2 in zip(p2_idx, self.pass2_batch(p2_items)):
+            st = stats[i]
+            st.mad = r2['abs_dev_sum']
+            st.hist_counts = r2['hist']
+            st.high_idx = r2['n_high']
+            st.low_idx = r2['n_low']
+        return stats
 
     def numeric_pass1(self, col, probs=PROBS):
         plan_dev, plan = self.plan(col, probs)
