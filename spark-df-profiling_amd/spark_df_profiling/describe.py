@@ -95,6 +95,15 @@ def _value_counts_first(engine, col, k):
     return _series(engine.first_rows(col, k), col).value_counts()
 
 
+def _distinct_hint(p1, spark_t):
+    """Upper bound of a NUM column's distinct count from pass 1: the valid
+    rows, or the integral value range."""
+    hint = p1['n_valid']
+    if spark_t in INT_TYPES and p1['count']:
+        hint = min(hint, p1['imax'] - p1['imin'] + 1 + (p1['n_valid'] - p1['count']))
+    return hint
+
+
 def _distinct_count(engine, col, p1, hint):
     """countDistinct (describe.py:143) of a NUM/DATE column: a value bitmap when
     the integral range from pass 1 is small, else exact hash grouping."""
@@ -119,10 +128,9 @@ def describe_1d(engine: Engine, col: DeviceColumn, nrows, bins, k, freq, bundle)
         p1_pack = bundle.pop('p1_pack', None) or engine.numeric_pass1(col)
         p1 = p1_pack[0]
         count = p1['count']
-        hint = p1['n_valid']
-        if spark_t in INT_TYPES and p1['count']:
-            hint = min(hint, p1['imax'] - p1['imin'] + 1 + (p1['n_valid'] - p1['count']))
-        distinct = _distinct_count(engine, col, p1, hint)
+        distinct = bundle.pop('distinct_pre', None)
+        if distinct is None:
+            distinct = _distinct_count(engine, col, p1, _distinct_hint(p1, spark_t))
     elif spark_t in DATE_TYPES:
         p1 = engine.minmax_pass(col)
         bundle['minmax'] = p1
@@ -314,6 +322,13 @@ def describe(df, bins=10, corr_reject=0.9, **kwargs):
                 # column that turns out CONST (one distinct value) is never NUM
                 if plots and st.error is None and owner[col.name] == rank and not _const_numeric(st):
                     early_plots[col.name] = _submit_plot(st)
+        if world == 1:
+            # every NUM column's countDistinct with shared readbacks
+            p1s = [pk[0] for pk in packs]
+            hints = [_distinct_hint(p1, c.spark_type) for c, p1 in zip(num_cols, p1s)]
+            bounds = [(p1['imin'], p1['imax']) if p1['count'] else None for p1 in p1s]
+            for col, d in zip(num_cols, engine.distinct_batch(num_cols, hints, bounds)):
+                bundles[col.name]['distinct_pre'] = d
     if workers > 1:
         done = _describe_concurrent(engine, table.columns, one, workers)
     else:

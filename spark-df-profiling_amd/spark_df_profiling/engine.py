@@ -922,7 +922,45 @@ class Engine:
         offsets (sdp_part.hip).  Returns a tab dict (dense (key, count) group
         arrays when counts are needed), or None when the column needs the exact
         global-table path (64-bit hash collision between different strings, or
-        a final bucket larger than its LDS table)."""
+        a final bucket larger than its LDS table).  Two host readbacks: the
+        level-1 bucket starts, then the group statistics."""
+        ctx = self._group_begin(col, with_counts)
+        if ctx is None:
+            return None
+        self._group_middle(ctx, ctx['bsn_dev'].cpu().numpy().astype(np.int64))
+        return self._group_end(ctx, self._host_u64(ctx['stats_dev']), dense)
+
+    def group_batch(self, cols):
+        """group(col, with_counts=False, dense=False) -- countDistinct
+        (describe.py:143) -- of several columns with two host readbacks in
+        all: every column's level-1 count, one readback of every bucket-start
+        array, every column's scatters and de-duplication queued back to back
+        (record buffers recycled on the stream between columns), one readback
+        of every column's group statistics.  None where group() returns None."""
+        ctxs = [self._group_begin(c, False) for c in cols]
+        live = [c for c in ctxs if c is not None]
+        if not live:
+            return [None] * len(cols)
+        flat = torch.cat([c['bsn_dev'] for c in live]).cpu().numpy().astype(np.int64)
+        off = 0
+        for c in live:
+            m = c['bsn_dev'].numel()
+            self._group_middle(c, flat[off:off + m])
+            off += m
+        sizes = [c['stats_dev'].numel() for c in live]
+        allst = self._host_u64(torch.cat([c['stats_dev'] for c in live]))
+        out, off, it = [], 0, iter(zip(live, sizes))
+        for c in ctxs:
+            if c is None:
+                out.append(None)
+                continue
+            ctx, m = next(it)
+            out.append(self._group_end(ctx, allst[off:off + m], False))
+            off += m
+        return out
+
+    def _group_begin(self, col, with_counts):
+        """Level-1 bucket counts of `col` and their scan (no readback)."""
         isb = col.kind == 'bytes'
         with_counts = with_counts or isb
         n = col.length
@@ -942,22 +980,38 @@ class Engine:
         stats = self._u64(68, zero=True)
         cs = None if isb else col.sdp()
         bc = col.sdp_bytes() if isb else None
-        cref = None if isb else ctypes.byref(cs)
-        bref = ctypes.byref(bc) if isb else None
         hv = self._heavy_keys(col, isb)
-        hvref = ctypes.byref(hv['struct']) if hv else None
         hcnt = self._u64(max(hv['n'] if hv else 1, 1), zero=True)
-        # level 1: rows -> nb1 buckets
         rpb = sdp.sdp_part_rows_per_block(n, int(isb))
         grid = max(1, -(-n // rpb))
         h1 = torch.empty(nb1 * grid, dtype=torch.int32, device=self.device)
-        rb = col_read_bytes(col)
-        recw = 24 if isb else 8
-        nat.annotate(_label(col, 'count'), rb)
-        sdp.sdp_part_rows(cref, bref, hvref, b1, 0, ptr(h1), None, None, ptr(hcnt), ptr(stats), s)
+        ctx = {'col': col, 'isb': isb, 'with_counts': with_counts, 'large': large, 'b1': b1, 'b2': b2,
+               'nb1': nb1, 'nb2': nb2, 'stats': stats, 'cs': cs, 'bc': bc, 'hv': hv, 'hcnt': hcnt, 'grid': grid,
+               'rb': col_read_bytes(col), 'recw': 24 if isb else 8}
+        nat.annotate(_label(col, 'count'), ctx['rb'])
+        sdp.sdp_part_rows(self._gref(ctx), ctypes.byref(bc) if isb else None,
+                          ctypes.byref(hv['struct']) if hv else None, b1, 0, ptr(h1), None, None, ptr(hcnt),
+                          ptr(stats), s)
         o1 = self._scan(h1)
-        # record count and L1 bucket starts in one readback
-        bsn = torch.cat([o1[0:nb1 * grid:grid], o1[-1:]]).cpu().numpy().astype(np.int64)
+        ctx['o1'] = o1
+        ctx['bsn_dev'] = torch.cat([o1[0:nb1 * grid:grid], o1[-1:]])     # record count + L1 bucket starts
+        return ctx
+
+    @staticmethod
+    def _gref(ctx):
+        return None if ctx['isb'] else ctypes.byref(ctx['cs'])
+
+    def _group_middle(self, ctx, bsn):
+        """Level-1 scatter, level-2 count/scan/scatter and the LDS
+        de-duplication, all queued; `bsn` = the host copy of bsn_dev."""
+        s = self._s()
+        isb, with_counts, large = ctx['isb'], ctx['with_counts'], ctx['large']
+        b1, b2, nb1, nb2, grid = ctx['b1'], ctx['b2'], ctx['nb1'], ctx['nb2'], ctx['grid']
+        col, hv, hcnt, stats, o1 = ctx['col'], ctx['hv'], ctx['hcnt'], ctx['stats'], ctx['o1']
+        rb, recw = ctx['rb'], ctx['recw']
+        cref = self._gref(ctx)
+        bref = ctypes.byref(ctx['bc']) if isb else None
+        hvref = ctypes.byref(hv['struct']) if hv else None
         nrec = int(bsn[-1])
         r1, keep1 = self._records(nrec, isb)
         if nrec:
@@ -1005,7 +1059,15 @@ class Engine:
             sdp.sdp_part_dedup(ctypes.byref(rf), int(isb), bref, ptr(starts), nfinal,
                                int(with_counts) | (2 if large else 0) | direct,
                                ptr(out_key), ptr(out_cnt), ptr(ngroups), ptr(stats), s)
-        both = self._host_u64(torch.cat([stats, hcnt[:hv['n']]]) if hv else stats)   # one readback
+        del keepf, rf
+        ctx.update({'starts': starts, 'ngroups': ngroups, 'out_key': out_key, 'out_cnt': out_cnt, 'nfinal': nfinal})
+        del ctx['o1'], ctx['bsn_dev']
+        ctx['stats_dev'] = torch.cat([stats, hcnt[:hv['n']]]) if hv else stats
+
+    def _group_end(self, ctx, both, dense):
+        """The tab dict from the host copy of stats_dev (see group)."""
+        s = self._s()
+        isb, with_counts, col, hv = ctx['isb'], ctx['with_counts'], ctx['col'], ctx['hv']
         st, hc = both[:68], both[68:]
         if st[2] or st[3]:
             return None
@@ -1016,12 +1078,13 @@ class Engine:
         tab = {'bytes': isb, 'dense': True, 'rows': st[0], 'max_key_rows': 0, 'col': col,
                'groups': total, 'groups_local': total}
         if dense and with_counts:
+            starts, ngroups, nfinal = ctx['starts'], ctx['ngroups'], ctx['nfinal']
             keys = self._u64(max(total, 1))
             counts = self._u64(max(total, 1))
             if groups_local:
                 offs = self._scan(ngroups)
-                sdp.sdp_part_compact(ptr(out_key), ptr(out_cnt), ptr(starts), ptr(ngroups), ptr(offs), nfinal,
-                                     ptr(keys), ptr(counts), s)
+                sdp.sdp_part_compact(ptr(ctx['out_key']), ptr(ctx['out_cnt']), ptr(starts), ptr(ngroups), ptr(offs),
+                                     nfinal, ptr(keys), ptr(counts), s)
             extra_k, extra_c = [], []
             if hv:
                 hh = self._host_u64(hv['h'])
@@ -1042,6 +1105,34 @@ class Engine:
                 counts[groups_local:groups_local + m] = torch.tensor(extra_c, dtype=torch.int64, device=self.device)
             tab.update({'slots': keys, 'counts': counts, 'capacity': max(total, 1)})
         return tab
+
+    def distinct_batch(self, cols, hints, bounds):
+        """countDistinct of several NUM/DATE columns (describe.py:143) with
+        the path choice of describe._distinct_count / distinct_fixed per column
+        and the host readbacks shared: LDS bitmaps for small integral ranges
+        (one readback for all), hash partitioning for the rest (group_batch).
+        `bounds[i]` = (imin, imax) for integral columns with values, else None.
+        Single rank only; returns [distinct count]."""
+        out = [None] * len(cols)
+        bm, grp = [], []
+        for i, (col, hint, bd) in enumerate(zip(cols, hints, bounds)):
+            if (bd is not None and col.kind == 'fixed' and col.dtype in self.BITMAP_DTYPES
+                    and bd[1] - bd[0] + 1 <= nat.BITMAP_MAX_BITS):
+                bm.append(i)
+            elif hint * 4 > max(col.length, 1) and col.length >= (1 << 16):
+                grp.append(i)
+        if bm:
+            outs = [self._distinct_bitmap_launch(cols[i], bounds[i][0], bounds[i][1] - bounds[i][0] + 1) for i in bm]
+            for i, v in zip(bm, self._host_u64(torch.cat(outs))):
+                out[i] = int(v)
+        if grp:
+            for i, tab in zip(grp, self.group_batch([cols[i] for i in grp])):
+                if tab is not None:
+                    out[i] = tab['groups']
+        for i, col in enumerate(cols):                  # global-table path / fallbacks
+            if out[i] is None:
+                out[i] = self.distinct_fixed(col, with_counts=False, capacity_hint=hints[i])['groups']
+        return out
 
     def group_sharded(self, col):
         """countDistinct (describe.py:143) of a fixed-width column of a
@@ -1154,10 +1245,7 @@ class Engine:
 
     BITMAP_DTYPES = (nat.I8, nat.I16, nat.I32, nat.I64, nat.U8, nat.U16, nat.U32)
 
-    def distinct_bitmap(self, col, lo, range_):
-        """countDistinct (describe.py:143) of an integral column whose values lie
-        in [lo, lo + range_), range_ <= 2^20: LDS bitmaps (sdp_bitmap.hip).  Ranks
-        all-gather their OR-ed bitmaps and re-reduce them."""
+    def _distinct_bitmap_launch(self, col, lo, range_, keep_bitmap=False):
         nw = (range_ + 31) // 32
         work = self._bytes(sdp.sdp_bitmap_workspace_bytes(col.length, range_))
         bm = torch.zeros(nw, dtype=torch.int32, device=self.device)      # (an empty shard writes nothing)
@@ -1166,6 +1254,13 @@ class Engine:
         nat.annotate(_label(col), col_read_bytes(col))
         sdp.sdp_distinct_bitmap(ctypes.byref(cs), int(lo), int(range_), ptr(work), work.numel(), ptr(bm), ptr(out),
                                 self._s())
+        return (out, bm, nw) if keep_bitmap else out
+
+    def distinct_bitmap(self, col, lo, range_):
+        """countDistinct (describe.py:143) of an integral column whose values lie
+        in [lo, lo + range_), range_ <= 2^20: LDS bitmaps (sdp_bitmap.hip).  Ranks
+        all-gather their OR-ed bitmaps and re-reduce them."""
+        out, bm, nw = self._distinct_bitmap_launch(col, lo, range_, keep_bitmap=True)
         if self.comm.world > 1:
             allb = torch.cat(self.comm.allgather(bm))
             out.zero_()
