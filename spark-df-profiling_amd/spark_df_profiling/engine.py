@@ -888,27 +888,35 @@ class Engine:
             sdp.sdp_part_sample(ctypes.byref(col.sdp()), None, ns, ptr(h), None, s)
         if gather and self.comm.world > 1:
             h = torch.cat(self.comm.allgatherv(h))
-        hn = h.cpu().numpy().view(np.uint64)
+        meta = None
+        if isb and keep is not None:            # sample hashes and metas in one readback
+            both = torch.cat([h, keep[2][:ns]]).cpu().numpy().view(np.uint64)
+            hn, meta = both[:h.numel()], both[h.numel():]
+        else:
+            hn = h.cpu().numpy().view(np.uint64)
         pos = np.nonzero(hn != np.uint64(U64))[0]
         if isb and pos.size:
-            meta = keep[2].cpu().numpy().view(np.uint64)
             pos = pos[(meta[pos] >> np.uint64(40)) <= np.uint64(16)]
         if pos.size == 0:
             return None
         u, first, cnt = np.unique(hn[pos], return_index=True, return_counts=True)
-        return self._heavy_struct(u, cnt, first, pos, keep, isb)
+        return self._heavy_struct(u, cnt, first, pos, keep, isb, meta)
 
-    def _heavy_struct(self, u, cnt, first=None, pos=None, keep=None, isb=False):
+    def _heavy_struct(self, u, cnt, first=None, pos=None, keep=None, isb=False, meta=None):
         """Heavy keys (>= HEAVY_MIN sample occurrences, at most HEAVY_MAX by
-        count) from the sample's distinct hashes u (ascending) and counts."""
+        count) from the sample's distinct hashes u (ascending) and counts.
+        Host copies of the hashes (and byte-key metas) stay in the dict, so the
+        group assembly needs no readback of them."""
         sel = np.nonzero(cnt >= HEAVY_MIN)[0]
         if sel.size == 0:
             return None
         if sel.size > nat.HEAVY_MAX:
             sel = sel[np.argsort(-cnt[sel], kind='stable')[:nat.HEAVY_MAX]]
-        hv = {'h': self._h2d(u[sel].view(np.int64).copy()), 'n': int(sel.size)}
+        hv = {'h': self._h2d(u[sel].view(np.int64).copy()), 'n': int(sel.size),
+              'h_host': [int(x) for x in u[sel].tolist()]}
         if isb:
             rows = pos[first[sel]]
+            hv['meta_host'] = [int(x) for x in meta[rows].tolist()]
             idx = self._h2d(rows.astype(np.int64))
             hv['k0'], hv['k1'], hv['meta'] = keep[0][idx].contiguous(), keep[1][idx].contiguous(), \
                 keep[2][idx].contiguous()
@@ -1087,8 +1095,8 @@ class Engine:
                                      nfinal, ptr(keys), ptr(counts), s)
             extra_k, extra_c = [], []
             if hv:
-                hh = self._host_u64(hv['h'])
-                meta = self._host_u64(hv['meta']) if isb else None
+                hh = hv['h_host']
+                meta = hv['meta_host'] if isb else None
                 for i in heavy_sel:
                     if isb:
                         extra_k.append(((hh[i] >> 40) << 40) | (meta[i] & ((1 << 40) - 1)))
@@ -1352,9 +1360,16 @@ class Engine:
 
         def sort_take(sel, n_dev, take):
             sdp.sdp_sort_groups(ptr(sel), ptr(n_dev), ptr(slots), ptr(counts), bref, s)
-            m = min(int(n_dev.item()), take)
-            idx = self._host_u64(sel[:m]) if m else []
-            cnt = self._host_u64(counts[sel[:m]]) if m else []
+            # count, slot indices, counts and slot values in ONE readback
+            # (indices past the count are masked to slot 0 before the gathers)
+            t = max(1, min(take, sel.numel()))
+            live = torch.arange(t, device=self.device) < n_dev[0]
+            idx_d = torch.where(live, sel[:t], torch.zeros_like(sel[:t]))
+            got = self._host_u64(torch.cat([n_dev[:1], idx_d, counts[idx_d], slots[idx_d]]))
+            m = min(got[0], take)
+            idx, cnt, val = got[1:1 + m], got[1 + t:1 + t + m], got[1 + 2 * t:1 + 2 * t + m]
+            cache = tab.setdefault('_slotval', {})
+            cache.update(zip(idx, val))
             return list(zip(idx, cnt))
 
         extra = []
@@ -1463,18 +1478,16 @@ class Engine:
 
     def group_values(self, tab, slot_list, col: DeviceColumn):
         """Host values of the groups at `slot_list` (None = the EMPTY64 key)."""
+        cache = tab.get('_slotval', {})
+        need = [sl for sl in slot_list if sl is not None and sl not in cache]
+        if need:
+            idx = torch.tensor(need, dtype=torch.int64, device=self.device)
+            cache = dict(cache)
+            cache.update(zip(need, self._host_u64(tab['slots'][idx])))
         if not tab['bytes']:
-            keys = []
-            if any(s is not None for s in slot_list):
-                idx = torch.tensor([s for s in slot_list if s is not None], dtype=torch.int64, device=self.device)
-                keys = self._host_u64(tab['slots'][idx])
-            it = iter(keys)
-            return [fixed_key_to_value(EMPTY64 if s is None else next(it), col) for s in slot_list]
+            return [fixed_key_to_value(EMPTY64 if sl is None else cache[sl], col) for sl in slot_list]
         src = tab.get('src_col', col)
-        rows = []
-        if slot_list:
-            idx = torch.tensor(slot_list, dtype=torch.int64, device=self.device)
-            rows = [(x & ((1 << 40) - 1)) - 1 for x in self._host_u64(tab['slots'][idx])]
+        rows = [(cache[sl] & ((1 << 40) - 1)) - 1 for sl in slot_list]
         return self.row_bytes_values(src, rows, col)
 
     # -- first rows (limit(1) / limit(50)) ----------------------------------------
@@ -1533,9 +1546,9 @@ class Engine:
             ends = [s + w for s in starts]
         else:
             ri = torch.tensor(rows, dtype=torch.int64, device=self.device)
-            o = src.offsets.to(torch.int64)
-            starts = o[ri].cpu().tolist()
-            ends = o[ri + 1].cpu().tolist()
+            o = src.offsets
+            se = torch.cat([o[ri], o[ri + 1]]).to(torch.int64).cpu().tolist()    # one readback
+            starts, ends = se[:len(rows)], se[len(rows):]
         pos = np.concatenate([np.arange(a, b, dtype=np.int64) for a, b in zip(starts, ends)]) if rows else []
         flat = src.data[torch.from_numpy(pos).to(self.device)].cpu().numpy().tobytes() if len(pos) else b''
         out = []
@@ -1590,7 +1603,8 @@ def _merge_special(res, extra, k, tab):
 
 
 def _slot_key_for_sort(tab, slot):
-    return _u(tab['slots'][slot].item())
+    cached = tab.get('_slotval', {}).get(slot)
+    return _u(cached) if cached is not None else _u(tab['slots'][slot].item())
 
 
 def merge_pass1_results(parts):
