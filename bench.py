@@ -257,14 +257,14 @@ def label_kernels(label):
     if name in ('sdp_pass1', 'sdp_pass2'):
         return ['sdp::%s_kernel<%s' % (name[4:], _DT.get(dt, dt))]
     if name == 'sdp_gram':
-        return ['sdp::gram_kernel<']
+        return ['sdp::gram_kernel<', 'sdp::gram_wide_kernel', 'sdp::gram_reduce_kernel']
     return []
 
 
 # PMC traffic summary the bench reads `roofline.traffic` from, chosen by name
 # (never by file mtime, which a git checkout scrambles): the newest committed
 # summary of the default workload (tools/gpu_traffic.sh -> tools/traffic_summary.py).
-TRAFFIC_SUMMARY = {'c3': 'profiles/r01_bench1g_final_traffic.json', 'c5': None}
+TRAFFIC_SUMMARY = {'c3': 'profiles/r02a_c3_traffic.json', 'c5': 'profiles/r02a_c5_traffic.json'}
 
 
 def pmc_traffic(label, path):
@@ -367,7 +367,7 @@ def cpu_baseline(sample_rows, device):
                       'no pyspark/JVM in the image), %.1f s' % (sample_rows, workers, dt)}
 
 
-def gram_roofline(rec, steps, ncols, n_rows):
+def gram_roofline(rec, steps, ncols, n_rows, traffic_path=None):
     """C5: the Pearson Gram on the fp64 matrix cores.  F_alg = n C (C + 1)
     flop per launch (symmetric X^T X, one multiply-add per
     unique entry) over the launch's average HIP-event duration."""
@@ -379,9 +379,12 @@ def gram_roofline(rec, steps, ncols, n_rows):
     flop = float(n_rows) * ncols * (ncols + 1)
     tfs = flop / (ms * 1e-3) / 1e12
     alg_bytes = sum(x for _, _, x in ev if x is not None) / len(ev)
+    traffic, tsrc = pmc_traffic('sdp_gram', traffic_path)
     return {'bound': 'mfma', 'kernel': 'sdp_gram (gram_wide_kernel + gram_reduce_kernel<128>, v_mfma_f64_16x16x4f64)',
             'achieved': round(tfs, 2), 'peak': FP64_MFMA_PEAK_TFS, 'unit': 'TFLOP/s',
-            'frac': round(tfs / FP64_MFMA_PEAK_TFS, 4), 'traffic': None,
+            'frac': round(tfs / FP64_MFMA_PEAK_TFS, 4),
+            'traffic': int(traffic) if traffic is not None else None,
+            'traffic_unit': 'HBM bytes per launch (PMC FETCH_SIZE x2 + WRITE_SIZE)', 'traffic_source': tsrc,
             'flop_per_launch': flop, 'avg_launch_ms': round(ms, 4), 'launches_per_step': len(ev) // steps,
             'hbm_alg_bytes_per_launch': int(alg_bytes),
             'hbm_achieved_gbs': round(alg_bytes / (ms * 1e-3) / 1e9, 1)}
@@ -484,7 +487,7 @@ def main():
     ncols = len(table.columns)
     if args.workload == 'c5':
         hbm_rl = rl
-        rl = gram_roofline(rec, args.steps, ncols, table.num_rows)
+        rl = gram_roofline(rec, args.steps, ncols, table.num_rows, traffic_path)
         rl['hbm_dominant'] = {k: hbm_rl[k] for k in ('kernel', 'achieved', 'frac', 'avg_launch_ms')}
         rl['whole_profile'] = hbm_rl['whole_profile']
 
