@@ -282,7 +282,8 @@ def pmc_traffic(label, path):
     hits = [v for k, v in summ['kernels'].items() if any(k.startswith(p) for p in pre)]
     if not hits:
         return None, None
-    n = sum(v['dispatches'] for v in hits)
+    # one entry-point launch runs each matching kernel once (e.g. gram + reduce)
+    n = max(v['dispatches'] for v in hits)
     return sum(v['traffic_bytes'] * v['dispatches'] for v in hits) / n, path
 
 
