@@ -254,7 +254,7 @@ def label_kernels(label):
         return ['sdp::part_%s_rows_u64_kernel<%s>' % (st, _DT.get(dt, dt))]
     if name == 'sdp_part_dedup':
         return ['sdp::part_dedup_bytes_kernel'] if dt == 'bytes' else ['sdp::part_dedup_u64']
-    if name in ('sdp_pass1', 'sdp_pass2'):
+    if name in ('sdp_pass1', 'sdp_pass2', 'sdp_pass2_count'):
         return ['sdp::%s_kernel<%s' % (name[4:], _DT.get(dt, dt))]
     if name == 'sdp_gram':
         return ['sdp::gram_kernel<', 'sdp::gram_wide_kernel', 'sdp::gram_reduce_kernel']

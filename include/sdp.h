@@ -353,6 +353,17 @@ typedef struct sdp_chunk {
     int64_t start, end, hbase, hstride;
 } sdp_chunk;
 
+/* sdp_pass2 fused with sdp_part_rows phase 0 (the level-1 count of the
+ * column's distinct-count partitioning, describe.py:143): the same pass-2
+ * outputs, plus d_part_hist / d_heavy_counts / d_stats exactly as
+ * sdp_part_rows(col, NULL, heavy, b1, 0, ...) writes them -- one read of the
+ * column instead of two.  Workspace: sdp_pass2_count_workspace_bytes. */
+int64_t sdp_pass2_count_workspace_bytes(int64_t length, int32_t bins);
+int sdp_pass2_count(const sdp_column *col, double mean, const double *d_edges, int32_t bins,
+                    int32_t edges_monotone, double hi_t, double lo_t, void *d_work, int64_t work_bytes,
+                    sdp_pass2_result *d_result, uint64_t *d_hist, const sdp_heavy *heavy, int32_t b1,
+                    uint32_t *d_part_hist, uint64_t *d_heavy_counts, uint64_t *d_stats, void *stream);
+
 /* Rows per partition workgroup (grid = ceil(length / this)). */
 int64_t sdp_part_rows_per_block(int64_t length, int32_t is_bytes);
 /* Mean records per final bucket the dedup tables are sized for. */

@@ -614,12 +614,28 @@ __global__ void __launch_bounds__(GW_BLOCK, 2) gram_wide_kernel(const GramCol *c
     __shared__ double pb[2][GW_TILE * GW_PITCH];
     __shared__ int s_unit;
     const int U = S * T;
+    // XCD-affine: workgroup b runs on XCD b % 8 (the usual round-robin; for
+    // speed only -- any placement is correct) and first drains that XCD's
+    // contiguous eighth of the chunk-major units, so the tiles of one row chunk
+    // share the XCD's L2; then it helps the other XCDs' ranges.
+    const int x0 = (int)(blockIdx.x & 7);
+    int d = 0;
     for (;;) {
-        if (threadIdx.x == 0) s_unit = (int)atomicAdd(next_unit, 1u);
+        if (threadIdx.x == 0) {
+            int L = -1;
+            while (d < 8) {
+                const int x = (x0 + d) & 7;
+                const int lo = (int)((int64_t)U * x / 8), hi = (int)((int64_t)U * (x + 1) / 8);
+                const int u = lo + (int)atomicAdd(&next_unit[16 * x], 1u);
+                if (u < hi) { L = u; break; }
+                ++d;                                   // this range is drained (counters only grow)
+            }
+            s_unit = L;
+        }
         __syncthreads();
         const int L = s_unit;
         __syncthreads();                           // everyone has read s_unit before it is rewritten
-        if (L >= U) return;
+        if (L < 0) return;
         int ti = 0, rem = L % T;                   // diagonal tiles take their own instantiation
         while (rem >= side - ti) { rem -= side - ti; ++ti; }
         const int tj = ti + rem;
@@ -774,7 +790,7 @@ extern "C" int64_t sdp_gram_workspace_bytes(int64_t length, int32_t ncols) {
     b += align256((int64_t)g.S * g.side * g.tile * sizeof(double));
     b += align256((int64_t)g.S * sizeof(double));
     b += align256((int64_t)ncols * sizeof(MaskCol));
-    b += 256;                                       // wide kernel's unit counter
+    b += 512;                                       // wide kernel's per-XCD unit counters
     return b;
 }
 
@@ -831,9 +847,9 @@ extern "C" int sdp_gram(const sdp_column *cols, int32_t ncols, const uint32_t *d
     free(h);
     if (e != hipSuccess) return set_error(SDP_EHIP, "sdp_gram: %s", hipGetErrorString(e));
     if (g.tile == GW_TILE) {
-        // unit counter: the last 256 bytes of the workspace
-        unsigned int *ctr = (unsigned int *)((char *)d_work + sdp_gram_workspace_bytes(n, ncols) - 256);
-        hipError_t me = hipMemsetAsync(ctr, 0, sizeof(unsigned int), s);
+        // per-XCD unit counters (64 B apart): the last 512 bytes of the workspace
+        unsigned int *ctr = (unsigned int *)((char *)d_work + sdp_gram_workspace_bytes(n, ncols) - 512);
+        hipError_t me = hipMemsetAsync(ctr, 0, 512, s);
         if (me != hipSuccess) return set_error(SDP_EHIP, "sdp_gram: %s", hipGetErrorString(me));
         int dev = 0, cus = 256;
         if (hipGetDevice(&dev) == hipSuccess && hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) cus = 256;

@@ -1,0 +1,126 @@
+// sdp_heavy.h -- heavy-key LDS tables and the fixed-width grouping key, shared by
+// the partitioning kernels (sdp_part.hip) and the fused pass-2 + level-1 count
+// kernel (sdp_numeric.hip).  Keys seen >= HEAVY_MIN times in the pre-pass
+// sample are counted in an LDS table and never become partition records, so
+// skewed columns (describe.py:251's hot groups) cannot pile into one bucket.
+#pragma once
+#include "sdp_common.h"
+
+namespace sdp {
+
+constexpr int MAXB = 1024;              // buckets per level (b <= 10)
+constexpr int HEAVY_MAX = 256;
+constexpr int HEAVY_SLOTS = 1024;       // open-addressing slots (load <= 1/4)
+constexpr int HEAVY_FILTER = 16384;     // filter bits: most non-heavy rows need one LDS read
+constexpr int SHORT_MAX = 16;
+
+// ---- heavy keys ---------------------------------------------------------------
+struct HeavyArg {
+    const uint64_t *h;      // [n] hashes (fixed: h = mix64(key))
+    const uint64_t *k0;     // bytes only
+    const uint64_t *k1;
+    const uint64_t *meta;
+    int32_t n;
+};
+// (byte keys also keep each heavy key's first 16 bytes and length)
+template <bool BYTES>
+struct HeavyLdsT {
+    uint64_t h[HEAVY_SLOTS];
+    uint32_t filter[HEAVY_FILTER / 32];
+    int16_t idx[HEAVY_SLOTS];
+    uint32_t cnt[HEAVY_MAX];
+    uint64_t k0[BYTES ? HEAVY_MAX : 1];
+    uint64_t k1[BYTES ? HEAVY_MAX : 1];
+    uint32_t len[BYTES ? HEAVY_MAX : 1];
+};
+// filter bit of a hash: bits 20..33 (the slot uses the low bits, buckets the top)
+__device__ __forceinline__ uint32_t heavy_filter_bit(uint64_t h) { return (uint32_t)(h >> 20) & (HEAVY_FILTER - 1); }
+template <bool BYTES>
+__device__ __forceinline__ bool heavy_maybe(const HeavyLdsT<BYTES> &s, uint64_t h) {
+    const uint32_t fb = heavy_filter_bit(h);
+    return (s.filter[fb >> 5] >> (fb & 31)) & 1u;
+}
+template <bool BYTES>
+__device__ void heavy_build(HeavyLdsT<BYTES> &s, const HeavyArg &a) {
+    for (int i = threadIdx.x; i < HEAVY_SLOTS; i += blockDim.x) s.h[i] = EMPTY64;
+    for (int i = threadIdx.x; i < HEAVY_MAX; i += blockDim.x) s.cnt[i] = 0;
+    for (int i = threadIdx.x; i < HEAVY_FILTER / 32; i += blockDim.x) s.filter[i] = 0;
+    lds_barrier();
+    for (int i = threadIdx.x; i < a.n; i += blockDim.x) {
+        const uint64_t h = a.h[i];
+        const uint32_t fb = heavy_filter_bit(h);
+        atomicOr(&s.filter[fb >> 5], 1u << (fb & 31));
+        uint32_t pos = (uint32_t)h & (HEAVY_SLOTS - 1);
+        while (true) {
+            const uint64_t old = atomicCAS((unsigned long long *)&s.h[pos], (unsigned long long)EMPTY64,
+                                           (unsigned long long)h);
+            if (old == EMPTY64) { s.idx[pos] = (int16_t)i; break; }
+            pos = (pos + 1) & (HEAVY_SLOTS - 1);
+        }
+        if constexpr (BYTES) {
+            s.k0[i] = a.k0[i];
+            s.k1[i] = a.k1[i];
+            s.len[i] = (uint32_t)(a.meta[i] >> 40);
+        }
+    }
+    lds_barrier();
+}
+// index of the heavy key equal to this row, or -1
+__device__ __forceinline__ int heavy_find_u64(const HeavyLdsT<false> &s, int n, uint64_t h) {
+    if (n == 0 || h == EMPTY64 || !heavy_maybe(s, h)) return -1;
+    uint32_t pos = (uint32_t)h & (HEAVY_SLOTS - 1);
+    while (true) {
+        const uint64_t v = s.h[pos];
+        if (v == h) return s.idx[pos];
+        if (v == EMPTY64) return -1;
+        pos = (pos + 1) & (HEAVY_SLOTS - 1);
+    }
+}
+__device__ __forceinline__ int heavy_find_bytes(const HeavyLdsT<true> &s, int n, uint64_t h, uint64_t k0, uint64_t k1,
+                                                uint32_t len) {
+    if (n == 0 || len > SHORT_MAX || h == EMPTY64 || !heavy_maybe(s, h)) return -1;
+    uint32_t pos = (uint32_t)h & (HEAVY_SLOTS - 1);
+    while (true) {
+        const uint64_t v = s.h[pos];
+        if (v == EMPTY64) return -1;
+        if (v == h) {
+            const int i = s.idx[pos];
+            if (s.k0[i] == k0 && s.k1[i] == k1 && s.len[i] == len) return i;
+        }
+        pos = (pos + 1) & (HEAVY_SLOTS - 1);
+    }
+}
+// one device atomic per workgroup (not per wave) for a block total
+__device__ void block_add_u64(uint64_t v, uint64_t *dst) {
+    __shared__ uint64_t s_part[1024 / WAVE];
+    lds_barrier();                      // a previous call's reads of s_part are done
+    v = wave_sum_u64(v);
+    if (lane_id() == 0) s_part[threadIdx.x / WAVE] = v;
+    lds_barrier();
+    if (threadIdx.x == 0) {
+        uint64_t tot = 0;
+        for (int w = 0; w < (int)(blockDim.x / WAVE); ++w) tot += s_part[w];
+        if (tot) atomicAdd((unsigned long long *)dst, (unsigned long long)tot);
+    }
+}
+template <bool BYTES>
+__device__ void heavy_flush(HeavyLdsT<BYTES> &s, int n, uint64_t *counts) {
+    lds_barrier();
+    for (int i = threadIdx.x; i < n; i += blockDim.x)
+        if (s.cnt[i]) atomicAdd((unsigned long long *)&counts[i], (unsigned long long)s.cnt[i]);
+}
+
+// ---- grouping key of a fixed-width element (order-preserving u64) ----------
+template <typename T> __device__ __forceinline__ uint64_t key_of(T v);
+template <> __device__ __forceinline__ uint64_t key_of<double>(double v) { return f64_key(v); }
+template <> __device__ __forceinline__ uint64_t key_of<float>(float v) { return f64_key((double)v); }
+template <> __device__ __forceinline__ uint64_t key_of<int64_t>(int64_t v) { return i64_key(v); }
+template <> __device__ __forceinline__ uint64_t key_of<int32_t>(int32_t v) { return i64_key(v); }
+template <> __device__ __forceinline__ uint64_t key_of<int16_t>(int16_t v) { return i64_key(v); }
+template <> __device__ __forceinline__ uint64_t key_of<int8_t>(int8_t v) { return i64_key(v); }
+template <> __device__ __forceinline__ uint64_t key_of<uint64_t>(uint64_t v) { return v; }
+template <> __device__ __forceinline__ uint64_t key_of<uint32_t>(uint32_t v) { return v; }
+template <> __device__ __forceinline__ uint64_t key_of<uint16_t>(uint16_t v) { return v; }
+template <> __device__ __forceinline__ uint64_t key_of<uint8_t>(uint8_t v) { return v; }
+
+}  // namespace sdp

@@ -11,7 +11,7 @@
 // All block partials are merged by a single-block kernel in block order, so
 // every result is deterministic for a given grid.
 #include <type_traits>
-#include "sdp_common.h"
+#include "sdp_heavy.h"
 
 namespace sdp {
 
@@ -184,6 +184,7 @@ struct P1Thread {
     int64_t isum, imin, imax;
     double dmin, dmax;
     double s1, s1c, s2, s3, s3c, s4;
+    double t1, t3;                    // plain sums of d and d^3 over the current tile
     uint32_t gt[SDP_MAX_WINDOWS], eqlo[SDP_MAX_WINDOWS], eqhi[SDP_MAX_WINDOWS];
     uint32_t wcur[SDP_MAX_WINDOWS];   // wave-uniform candidate cursors (wave-private slots)
 };
@@ -250,11 +251,14 @@ __device__ __forceinline__ void p1_elem(P1Thread &st, const P1Ctx &cx, T x, bool
             st.isum = (int64_t)((uint64_t)st.isum + (uint64_t)xi);
         }
         st.n_zero += (xd == 0.0);
+        // d and d^3 are summed plainly over the thread's tile (<= 16 terms) and
+        // folded into the compensated totals once per tile (p1_fold): the sum
+        // errs by <= ~3 eps * sum|d| instead of costing two TwoSums per element
         const double d = xd - cx.K;
         const double d2 = d * d;
-        two_sum_acc(st.s1, st.s1c, d);
+        st.t1 += d;
         st.s2 += d2;
-        two_sum_acc(st.s3, st.s3c, d2 * d);
+        st.t3 = fma(d2, d, st.t3);
         st.s4 = fma(d2, d2, st.s4);
     }
     if (!WIN) return;                   // no quantile windows (date/timestamp min/max)
@@ -279,6 +283,12 @@ __device__ __forceinline__ void p1_elem(P1Thread &st, const P1Ctx &cx, T x, bool
             st.wcur[w] = c + (uint32_t)__popcll(m);
         }
     }
+}
+
+__device__ __forceinline__ void p1_fold(P1Thread &st) {
+    two_sum_acc(st.s1, st.s1c, st.t1);
+    two_sum_acc(st.s3, st.s3c, st.t3);
+    st.t1 = st.t3 = 0.0;
 }
 
 template <typename T, bool WIN>
@@ -307,6 +317,7 @@ __global__ void __launch_bounds__(P1_BLOCK, 4) pass1_kernel(sdp_column col, cons
     st.dmin = __builtin_inf();
     st.dmax = -__builtin_inf();
     st.s1 = st.s1c = st.s2 = st.s3 = st.s3c = st.s4 = 0.0;
+    st.t1 = st.t3 = 0.0;
 #pragma unroll
     for (int w = 0; w < SDP_MAX_WINDOWS; ++w) st.gt[w] = st.eqlo[w] = st.eqhi[w] = st.wcur[w] = 0;
 
@@ -328,6 +339,7 @@ __global__ void __launch_bounds__(P1_BLOCK, 4) pass1_kernel(sdp_column col, cons
 #pragma unroll
             for (int e = 0; e < VPT; ++e) p1_elem<T, WIN>(st, cx, cur.v[u].v[e], (cur.vb[u] >> e) & 1u);
         }
+        p1_fold(st);
         if (more) cur = nxt;
     }
     // tail elements (n % VPT) by the first wave of block 0
@@ -337,6 +349,7 @@ __global__ void __launch_bounds__(P1_BLOCK, 4) pass1_kernel(sdp_column col, cons
         T x = inb ? ((const T *)col.d_values)[i] : (T)0;
         const bool valid = inb && valid_bit(col.d_validity, col.validity_bit_offset, i);
         p1_elem<T, WIN>(st, cx, x, valid);
+        p1_fold(st);
     }
 
     // ---- block reduction: waves, then LDS, fixed order ----------------------
@@ -1000,6 +1013,150 @@ __global__ void __launch_bounds__(P2_BLOCK, 4) pass2_kernel(sdp_column col, doub
         part_cnt[(int64_t)blockIdx.x * stride + 3 + i] = s_hist[i];
 }
 
+// ---- pass 2 fused with the level-1 partition count --------------------------
+// For a NUM column whose countDistinct (describe.py:143) takes the partitioning
+// path, pass 2 also does the level-1 count of sdp_part_rows (phase 0) on the
+// same read: block g streams rows [g * rpb, min(n, (g + 1) * rpb)) -- the row
+// ranges of the partition scatter, so its per-block bucket histogram is the
+// count kernel's -- doing pass 2's per-element work and, for every valid row,
+// hashing the grouping key and counting it into the heavy-key table or the LDS
+// bucket histogram.  One column read instead of two.
+struct P2CountLds {
+    HeavyLdsT<false> heavy;
+    uint32_t hist[MAXB];
+};
+
+template <typename T, bool SMALL, bool MONO, int NB = P2_SMALL_BINS>
+__global__ void __launch_bounds__(P2_BLOCK, 4) pass2_count_kernel(sdp_column col, double mean, const double *edges,
+                                                               int bins, int monotone, double hi_t, double lo_t,
+                                                               double *part_mad, uint64_t *part_cnt, HeavyArg heavy,
+                                                               int b1, int64_t rows_per_block, uint32_t *hist,
+                                                               uint64_t *heavy_counts, uint64_t *stats) {
+    constexpr int VPT = Vec16<T>::N;
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    __shared__ P2CountLds cl;
+    double *s_edges = (double *)smem;
+    uint32_t *s_hist = (uint32_t *)(smem + sizeof(double) * bins);
+    const int G = gridDim.x, g = blockIdx.x, t = threadIdx.x;
+    const int nb = 1 << b1;
+    const int shift = 64 - b1;
+    for (int i = t; i < bins; i += blockDim.x) { s_edges[i] = edges[i]; s_hist[i] = 0; }
+    for (int b = t; b < nb; b += P2_BLOCK) cl.hist[b] = 0;
+    heavy_build<false>(cl.heavy, heavy);               // (ends with a barrier)
+    P2Ctx c;
+    c.mean = mean; c.hi_t = hi_t; c.lo_t = lo_t; c.edges = s_edges; c.bins = bins;
+    c.monotone = monotone != 0;
+    c.e0 = s_edges[0];
+#pragma unroll
+    for (int j = 0; j < P2_SMALL_BINS; ++j) c.ev[j] = j < bins ? edges[j] : __builtin_inf();
+    {
+        const double w = (bins > 1) ? (s_edges[bins - 1] - s_edges[0]) / (double)(bins - 1) : 0.0;
+        c.inv_w = (w > 0.0) ? 1.0 / w : 0.0;
+    }
+    P2Thread st;
+    st.mad = 0.0; st.high = st.low = st.unbinned = st.okc = 0;
+#pragma unroll
+    for (int j = 0; j < P2_SMALL_BINS; ++j) st.bc[j] = 0;
+    uint64_t rows = 0, special = 0;
+    const bool any_heavy = heavy.n > 0;
+    auto count = [&](T x, bool valid) {
+        if (!valid) return;
+        ++rows;
+        const uint64_t h = mix64(key_of<T>(x));
+        const int hv = any_heavy ? heavy_find_u64(cl.heavy, heavy.n, h) : -1;
+        if (hv >= 0) atomicAdd(&cl.heavy.cnt[hv], 1u);
+        else if (h == EMPTY64) ++special;              // the key whose hash is the empty marker
+        else atomicAdd(&cl.hist[b1 ? (int)(h >> shift) : 0], 1u);
+    };
+
+    const int64_t n = col.length;
+    const int64_t r0 = (int64_t)g * rows_per_block;    // a multiple of 16 K rows: whole vectors
+    const int64_t r1 = min(n, r0 + rows_per_block);
+    const int64_t v0 = r0 / VPT, v1 = r1 / VPT;        // whole vectors of this block's rows
+    const Vec16<T> *vals = (const Vec16<T> *)col.d_values;
+    constexpr int U = sizeof(T) >= 8 ? P2_UNROLL : (std::is_same<T, float>::value ? P2_UNROLL / 2 : 1);
+    constexpr int64_t TV = (int64_t)P2_BLOCK * U;
+    Vec16<T> cv[U], nv[U];
+    uint32_t cb[U], nbits[U];
+    auto load = [&](int64_t vb, Vec16<T> (&v)[U], uint32_t (&b)[U]) {
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int64_t vi = vb + (int64_t)u * P2_BLOCK + t;
+            if (vi < v1) {
+                v[u] = vals[vi];
+                b[u] = valid_bits(col.d_validity, col.validity_bit_offset, vi * VPT, VPT);
+            } else {
+                b[u] = 0;
+#pragma unroll
+                for (int e = 0; e < VPT; ++e) v[u].v[e] = (T)0;
+            }
+        }
+    };
+    if (v0 < v1) load(v0, cv, cb);
+    for (int64_t vb = v0; vb < v1; vb += TV) {
+        const bool more = vb + TV < v1;
+        if (more) load(vb + TV, nv, nbits);            // next tile in flight
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+#pragma unroll
+            for (int e = 0; e < VPT; ++e) {
+                const bool valid = (cb[u] >> e) & 1u;
+                p2_elem<T, SMALL, MONO, NB>(st, c, s_hist, cv[u].v[e], valid);
+                count(cv[u].v[e], valid);
+            }
+        if (more) {
+#pragma unroll
+            for (int u = 0; u < U; ++u) { cv[u] = nv[u]; cb[u] = nbits[u]; }
+        }
+    }
+    if (r1 == n && t < WAVE) {                         // the column's last n % VPT rows (last block)
+        const int64_t i = v1 * VPT + t;
+        const bool inb = i < n;
+        T x = inb ? ((const T *)col.d_values)[i] : (T)0;
+        const bool valid = inb && valid_bit(col.d_validity, col.validity_bit_offset, i);
+        p2_elem<T, SMALL, MONO, NB>(st, c, s_hist, x, valid);
+        count(x, valid);
+    }
+    // ---- pass-2 block partial (as pass2_kernel) ----
+    __shared__ double s_mad[P2_BLOCK / WAVE];
+    __shared__ uint64_t s_u[P2_BLOCK / WAVE][3];
+    const int wid = t / WAVE, lane = lane_id();
+    const double mad = wave_sum_f64(st.mad);
+    const uint64_t hi = wave_sum_u64(st.high), lo = wave_sum_u64(st.low);
+    uint64_t ub = wave_sum_u64(st.unbinned);
+    if (SMALL && MONO) {
+#pragma unroll
+        for (int j = 0; j < P2_SMALL_BINS; ++j) st.bc[j] = j < NB ? (uint32_t)wave_sum_u64(st.bc[j]) : 0u;
+        ub = wave_sum_u64(st.okc) - st.bc[0];
+#pragma unroll
+        for (int j = 0; j < P2_SMALL_BINS - 1; ++j)
+            if (j + 1 < bins) st.bc[j] -= st.bc[j + 1];
+    }
+    if (lane == 0) { s_mad[wid] = mad; s_u[wid][0] = hi; s_u[wid][1] = lo; s_u[wid][2] = ub; }
+    if (SMALL && lane == 0) {
+#pragma unroll
+        for (int j = 0; j < P2_SMALL_BINS; ++j)
+            if (j < bins && st.bc[j]) atomicAdd(&s_hist[j], st.bc[j]);
+    }
+    __syncthreads();
+    const int stride = 3 + bins;
+    if (t == 0) {
+        double m = 0.0;
+        uint64_t a = 0, b = 0, u = 0;
+        for (int w = 0; w < P2_BLOCK / WAVE; ++w) { m += s_mad[w]; a += s_u[w][0]; b += s_u[w][1]; u += s_u[w][2]; }
+        part_mad[g] = m;
+        part_cnt[(int64_t)g * stride + 0] = a;
+        part_cnt[(int64_t)g * stride + 1] = b;
+        part_cnt[(int64_t)g * stride + 2] = u;
+    }
+    for (int i = t; i < bins; i += blockDim.x) part_cnt[(int64_t)g * stride + 3 + i] = s_hist[i];
+    // ---- level-1 count outputs (as part_count_rows_u64_kernel) ----
+    for (int b = t; b < nb; b += P2_BLOCK) hist[(int64_t)b * G + g] = cl.hist[b];
+    heavy_flush(cl.heavy, heavy.n, heavy_counts);
+    block_add_u64(rows, &stats[0]);
+    block_add_u64(special, &stats[1]);
+}
+
 __global__ void __launch_bounds__(MERGE_T) pass2_merge_kernel(const double *part_mad, const uint64_t *part_cnt,
                                                               int grid, int bins, sdp_pass2_result *out,
                                                               uint64_t *hist) {
@@ -1531,6 +1688,58 @@ extern "C" int sdp_column_keys(const sdp_column *col, uint64_t *d_out, uint64_t 
     SDP_DISPATCH_NUMERIC(col->dtype,
         hipLaunchKernelGGL(column_keys_kernel<T>, dim3(1024), dim3(256), 0, s, *col, d_out, d_out_n));
     return check_launch("column_keys_kernel");
+}
+
+extern "C" int64_t sdp_pass2_count_workspace_bytes(int64_t length, int32_t bins) {
+    if (length < 0 || bins < 1) return -1;
+    const int64_t rpb = sdp_part_rows_per_block(length, 0);
+    const int64_t g = (length + rpb - 1) / rpb < 1 ? 1 : (length + rpb - 1) / rpb;
+    return g * (int64_t)sizeof(double) + g * (int64_t)(3 + bins) * (int64_t)sizeof(uint64_t);
+}
+
+extern "C" int sdp_pass2_count(const sdp_column *col, double mean, const double *d_edges, int32_t bins,
+                               int32_t edges_monotone, double hi_t, double lo_t, void *d_work, int64_t work_bytes,
+                               sdp_pass2_result *d_result, uint64_t *d_hist, const sdp_heavy *heavy, int32_t b1,
+                               uint32_t *d_part_hist, uint64_t *d_heavy_counts, uint64_t *d_stats, void *stream) {
+    int rc = check_col(col, "sdp_pass2_count");
+    if (rc) return rc;
+    if (bins < 2 || bins > 8192) return set_error(SDP_EINVAL, "sdp_pass2_count: bins %d", bins);
+    if (b1 < 0 || b1 > 10 || d_part_hist == nullptr || d_stats == nullptr)
+        return set_error(SDP_EINVAL, "sdp_pass2_count: b1 %d / outputs", b1);
+    HeavyArg hv{nullptr, nullptr, nullptr, nullptr, 0};
+    if (heavy && heavy->n > 0) {
+        if (heavy->n > HEAVY_MAX || d_heavy_counts == nullptr)
+            return set_error(SDP_EINVAL, "sdp_pass2_count: %d heavy keys", heavy->n);
+        hv = HeavyArg{heavy->d_h, nullptr, nullptr, nullptr, heavy->n};
+    }
+    const int64_t n = col->length;
+    const int64_t rpb = sdp_part_rows_per_block(n, 0);
+    const int grid = (int)((n + rpb - 1) / rpb < 1 ? 1 : (n + rpb - 1) / rpb);
+    const int64_t need = sdp_pass2_count_workspace_bytes(n, bins);
+    if (work_bytes < need) return set_error(SDP_ECAP, "sdp_pass2_count: workspace %lld < %lld",
+                                            (long long)work_bytes, (long long)need);
+    double *pm = (double *)d_work;
+    uint64_t *pc = (uint64_t *)((char *)d_work + (int64_t)grid * sizeof(double));
+    const size_t lds = (size_t)bins * (sizeof(double) + sizeof(uint32_t)) + 16;
+    hipStream_t s = (hipStream_t)stream;
+#define SDP_P2C(SM, MO, ...) \
+    hipLaunchKernelGGL((pass2_count_kernel<T, SM, MO, ##__VA_ARGS__>), dim3(grid), dim3(P2_BLOCK), lds, s, *col, mean, \
+                       d_edges, bins, edges_monotone, hi_t, lo_t, pm, pc, hv, b1, rpb, d_part_hist, d_heavy_counts, \
+                       d_stats)
+    if (bins <= 10 && edges_monotone) {
+        SDP_DISPATCH_NUMERIC(col->dtype, SDP_P2C(true, true, 10));
+    } else if (bins <= P2_SMALL_BINS && edges_monotone) {
+        SDP_DISPATCH_NUMERIC(col->dtype, SDP_P2C(true, true));
+    } else if (bins <= P2_SMALL_BINS) {
+        SDP_DISPATCH_NUMERIC(col->dtype, SDP_P2C(true, false));
+    } else {
+        SDP_DISPATCH_NUMERIC(col->dtype, SDP_P2C(false, false));
+    }
+#undef SDP_P2C
+    rc = check_launch("pass2_count_kernel");
+    if (rc) return rc;
+    hipLaunchKernelGGL(pass2_merge_kernel, dim3(1), dim3(MERGE_T), 0, s, pm, pc, grid, bins, d_result, d_hist);
+    return check_launch("pass2_merge_kernel");
 }
 
 extern "C" int sdp_pass2(const sdp_column *col, double mean, const double *d_edges, int32_t bins,

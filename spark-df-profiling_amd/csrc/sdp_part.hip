@@ -28,16 +28,11 @@
 // output is packed exactly and nothing can overflow; every stage except the
 // LDS atomics inside a tile is deterministic.
 #include <type_traits>
-#include "sdp_common.h"
+#include "sdp_heavy.h"
 
 namespace sdp {
 
 constexpr int PT = 256;                 // threads of the small helper kernels
-constexpr int MAXB = 1024;              // buckets per level (b <= 10)
-constexpr int HEAVY_MAX = 256;
-constexpr int HEAVY_SLOTS = 1024;       // open-addressing slots (load <= 1/4)
-constexpr int HEAVY_FILTER = 16384;     // filter bits: most non-heavy rows need one LDS read
-constexpr int SHORT_MAX = 16;
 constexpr uint64_t RMASK40 = (1ull << 40) - 1ull;
 constexpr uint64_t LEN_MAX = (1ull << 24) - 1ull;
 
@@ -118,102 +113,6 @@ __device__ bool rows_equal_global(const sdp_bytes_column &c, int64_t ra, int64_t
     return true;
 }
 
-// ---- heavy keys ---------------------------------------------------------------
-struct HeavyArg {
-    const uint64_t *h;      // [n] hashes (fixed: h = mix64(key))
-    const uint64_t *k0;     // bytes only
-    const uint64_t *k1;
-    const uint64_t *meta;
-    int32_t n;
-};
-// (byte keys also keep each heavy key's first 16 bytes and length)
-template <bool BYTES>
-struct HeavyLdsT {
-    uint64_t h[HEAVY_SLOTS];
-    uint32_t filter[HEAVY_FILTER / 32];
-    int16_t idx[HEAVY_SLOTS];
-    uint32_t cnt[HEAVY_MAX];
-    uint64_t k0[BYTES ? HEAVY_MAX : 1];
-    uint64_t k1[BYTES ? HEAVY_MAX : 1];
-    uint32_t len[BYTES ? HEAVY_MAX : 1];
-};
-// filter bit of a hash: bits 20..33 (the slot uses the low bits, buckets the top)
-__device__ __forceinline__ uint32_t heavy_filter_bit(uint64_t h) { return (uint32_t)(h >> 20) & (HEAVY_FILTER - 1); }
-template <bool BYTES>
-__device__ __forceinline__ bool heavy_maybe(const HeavyLdsT<BYTES> &s, uint64_t h) {
-    const uint32_t fb = heavy_filter_bit(h);
-    return (s.filter[fb >> 5] >> (fb & 31)) & 1u;
-}
-template <bool BYTES>
-__device__ void heavy_build(HeavyLdsT<BYTES> &s, const HeavyArg &a) {
-    for (int i = threadIdx.x; i < HEAVY_SLOTS; i += blockDim.x) s.h[i] = EMPTY64;
-    for (int i = threadIdx.x; i < HEAVY_MAX; i += blockDim.x) s.cnt[i] = 0;
-    for (int i = threadIdx.x; i < HEAVY_FILTER / 32; i += blockDim.x) s.filter[i] = 0;
-    lds_barrier();
-    for (int i = threadIdx.x; i < a.n; i += blockDim.x) {
-        const uint64_t h = a.h[i];
-        const uint32_t fb = heavy_filter_bit(h);
-        atomicOr(&s.filter[fb >> 5], 1u << (fb & 31));
-        uint32_t pos = (uint32_t)h & (HEAVY_SLOTS - 1);
-        while (true) {
-            const uint64_t old = atomicCAS((unsigned long long *)&s.h[pos], (unsigned long long)EMPTY64,
-                                           (unsigned long long)h);
-            if (old == EMPTY64) { s.idx[pos] = (int16_t)i; break; }
-            pos = (pos + 1) & (HEAVY_SLOTS - 1);
-        }
-        if constexpr (BYTES) {
-            s.k0[i] = a.k0[i];
-            s.k1[i] = a.k1[i];
-            s.len[i] = (uint32_t)(a.meta[i] >> 40);
-        }
-    }
-    lds_barrier();
-}
-// index of the heavy key equal to this row, or -1
-__device__ __forceinline__ int heavy_find_u64(const HeavyLdsT<false> &s, int n, uint64_t h) {
-    if (n == 0 || h == EMPTY64 || !heavy_maybe(s, h)) return -1;
-    uint32_t pos = (uint32_t)h & (HEAVY_SLOTS - 1);
-    while (true) {
-        const uint64_t v = s.h[pos];
-        if (v == h) return s.idx[pos];
-        if (v == EMPTY64) return -1;
-        pos = (pos + 1) & (HEAVY_SLOTS - 1);
-    }
-}
-__device__ __forceinline__ int heavy_find_bytes(const HeavyLdsT<true> &s, int n, uint64_t h, uint64_t k0, uint64_t k1,
-                                                uint32_t len) {
-    if (n == 0 || len > SHORT_MAX || h == EMPTY64 || !heavy_maybe(s, h)) return -1;
-    uint32_t pos = (uint32_t)h & (HEAVY_SLOTS - 1);
-    while (true) {
-        const uint64_t v = s.h[pos];
-        if (v == EMPTY64) return -1;
-        if (v == h) {
-            const int i = s.idx[pos];
-            if (s.k0[i] == k0 && s.k1[i] == k1 && s.len[i] == len) return i;
-        }
-        pos = (pos + 1) & (HEAVY_SLOTS - 1);
-    }
-}
-// one device atomic per workgroup (not per wave) for a block total
-__device__ void block_add_u64(uint64_t v, uint64_t *dst) {
-    __shared__ uint64_t s_part[1024 / WAVE];
-    lds_barrier();                      // a previous call's reads of s_part are done
-    v = wave_sum_u64(v);
-    if (lane_id() == 0) s_part[threadIdx.x / WAVE] = v;
-    lds_barrier();
-    if (threadIdx.x == 0) {
-        uint64_t tot = 0;
-        for (int w = 0; w < (int)(blockDim.x / WAVE); ++w) tot += s_part[w];
-        if (tot) atomicAdd((unsigned long long *)dst, (unsigned long long)tot);
-    }
-}
-template <bool BYTES>
-__device__ void heavy_flush(HeavyLdsT<BYTES> &s, int n, uint64_t *counts) {
-    lds_barrier();
-    for (int i = threadIdx.x; i < n; i += blockDim.x)
-        if (s.cnt[i]) atomicAdd((unsigned long long *)&counts[i], (unsigned long long)s.cnt[i]);
-}
-
 // ---- block scan of nb <= MAXB LDS counters (exclusive), NT threads -----------
 template <int NT>
 __device__ void block_excl_scan(const uint32_t *in, uint32_t *out, int nb, uint32_t *s_wsum) {
@@ -271,17 +170,6 @@ __device__ __forceinline__ uint64_t fetch_key(const sdp_column &c, int64_t i, bo
     default: valid = false; return 0;
     }
 }
-template <typename T> __device__ __forceinline__ uint64_t key_of(T v);
-template <> __device__ __forceinline__ uint64_t key_of<double>(double v) { return f64_key(v); }
-template <> __device__ __forceinline__ uint64_t key_of<float>(float v) { return f64_key((double)v); }
-template <> __device__ __forceinline__ uint64_t key_of<int64_t>(int64_t v) { return i64_key(v); }
-template <> __device__ __forceinline__ uint64_t key_of<int32_t>(int32_t v) { return i64_key(v); }
-template <> __device__ __forceinline__ uint64_t key_of<int16_t>(int16_t v) { return i64_key(v); }
-template <> __device__ __forceinline__ uint64_t key_of<int8_t>(int8_t v) { return i64_key(v); }
-template <> __device__ __forceinline__ uint64_t key_of<uint64_t>(uint64_t v) { return v; }
-template <> __device__ __forceinline__ uint64_t key_of<uint32_t>(uint32_t v) { return v; }
-template <> __device__ __forceinline__ uint64_t key_of<uint16_t>(uint16_t v) { return v; }
-template <> __device__ __forceinline__ uint64_t key_of<uint8_t>(uint8_t v) { return v; }
 
 // One tile of NT * RPT rows held in registers.  Full tiles of a vectorisable
 // dtype are fetched with 16-byte loads by load() (issued early, so the next
@@ -542,6 +430,66 @@ __device__ __forceinline__ void bytes_tile(const sdp_bytes_column &col, int64_t 
     }
 }
 
+// The same tile in two stages, so a kernel can issue the NEXT tile's validity
+// and offsets (stage A) before it fetches this tile's key bytes (stage B, which
+// depends on A) and works on them: one memory latency per tile instead of two.
+template <int RPT>
+struct BytesOffs {
+    int64_t o0[RPT], o1[RPT];
+    uint32_t vmask;
+};
+template <int NT, int RPT>
+__device__ __forceinline__ void bytes_tile_a(const sdp_bytes_column &col, int64_t base, int64_t end,
+                                             BytesOffs<RPT> &a) {
+    const int t = threadIdx.x;
+    a.vmask = 0;
+#pragma unroll
+    for (int q = 0; q < RPT; ++q) {
+        const int64_t row = base + (int64_t)q * NT + t;
+        const bool ok = row < end && valid_bit(col.d_validity, col.validity_bit_offset, row);
+        a.vmask |= (uint32_t)ok << q;
+        a.o0[q] = ok ? str_off(col, row) : 0;
+        a.o1[q] = ok ? str_off(col, row + 1) : 0;
+    }
+}
+template <int NT, int RPT>
+__device__ __forceinline__ void bytes_tile_b(const sdp_bytes_column &col, int64_t base, const BytesOffs<RPT> &a,
+                                             uint64_t (&k0)[RPT], uint64_t (&k1)[RPT], uint64_t (&meta)[RPT],
+                                             uint64_t (&h)[RPT]) {
+    const int t = threadIdx.x;
+    uint32_t w[RPT][5];
+#pragma unroll
+    for (int q = 0; q < RPT; ++q) {
+        const int64_t len = a.o1[q] - a.o0[q];
+        const uintptr_t ad = (uintptr_t)(col.d_data + a.o0[q]);
+        const uint32_t *p = (const uint32_t *)(ad & ~(uintptr_t)3);
+        const int64_t need = len <= SHORT_MAX ? (int64_t)((ad & 3) + len + 3) >> 2 : 0;
+#pragma unroll
+        for (int k = 0; k < 5; ++k) w[q][k] = (((a.vmask >> q) & 1u) && k < need) ? p[k] : 0u;
+    }
+#pragma unroll
+    for (int q = 0; q < RPT; ++q) {
+        k0[q] = k1[q] = meta[q] = h[q] = 0;
+        if (!((a.vmask >> q) & 1u)) continue;
+        const int64_t row = base + (int64_t)q * NT + t;
+        const int64_t len = a.o1[q] - a.o0[q];
+        if (len <= SHORT_MAX) {
+            const uint32_t sh = (uint32_t)((uintptr_t)(col.d_data + a.o0[q]) & 3);
+            const uint64_t v0 = (uint64_t)__builtin_amdgcn_alignbyte(w[q][1], w[q][0], sh) |
+                                ((uint64_t)__builtin_amdgcn_alignbyte(w[q][2], w[q][1], sh) << 32);
+            const uint64_t v1 = (uint64_t)__builtin_amdgcn_alignbyte(w[q][3], w[q][2], sh) |
+                                ((uint64_t)__builtin_amdgcn_alignbyte(w[q][4], w[q][3], sh) << 32);
+            k0[q] = mask_bytes(v0, len);
+            k1[q] = mask_bytes(v1, len - 8);
+            h[q] = bh_short(k0[q], k1[q], (uint64_t)len);
+        } else {
+            h[q] = hash_long_global(col.d_data + a.o0[q], len);
+            k0[q] = h[q];
+        }
+        meta[q] = ((uint64_t)min((int64_t)LEN_MAX, len) << 40) | (uint64_t)(row + 1);
+    }
+}
+
 struct BCountLds {
     HeavyLdsT<true> heavy;
     uint32_t hist[MAXB];
@@ -571,10 +519,16 @@ __global__ void __launch_bounds__(B_CT) part_count_rows_bytes_kernel(sdp_bytes_c
     for (int b = t; b < nb; b += B_CT) s.hist[b] = 0;
     lds_barrier();
     uint64_t rows = 0;
-    for (int64_t base = r0; base < r1; base += B_CT * B_C_RPT) {
+    constexpr int64_t STEP = (int64_t)B_CT * B_C_RPT;
+    BytesOffs<B_C_RPT> oc, on;
+    if (r0 < r1) bytes_tile_a<B_CT, B_C_RPT>(col, r0, r1, oc);
+    for (int64_t base = r0; base < r1; base += STEP) {
         uint64_t k0[B_C_RPT], k1[B_C_RPT], meta[B_C_RPT], h[B_C_RPT];
-        uint32_t vmask;
-        bytes_tile<B_CT, B_C_RPT>(col, base, r1, k0, k1, meta, h, vmask);
+        const bool more = base + STEP < r1;
+        if (more) bytes_tile_a<B_CT, B_C_RPT>(col, base + STEP, r1, on);   // next tile's offsets in flight
+        bytes_tile_b<B_CT, B_C_RPT>(col, base, oc, k0, k1, meta, h);
+        const uint32_t vmask = oc.vmask;
+        if (more) oc = on;
 #pragma unroll
         for (int q = 0; q < B_C_RPT; ++q) {
             if ((vmask >> q) & 1u) {
@@ -607,12 +561,18 @@ __global__ void __launch_bounds__(B_ST) part_scatter_rows_bytes_kernel(sdp_bytes
         s.cur[b] = offs[(int64_t)b * G + g];
     }
     lds_barrier();
+    BytesOffs<B_S_RPT> oc, on;
+    if (r0 < r1) bytes_tile_a<B_ST, B_S_RPT>(col, r0, r1, oc);
     for (int64_t base = r0; base < r1; base += B_S_TILE) {
         uint64_t k0[B_S_RPT], k1[B_S_RPT], meta[B_S_RPT], h[B_S_RPT];
         uint32_t rank[B_S_RPT];
         int bk[B_S_RPT];
-        uint32_t keep = 0, vmask;
-        bytes_tile<B_ST, B_S_RPT>(col, base, r1, k0, k1, meta, h, vmask);
+        uint32_t keep = 0;
+        const bool more = base + B_S_TILE < r1;
+        bytes_tile_b<B_ST, B_S_RPT>(col, base, oc, k0, k1, meta, h);
+        const uint32_t vmask = oc.vmask;
+        // the next tile's offsets fly during this tile's LDS phases
+        if (more) bytes_tile_a<B_ST, B_S_RPT>(col, base + B_S_TILE, r1, on);
 #pragma unroll
         for (int q = 0; q < B_S_RPT; ++q) {
             if ((vmask >> q) & 1u) {
@@ -651,6 +611,7 @@ __global__ void __launch_bounds__(B_ST) part_scatter_rows_bytes_kernel(sdp_bytes
             s.hist[b] = 0;
         }
         lds_barrier();
+        if (more) oc = on;
     }
 }
 

@@ -135,6 +135,9 @@ _SIGNATURES = {
     'sdp_select_batch_step': (ctypes.c_int, [_P, _I32, _I32, _I32, _P, _P]),
     'sdp_compact_batch': (ctypes.c_int, [_P, _I32, _I64, _P]),
     'sdp_pass2': (ctypes.c_int, [_COL, _D, _P, _I32, _I32, _D, _D, _P, _I64, _P, _P, _P]),
+    'sdp_pass2_count_workspace_bytes': (_I64, [_I64, _I32]),
+    'sdp_pass2_count': (ctypes.c_int, [_COL, _D, _P, _I32, _I32, _D, _D, _P, _I64, _P, _P, _HVY, _I32, _P, _P, _P,
+                                       _P]),
     'sdp_table_clear': (ctypes.c_int, [_P, _P, _I64, _I32, _P]),
     'sdp_hash_u64': (ctypes.c_int, [_COL, _P, _P, _P, _I64, _I32, _P, _P]),
     'sdp_hash_bytes': (ctypes.c_int, [_BCOL, _P, _P, _P, _I64, _P, _P]),
@@ -166,7 +169,7 @@ _SIGNATURES = {
 _VALUE_FUNCS = {'sdp_last_error', 'sdp_version', 'sdp_pass1_workspace_bytes', 'sdp_pass2_workspace_bytes',
                 'sdp_pass1_grid', 'sdp_gram_workspace_bytes', 'sdp_part_rows_per_block', 'sdp_part_bucket_target',
                 'sdp_scan_workspace_bytes', 'sdp_bitmap_workspace_bytes', 'sdp_select_kth_workspace_bytes',
-                'sdp_select_rounds'}
+                'sdp_select_rounds', 'sdp_pass2_count_workspace_bytes'}
 _STATUS_FUNCS = set(_SIGNATURES) - _VALUE_FUNCS
 
 _lib = None

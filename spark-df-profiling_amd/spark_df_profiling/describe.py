@@ -313,7 +313,14 @@ def describe(df, bins=10, corr_reject=0.9, **kwargs):
         # per-column loop below only counts distincts and assembles
         num_cols = [c for c in table.columns if _is_numeric(c)]
         packs = engine.numeric_pass1_batch(num_cols)
-        stats = engine.numeric_stats_batch(num_cols, packs, bins, [k_vals.get(c.name, 2) for c in num_cols])
+        p1s = [pk[0] for pk in packs]
+        hints = [_distinct_hint(p1, c.spark_type) for c, p1 in zip(num_cols, p1s)]
+        bounds = [(p1['imin'], p1['imax']) if p1['count'] else None for p1 in p1s]
+        group_cols = set()
+        if world == 1:
+            group_cols = {i for i, pth in enumerate(engine.distinct_paths(num_cols, hints, bounds)) if pth == 'group'}
+        stats = engine.numeric_stats_batch(num_cols, packs, bins, [k_vals.get(c.name, 2) for c in num_cols],
+                                           group_cols=group_cols)
         for col, pack, st in zip(num_cols, packs, stats):
             bundles[col.name]['p1_pack'] = pack
             if st is not None:
@@ -324,9 +331,6 @@ def describe(df, bins=10, corr_reject=0.9, **kwargs):
                     early_plots[col.name] = _submit_plot(st)
         if world == 1:
             # every NUM column's countDistinct with shared readbacks
-            p1s = [pk[0] for pk in packs]
-            hints = [_distinct_hint(p1, c.spark_type) for c, p1 in zip(num_cols, p1s)]
-            bounds = [(p1['imin'], p1['imax']) if p1['count'] else None for p1 in p1s]
             for col, d in zip(num_cols, engine.distinct_batch(num_cols, hints, bounds)):
                 bundles[col.name]['distinct_pre'] = d
     if workers > 1:

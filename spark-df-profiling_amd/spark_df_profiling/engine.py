@@ -176,6 +176,7 @@ class Engine:
     # -- small helpers ----------------------------------------------------------
     _heavy_pre = None
     _near_unique = frozenset()
+    _counted = {}            # id(col) -> group context whose level-1 count pass 2 did
 
     def _s(self):
         return nat.stream_handle(self.stream)
@@ -662,27 +663,45 @@ class Engine:
                 out[p] = key_to_float(values[lo_r])
         return out, st['fallback'] is not None
 
-    def pass2_batch(self, items):
+    def pass2_batch(self, items, count_ctx=None):
         """[(col, mean, edges, hi_t, lo_t)] -> [pass-2 dict] (see pass2), all
         launched back to back and read back once (sharded: one all-reduce of
-        every column's counts and bins, one all-gather of the mad partials)."""
+        every column's counts and bins, one all-gather of the mad partials).
+        count_ctx[i] (a _group_prepare context) makes column i's launch also do
+        the level-1 count of its distinct-count partitioning (sdp_pass2_count);
+        the context is then kept for group_batch."""
         if not items:
             return []
         s = self._s()
         rsz = ctypes.sizeof(nat.SdpPass2Result)
+        count_ctx = count_ctx or {}
         outs = []
-        for col, mean, edges, hi_t, lo_t in items:
+        for i, (col, mean, edges, hi_t, lo_t) in enumerate(items):
             bins = len(edges)
             e = self._h2d(np.array([float(x) for x in edges], dtype=np.float64))
             mono = all(math.isfinite(float(x)) for x in edges) and all(
-                float(edges[i]) <= float(edges[i + 1]) for i in range(bins - 1))
-            work = self._bytes(sdp.sdp_pass2_workspace_bytes(col.length, col.dtype, bins))
+                float(edges[j]) <= float(edges[j + 1]) for j in range(bins - 1))
             res = self._bytes(rsz)
             hist = self._u64(bins)
             cs = col.sdp()
-            nat.annotate(_label(col), col_read_bytes(col))
-            sdp.sdp_pass2(ctypes.byref(cs), float(mean), ptr(e), bins, int(mono), float(hi_t), float(lo_t), ptr(work),
-                          work.numel(), ptr(res), ptr(hist), s)
+            ctx = count_ctx.get(i)
+            if ctx is not None:
+                work = self._bytes(max(sdp.sdp_pass2_count_workspace_bytes(col.length, bins),
+                                       sdp.sdp_pass2_workspace_bytes(col.length, col.dtype, bins)))
+                hv = ctx['hv']
+                nat.annotate(_label(col), col_read_bytes(col))
+                sdp.sdp_pass2_count(ctypes.byref(cs), float(mean), ptr(e), bins, int(mono), float(hi_t), float(lo_t),
+                                    ptr(work), work.numel(), ptr(res), ptr(hist),
+                                    ctypes.byref(hv['struct']) if hv else None, ctx['b1'], ptr(ctx['h1']),
+                                    ptr(ctx['hcnt']), ptr(ctx['stats']), s)
+                if self._counted is Engine._counted:
+                    self._counted = {}
+                self._counted[id(col)] = ctx
+            else:
+                work = self._bytes(sdp.sdp_pass2_workspace_bytes(col.length, col.dtype, bins))
+                nat.annotate(_label(col), col_read_bytes(col))
+                sdp.sdp_pass2(ctypes.byref(cs), float(mean), ptr(e), bins, int(mono), float(hi_t), float(lo_t),
+                              ptr(work), work.numel(), ptr(res), ptr(hist), s)
             outs.append((res, hist, e, work))
         if self.comm.world == 1:
             raw = torch.cat([t for res, hist, _, _ in outs for t in (res[:rsz], hist.view(torch.uint8))]).cpu().numpy()
@@ -709,7 +728,7 @@ class Engine:
                            'n_low': int(v[1]), 'n_unbinned': int(v[2]), 'hist': v[3:].astype(np.int64)})
         return result
 
-    def numeric_stats_batch(self, cols, packs, bins=10, ks=None, probs=PROBS):
+    def numeric_stats_batch(self, cols, packs, bins=10, ks=None, probs=PROBS, group_cols=()):
         """numeric_stats of every column (None for a column with no non-null
         value) with two host readbacks in all.  A bins value the reference
         rejects (describe.py:46 with bins=1) is recorded per column and raised
@@ -743,7 +762,16 @@ class Engine:
             p2_items.append((col, st.mean, edges, hi_t, lo_t))
             p2_idx.append(i)
             stats[i] = st
-        for i, r2 in zip(p2_idx, self.pass2_batch(p2_items)):
+        # columns whose countDistinct takes the partitioning path: pass 2 also
+        # does their level-1 count (single rank; one column read fewer)
+        count_ctx = {}
+        if self.comm.world == 1:
+            for j, i in enumerate(p2_idx):
+                if i in group_cols:
+                    ctx = self._group_prepare(cols[i], False)
+                    if ctx is not None:
+                        count_ctx[j] = ctx
+        for i, r2 in zip(p2_idx, self.pass2_batch(p2_items, count_ctx)):
             st = stats[i]
             st.mad = r2['abs_dev_sum']
             st.hist_counts = r2['hist']
@@ -945,7 +973,10 @@ class Engine:
         array, every column's scatters and de-duplication queued back to back
         (record buffers recycled on the stream between columns), one readback
         of every column's group statistics.  None where group() returns None."""
-        ctxs = [self._group_begin(c, False) for c in cols]
+        ctxs = []
+        for c in cols:
+            pre = self._counted.pop(id(c), None)           # counted by pass 2 (sdp_pass2_count)
+            ctxs.append(self._group_scan(pre) if pre is not None else self._group_begin(c, False))
         live = [c for c in ctxs if c is not None]
         if not live:
             return [None] * len(cols)
@@ -967,8 +998,9 @@ class Engine:
             off += m
         return out
 
-    def _group_begin(self, col, with_counts):
-        """Level-1 bucket counts of `col` and their scan (no readback)."""
+    def _group_prepare(self, col, with_counts):
+        """Geometry and buffers of the two-level partitioning of `col` (None
+        when the column needs more than 20 hash bits of buckets)."""
         isb = col.kind == 'bytes'
         with_counts = with_counts or isb
         n = col.length
@@ -984,26 +1016,39 @@ class Engine:
         if b2 > 10:
             return None
         nb1, nb2 = 1 << b1, 1 << b2
-        s = self._s()
-        stats = self._u64(68, zero=True)
-        cs = None if isb else col.sdp()
-        bc = col.sdp_bytes() if isb else None
         hv = self._heavy_keys(col, isb)
-        hcnt = self._u64(max(hv['n'] if hv else 1, 1), zero=True)
         rpb = sdp.sdp_part_rows_per_block(n, int(isb))
         grid = max(1, -(-n // rpb))
-        h1 = torch.empty(nb1 * grid, dtype=torch.int32, device=self.device)
-        ctx = {'col': col, 'isb': isb, 'with_counts': with_counts, 'large': large, 'b1': b1, 'b2': b2,
-               'nb1': nb1, 'nb2': nb2, 'stats': stats, 'cs': cs, 'bc': bc, 'hv': hv, 'hcnt': hcnt, 'grid': grid,
-               'rb': col_read_bytes(col), 'recw': 24 if isb else 8}
+        return {'col': col, 'isb': isb, 'with_counts': with_counts, 'large': large, 'b1': b1, 'b2': b2,
+                'nb1': nb1, 'nb2': nb2, 'stats': self._u64(68, zero=True), 'cs': None if isb else col.sdp(),
+                'bc': col.sdp_bytes() if isb else None, 'hv': hv,
+                'hcnt': self._u64(max(hv['n'] if hv else 1, 1), zero=True), 'grid': grid,
+                'h1': torch.empty(nb1 * grid, dtype=torch.int32, device=self.device),
+                'rb': col_read_bytes(col), 'recw': 24 if isb else 8}
+
+    def _group_count(self, ctx):
+        """Level-1 bucket counts (sdp_part_rows phase 0)."""
+        col, isb, hv = ctx['col'], ctx['isb'], ctx['hv']
         nat.annotate(_label(col, 'count'), ctx['rb'])
-        sdp.sdp_part_rows(self._gref(ctx), ctypes.byref(bc) if isb else None,
-                          ctypes.byref(hv['struct']) if hv else None, b1, 0, ptr(h1), None, None, ptr(hcnt),
-                          ptr(stats), s)
-        o1 = self._scan(h1)
+        sdp.sdp_part_rows(self._gref(ctx), ctypes.byref(ctx['bc']) if isb else None,
+                          ctypes.byref(hv['struct']) if hv else None, ctx['b1'], 0, ptr(ctx['h1']), None, None,
+                          ptr(ctx['hcnt']), ptr(ctx['stats']), self._s())
+
+    def _group_scan(self, ctx):
+        o1 = self._scan(ctx['h1'])
+        del ctx['h1']
+        nb1, grid = ctx['nb1'], ctx['grid']
         ctx['o1'] = o1
         ctx['bsn_dev'] = torch.cat([o1[0:nb1 * grid:grid], o1[-1:]])     # record count + L1 bucket starts
         return ctx
+
+    def _group_begin(self, col, with_counts):
+        """Level-1 bucket counts of `col` and their scan (no readback)."""
+        ctx = self._group_prepare(col, with_counts)
+        if ctx is None:
+            return None
+        self._group_count(ctx)
+        return self._group_scan(ctx)
 
     @staticmethod
     def _gref(ctx):
@@ -1114,6 +1159,20 @@ class Engine:
             tab.update({'slots': keys, 'counts': counts, 'capacity': max(total, 1)})
         return tab
 
+    def distinct_paths(self, cols, hints, bounds):
+        """'bitmap' | 'group' | 'table' per column: the path choice of
+        describe._distinct_count / distinct_fixed on a single rank."""
+        out = []
+        for col, hint, bd in zip(cols, hints, bounds):
+            if (bd is not None and col.kind == 'fixed' and col.dtype in self.BITMAP_DTYPES
+                    and bd[1] - bd[0] + 1 <= nat.BITMAP_MAX_BITS):
+                out.append('bitmap')
+            elif hint * 4 > max(col.length, 1) and col.length >= (1 << 16):
+                out.append('group')
+            else:
+                out.append('table')
+        return out
+
     def distinct_batch(self, cols, hints, bounds):
         """countDistinct of several NUM/DATE columns (describe.py:143) with
         the path choice of describe._distinct_count / distinct_fixed per column
@@ -1122,13 +1181,9 @@ class Engine:
         `bounds[i]` = (imin, imax) for integral columns with values, else None.
         Single rank only; returns [distinct count]."""
         out = [None] * len(cols)
-        bm, grp = [], []
-        for i, (col, hint, bd) in enumerate(zip(cols, hints, bounds)):
-            if (bd is not None and col.kind == 'fixed' and col.dtype in self.BITMAP_DTYPES
-                    and bd[1] - bd[0] + 1 <= nat.BITMAP_MAX_BITS):
-                bm.append(i)
-            elif hint * 4 > max(col.length, 1) and col.length >= (1 << 16):
-                grp.append(i)
+        paths = self.distinct_paths(cols, hints, bounds)
+        bm = [i for i, pth in enumerate(paths) if pth == 'bitmap']
+        grp = [i for i, pth in enumerate(paths) if pth == 'group']
         if bm:
             outs = [self._distinct_bitmap_launch(cols[i], bounds[i][0], bounds[i][1] - bounds[i][0] + 1) for i in bm]
             for i, v in zip(bm, self._host_u64(torch.cat(outs))):
