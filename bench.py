@@ -486,6 +486,13 @@ def main():
     step_s = elapsed / args.steps
     rl, per_kernel = roofline(rec, args.steps, step_s, profile_alg_bytes(table, raw), traffic_path)
     ncols = len(table.columns)
+    # quantile-window candidates written by pass 1, as a fraction of each NUM
+    # column's counted rows (sum over its windows of the keys strictly inside)
+    cand = {}
+    for name, b in raw.get('columns', {}).items():
+        pk = b.get('p1_pack')
+        if pk and pk[0]['count']:
+            cand[name] = round(sum(pk[0]['w_in']) / pk[0]['count'], 4)
     if args.workload == 'c5':
         hbm_rl = rl
         rl = gram_roofline(rec, args.steps, ncols, table.num_rows, traffic_path)
@@ -510,6 +517,8 @@ def main():
                    'column_workers': column_workers_used},
         'roofline': rl,
         'per_kernel': per_kernel,
+        'quantile_candidates_frac': {'max': max(cand.values()) if cand else None,
+                                     'mean': round(sum(cand.values()) / len(cand), 4) if cand else None},
         'resident_gb_per_gpu': round(table_bytes(table) / 1e9, 2),
         'allocator': alloc,
         'gen_s': round(t_gen, 1),

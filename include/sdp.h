@@ -128,6 +128,15 @@ int sdp_sample_keys(const sdp_column *col, int32_t n_sample, uint64_t *d_sample,
 int sdp_quantile_plan(uint64_t *d_sample, int32_t n_sample, const double *probs,
                       int32_t n_probs, int32_t is_float, sdp_qplan *d_plan,
                       void *stream);
+/* Narrows the windows of n_cols plans (d_plans, as sdp_quantile_plan_batch
+ * wrote them) with a second, larger row sample per column (n_sample2 keys at
+ * d_samples2 + i * n_sample2, EMPTY64 = null/NaN): around each probability a
+ * window of +-(4 sigma + 2) ranks of the larger sample inside its first-sample
+ * window.  A plan whose windows hold more sample keys than one LDS sort (16 K)
+ * is left as it was. */
+int sdp_quantile_refine_batch(const uint64_t *d_samples2, int32_t n_sample2, int32_t n_cols,
+                              const double *d_probs, int32_t n_probs, sdp_qplan *d_plans, void *stream);
+
 /* sdp_quantile_plan of n_cols columns in one launch (one workgroup each):
  * samples [n_cols][n_sample], is_float [n_cols] (device), plans [n_cols]. */
 int sdp_quantile_plan_batch(uint64_t *d_samples, int32_t n_sample, int32_t n_cols,

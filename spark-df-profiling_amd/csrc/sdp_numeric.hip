@@ -164,6 +164,112 @@ __global__ void __launch_bounds__(1024) quantile_plan_kernel(uint64_t *sample, i
     *plan = p;
 }
 
+// Window refinement from a second, larger sample S2 (one workgroup per column).
+// The S1 windows are +-(4 sigma + 2) sample ranks of a 16 K sample; S2's keys
+// that fall inside those windows (~11 % of S2) are sorted in LDS, and around
+// each probability a window of +-(4 sigma2 + 2) S2 ranks is taken inside its S1
+// window, so windows shrink by sqrt(n2 / n1) at the same miss probability.
+// S2 keys below each window are counted to place the ranks.  If the in-window
+// keys exceed the LDS sort, or a rank lands outside every S1 window, the S1
+// plan stands (windows are a performance device: a miss falls back exactly).
+__global__ void __launch_bounds__(1024) quantile_refine_kernel(const uint64_t *samples2, int32_t ns2,
+                                                               const double *probs, int32_t np, sdp_qplan *plans) {
+    __shared__ uint64_t s[SORT_MAX];
+    __shared__ uint32_t s_cnt, s_valid;
+    __shared__ uint32_t s_below[SDP_MAX_WINDOWS], s_in[SDP_MAX_WINDOWS];
+    const uint64_t *sample2 = samples2 + (int64_t)blockIdx.x * ns2;
+    sdp_qplan *plan = plans + blockIdx.x;
+    const int nw = plan->n_windows;
+    if (nw == 0 || plan->n_sample < 64 || ns2 <= plan->n_sample) return;     // (uniform per block)
+    uint64_t lo[SDP_MAX_WINDOWS], hi[SDP_MAX_WINDOWS];
+#pragma unroll
+    for (int w = 0; w < SDP_MAX_WINDOWS; ++w) {
+        lo[w] = w < nw ? plan->lo[w] : EMPTY64;
+        hi[w] = w < nw ? plan->hi[w] : EMPTY64;
+    }
+    if (threadIdx.x == 0) { s_cnt = 0; s_valid = 0; }
+    if (threadIdx.x < SDP_MAX_WINDOWS) { s_below[threadIdx.x] = 0; s_in[threadIdx.x] = 0; }
+    __syncthreads();
+    uint32_t valid = 0, below[SDP_MAX_WINDOWS], inw[SDP_MAX_WINDOWS];
+#pragma unroll
+    for (int w = 0; w < SDP_MAX_WINDOWS; ++w) below[w] = inw[w] = 0;
+    for (int i = threadIdx.x; i < ns2; i += blockDim.x) {
+        const uint64_t k = sample2[i];
+        if (k == EMPTY64) continue;                  // null / NaN rows of the sample
+        ++valid;
+        bool in = false;
+#pragma unroll
+        for (int w = 0; w < SDP_MAX_WINDOWS; ++w) {
+            if (w >= nw) break;
+            below[w] += k < lo[w];
+            const bool iw = k >= lo[w] && k <= hi[w];
+            inw[w] += iw;
+            in = in || iw;
+        }
+        if (in) {
+            const uint32_t pos = atomicAdd(&s_cnt, 1u);
+            if (pos < SORT_MAX) s[pos] = k;
+        }
+    }
+    // block sums of the per-thread counters (fixed-order wave sums, then LDS atomics of 16 partials)
+    const uint32_t vs = (uint32_t)wave_sum_u64(valid);
+    if (lane_id() == 0) atomicAdd(&s_valid, vs);
+#pragma unroll
+    for (int w = 0; w < SDP_MAX_WINDOWS; ++w) {
+        const uint32_t b = (uint32_t)wave_sum_u64(below[w]), c = (uint32_t)wave_sum_u64(inw[w]);
+        if (lane_id() == 0 && w < nw) { atomicAdd(&s_below[w], b); atomicAdd(&s_in[w], c); }
+    }
+    __syncthreads();
+    const uint32_t cnt = s_cnt;
+    if (cnt > SORT_MAX || cnt == 0) return;        // the S1 plan stands
+    block_sort_keys(s, (int)cnt);                  // windows are disjoint: window w's keys form one run
+    if (threadIdx.x != 0) return;
+    const uint32_t m2 = s_valid;
+    sdp_qplan p = *plan;
+    uint32_t seg0[SDP_MAX_WINDOWS];
+    uint32_t acc = 0;
+    for (int w = 0; w < nw; ++w) { seg0[w] = acc; acc += s_in[w]; }
+    uint64_t nlo[SDP_MAX_WINDOWS], nhi[SDP_MAX_WINDOWS];
+    int nn = 0;
+    for (int t = 0; t < np && t < SDP_MAX_WINDOWS; ++t) {
+        const double q = probs[t];
+        const double r = q * (double)(m2 - 1);
+        int w = -1;
+        for (int v = 0; v < nw; ++v)
+            if ((double)s_below[v] <= floor(r) && ceil(r) < (double)(s_below[v] + s_in[v])) { w = v; break; }
+        if (w < 0) return;                         // a rank outside the S1 windows: keep the S1 plan
+        const int d = (int)ceil(4.0 * sqrt((double)m2 * q * (1.0 - q))) + 2;
+        const int cw = (int)s_in[w];
+        int il = (int)floor(r) - d - (int)s_below[w], ih = (int)ceil(r) + d - (int)s_below[w];
+        const uint64_t l = il <= 0 ? p.lo[w] : s[seg0[w] + il];
+        const uint64_t h = ih >= cw - 1 ? p.hi[w] : s[seg0[w] + ih];
+        if (nn > 0 && l <= nhi[nn - 1]) {
+            if (h > nhi[nn - 1]) nhi[nn - 1] = h;
+        } else {
+            nlo[nn] = l;
+            nhi[nn] = h;
+            ++nn;
+        }
+    }
+    for (int w = 0; w < SDP_MAX_WINDOWS; ++w) {
+        p.lo[w] = w < nn ? nlo[w] : 0;
+        p.hi[w] = w < nn ? nhi[w] : EMPTY64;
+        p.in_sample[w] = 0;
+    }
+    for (int w = 0; w < nn; ++w) {
+        // S2 keys strictly inside (lo, hi) by binary search on the sorted in-window keys
+        int a = 0, b = (int)cnt;
+        while (a < b) { int mid = (a + b) >> 1; if (s[mid] < p.hi[w]) a = mid + 1; else b = mid; }
+        const int below_hi = a;
+        a = 0; b = (int)cnt;
+        while (a < b) { int mid = (a + b) >> 1; if (s[mid] <= p.lo[w]) a = mid + 1; else b = mid; }
+        p.in_sample[w] = below_hi > a ? below_hi - a : 0;
+    }
+    p.n_windows = nn;
+    p.n_sample = (int32_t)m2;
+    *plan = p;
+}
+
 // ============================================================================
 // pass 1
 // ============================================================================
@@ -1217,7 +1323,7 @@ extern "C" int64_t sdp_pass2_workspace_bytes(int64_t length, int32_t dtype, int3
 extern "C" int sdp_sample_keys(const sdp_column *col, int32_t n_sample, uint64_t *d_sample, void *stream) {
     int rc = check_col(col, "sdp_sample_keys");
     if (rc) return rc;
-    if (n_sample < 1 || n_sample > SORT_MAX) return set_error(SDP_EINVAL, "sdp_sample_keys: n_sample %d", n_sample);
+    if (n_sample < 1 || n_sample > (1 << 22)) return set_error(SDP_EINVAL, "sdp_sample_keys: n_sample %d", n_sample);
     hipStream_t s = (hipStream_t)stream;
     const int blocks = (n_sample + 255) / 256;
     SDP_DISPATCH_NUMERIC(col->dtype,
@@ -1234,6 +1340,14 @@ extern "C" int sdp_quantile_plan(uint64_t *d_sample, int32_t n_sample, const dou
     return check_launch("quantile_plan_kernel");
 }
 
+extern "C" int sdp_quantile_refine_batch(const uint64_t *d_samples2, int32_t n_sample2, int32_t n_cols,
+                                         const double *d_probs, int32_t n_probs, sdp_qplan *d_plans, void *stream) {
+    if (n_sample2 < 1 || n_cols < 1 || n_probs < 0 || n_probs > SDP_MAX_WINDOWS)
+        return set_error(SDP_EINVAL, "sdp_quantile_refine_batch: n_sample2 %d n_cols %d", n_sample2, n_cols);
+    hipLaunchKernelGGL(quantile_refine_kernel, dim3(n_cols), dim3(1024), 0, (hipStream_t)stream, d_samples2,
+                       n_sample2, d_probs, n_probs, d_plans);
+    return check_launch("quantile_refine_kernel");
+}
 extern "C" int sdp_quantile_plan_batch(uint64_t *d_samples, int32_t n_sample, int32_t n_cols, const double *d_probs,
                                        int32_t n_probs, const int32_t *d_is_float, sdp_qplan *d_plans,
                                        void *stream) {
