@@ -490,9 +490,9 @@ def main():
     # column's counted rows (sum over its windows of the keys strictly inside)
     cand = {}
     for name, b in raw.get('columns', {}).items():
-        pk = b.get('p1_pack')
-        if pk and pk[0]['count']:
-            cand[name] = round(sum(pk[0]['w_in']) / pk[0]['count'], 4)
+        p1 = b.get('p1')
+        if p1 and p1['count']:
+            cand[name] = round(sum(p1['w_in']) / p1['count'], 4)
     if args.workload == 'c5':
         hbm_rl = rl
         rl = gram_roofline(rec, args.steps, ncols, table.num_rows, traffic_path)

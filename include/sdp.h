@@ -373,6 +373,11 @@ int sdp_pass2_count(const sdp_column *col, double mean, const double *d_edges, i
                     sdp_pass2_result *d_result, uint64_t *d_hist, const sdp_heavy *heavy, int32_t b1,
                     uint32_t *d_part_hist, uint64_t *d_heavy_counts, uint64_t *d_stats, void *stream);
 
+/* Packs the key bytes of n groups -- bytes [d_starts[i], d_starts[i] + d_lens[i])
+ * of d_data -- at d_out + d_offs[i] (the sharded string exchange's payload). */
+int sdp_gather_bytes(const uint8_t *d_data, const int64_t *d_starts, const int64_t *d_lens,
+                     const int64_t *d_offs, int64_t n, uint8_t *d_out, void *stream);
+
 /* Rows per partition workgroup (grid = ceil(length / this)). */
 int64_t sdp_part_rows_per_block(int64_t length, int32_t is_bytes);
 /* Mean records per final bucket the dedup tables are sized for. */

@@ -578,6 +578,21 @@ extern "C" int sdp_first_valid(const sdp_column *col, int32_t k, int64_t *d_idx,
     return check_launch("first_valid_kernel");
 }
 
+// Packs the key bytes of n groups (bytes [starts[i], starts[i] + lens[i]) of
+// `data`) back to back at out + offs[i]: the payload of the sharded string
+// exchange (distributed.exchange_bytes_groups).  One thread per group; keys are
+// short, so a byte loop beats any per-byte index array (which would cost 8 B of
+// index per key byte).
+__global__ void gather_bytes_kernel(const uint8_t *data, const int64_t *starts, const int64_t *lens,
+                                    const int64_t *offs, int64_t n, uint8_t *out) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        const uint8_t *src = data + starts[i];
+        uint8_t *dst = out + offs[i];
+        const int64_t len = lens[i];
+        for (int64_t b = 0; b < len; ++b) dst[b] = src[b];
+    }
+}
+
 // validity of byte columns for first_valid: expose the count of valid rows too
 __global__ void count_valid_kernel(const uint8_t *bm, int64_t off, int64_t n, uint64_t *out) {
     uint64_t c = 0;
@@ -592,4 +607,15 @@ extern "C" int sdp_count_valid(const uint8_t *d_validity, int64_t bit_offset, in
     hipLaunchKernelGGL(count_valid_kernel, dim3(grid_for(length, 256 * 32, 2048)), dim3(256), 0, (hipStream_t)stream,
                        d_validity, bit_offset, length, d_out);
     return check_launch("count_valid_kernel");
+}
+
+extern "C" int sdp_gather_bytes(const uint8_t *d_data, const int64_t *d_starts, const int64_t *d_lens,
+                                const int64_t *d_offs, int64_t n, uint8_t *d_out, void *stream) {
+    if (n < 0) return set_error(SDP_EINVAL, "sdp_gather_bytes: n %lld", (long long)n);
+    if (n == 0) return 0;
+    int64_t grid = (n + 255) / 256;
+    if (grid > 65536) grid = 65536;
+    hipLaunchKernelGGL(gather_bytes_kernel, dim3((unsigned)grid), dim3(256), 0, (hipStream_t)stream, d_data, d_starts,
+                       d_lens, d_offs, n, d_out);
+    return check_launch("gather_bytes_kernel");
 }

@@ -360,6 +360,7 @@ __device__ __forceinline__ void p1_elem(P1Thread &st, const P1Ctx &cx, T x, bool
         // d and d^3 are summed plainly over the thread's tile (<= 16 terms) and
         // folded into the compensated totals once per tile (p1_fold): the sum
         // errs by <= ~3 eps * sum|d| instead of costing two TwoSums per element
+        // (a branch-free form of this block with selects measured 1.8x slower)
         const double d = xd - cx.K;
         const double d2 = d * d;
         st.t1 += d;

@@ -139,6 +139,7 @@ _SIGNATURES = {
     'sdp_pass2_count_workspace_bytes': (_I64, [_I64, _I32]),
     'sdp_pass2_count': (ctypes.c_int, [_COL, _D, _P, _I32, _I32, _D, _D, _P, _I64, _P, _P, _HVY, _I32, _P, _P, _P,
                                        _P]),
+    'sdp_gather_bytes': (ctypes.c_int, [_P, _P, _P, _P, _I64, _P, _P]),
     'sdp_table_clear': (ctypes.c_int, [_P, _P, _I64, _I32, _P]),
     'sdp_hash_u64': (ctypes.c_int, [_COL, _P, _P, _P, _I64, _I32, _P, _P]),
     'sdp_hash_bytes': (ctypes.c_int, [_BCOL, _P, _P, _P, _I64, _P, _P]),

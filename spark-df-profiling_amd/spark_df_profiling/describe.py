@@ -127,6 +127,7 @@ def describe_1d(engine: Engine, col: DeviceColumn, nrows, bins, k, freq, bundle)
     elif numeric:
         p1_pack = bundle.pop('p1_pack', None) or engine.numeric_pass1(col)
         p1 = p1_pack[0]
+        bundle['p1'] = p1
         count = p1['count']
         distinct = bundle.pop('distinct_pre', None)
         if distinct is None:
