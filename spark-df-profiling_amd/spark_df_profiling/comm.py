@@ -11,8 +11,10 @@ Every statistic resolves through one of three collectives:
 
 `LocalComm` is the single-process identity.  `TorchComm` uses
 torch.distributed: backend 'nccl' is RCCL over xGMI on ROCm; 'gloo' is used by
-the CPU tests (tensors are moved to the host for the collective).  gloo has no
-all_to_all, so alltoallv falls back to all_gather + local selection there.
+the CPU tests (tensors are moved to the host for the collective); it runs the
+same all_to_all_single calls as RCCL, on host copies.  RCCL itself refuses two
+ranks on one GPU ("Duplicate GPU detected", tools/rccl_probe.py), so the nccl
+branches run for the first time on a multi-GPU node.
 """
 
 from __future__ import annotations
@@ -97,25 +99,22 @@ class TorchComm:
 
     def alltoallv(self, send, send_counts):
         """send is laid out rank-major (send_counts[r] elements for rank r)."""
+        # gloo runs the same all_to_all_single calls on host copies, so the
+        # CPU tests exercise exactly the split logic RCCL sees
         dev = send.device
-        counts = torch.tensor(send_counts, dtype=torch.int64, device=dev)
-        if self.cpu:
-            # gloo: no all_to_all -- gather everything and keep our slice
-            all_counts = self.allgather(counts)
-            all_send = self.allgatherv(send)
-            parts = []
-            for r in range(self.world):
-                c = all_counts[r].tolist()
-                start = sum(c[:self.rank])
-                parts.append(all_send[r][start:start + c[self.rank]])
-            return torch.cat(parts) if parts else send[:0]
+        counts = self._io(torch.tensor(send_counts, dtype=torch.int64, device=dev))
         recv_counts = torch.empty_like(counts)
         self.dist.all_to_all_single(recv_counts, counts, group=self.group)
-        rc = recv_counts.tolist()
-        out = torch.empty(sum(rc), dtype=send.dtype, device=dev)
-        self.dist.all_to_all_single(out, send, output_split_sizes=rc, input_split_sizes=list(send_counts),
-                                    group=self.group)
-        return out
+        return self.alltoallv_known(send, send_counts, recv_counts.tolist())
+
+    def alltoallv_known(self, send, send_counts, recv_counts):
+        """alltoallv when every rank already knows its receive counts."""
+        dev = send.device
+        x = self._io(send.contiguous())
+        out = torch.empty(sum(recv_counts), dtype=send.dtype, device=x.device)
+        self.dist.all_to_all_single(out, x, output_split_sizes=list(recv_counts),
+                                    input_split_sizes=list(send_counts), group=self.group)
+        return out.to(dev)
 
     def allgather_object(self, obj):
         out = [None] * self.world

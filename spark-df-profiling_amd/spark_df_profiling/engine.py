@@ -1393,9 +1393,9 @@ class Engine:
                 return self._exchange_bytes(tab) if self.comm.world > 1 else tab
         return self.value_counts_bytes_table(col)
 
-    def value_counts_bytes_table(self, col, row_counts=None, exchanged=False):
+    def value_counts_bytes_table(self, col, row_counts=None, exchanged=False, capacity=None):
         """Global open-addressing byte-key table (fallback / multi-rank path)."""
-        cap = _next_pow2(2 * max(col.length, 1))
+        cap = capacity if capacity is not None else _next_pow2(2 * max(col.length, 1))
         slots, counts = self._table(cap, True, True)
         stats = self._u64(4, zero=True)
         bc = col.sdp_bytes()

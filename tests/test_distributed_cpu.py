@@ -46,7 +46,7 @@ def _worker(rank, world, port, q):
         for part in comm.allgather_object(dict(imgs)):
             imgs.update(part)
         out['images'] = sorted(imgs.items())
-        # alltoallv (gloo emulation): rank r sends (r*10 + d) repeated d+1 times to rank d
+        # alltoallv (all_to_all_single, as on RCCL): rank r sends (r*10 + d) repeated d+1 times to rank d
         send = torch.cat([torch.full((d + 1,), rank * 10 + d, dtype=torch.int64) for d in range(world)])
         out['alltoallv'] = comm.alltoallv(send, [d + 1 for d in range(world)]).tolist()
         # top-k merge: (count desc, key asc), deterministic on every rank

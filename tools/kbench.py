@@ -22,7 +22,8 @@ for r in range(reps):
     if what == 'group':
         e.group(col, col.kind == 'bytes', dense=False)
     elif what == 'table':
-        e._distinct_fixed_table(col) if col.kind != 'bytes' else e.value_counts_bytes_table(col)
+        cap = int(os.environ['KB_CAP']) if os.environ.get('KB_CAP') else None
+        e._distinct_fixed_table(col) if col.kind != 'bytes' else e.value_counts_bytes_table(col, capacity=cap)
     elif what == 'pass1':
         e.numeric_pass1(col)
     elif what == 'pass2':
