@@ -76,17 +76,65 @@ template <typename T> struct alignas(16) Vec16 {
 // Validity bits [idx, idx+cnt) of an Arrow bitmap (cnt <= 32), LSB = row idx.
 __device__ __forceinline__ uint32_t valid_bits(const uint8_t *bm, int64_t bitoff, int64_t idx,
                                                int cnt) {
+    // cnt <= 32 bits from bit bitoff + idx, branch-free: two dword loads from
+    // the 4-byte-aligned base below bm (bitmaps carry >= 8 bytes of padding;
+    // a sliced bitmap's base lies inside its parent) and one alignbit.  A byte
+    // loop here put an s_waitcnt vmcnt(0) inside every tile load, which waited
+    // for the prefetched next tile as well.
     if (bm == nullptr) return cnt >= 32 ? 0xFFFFFFFFu : ((1u << cnt) - 1u);
-    const int64_t b = bitoff + idx;
-    const int64_t byte0 = b >> 3;
-    const int sh = (int)(b & 7);
-    // read 5 bytes max (cnt<=32 plus shift<8 -> <= 39 bits)
-    uint64_t w = 0;
-    const int nbytes = (sh + cnt + 7) >> 3;
-    for (int k = 0; k < nbytes; ++k) w |= (uint64_t)bm[byte0 + k] << (8 * k);
-    w >>= sh;
-    return cnt >= 32 ? (uint32_t)w : (uint32_t)(w & ((1ull << cnt) - 1ull));
+    // (pointer arithmetic, not an integer round trip, so the loads stay
+    // global_load: a pointer rebuilt from an integer becomes a flat load, and
+    // every flat result waits for all LDS traffic too)
+    const uint32_t mis = (uint32_t)((uintptr_t)bm & 3u);
+    const int64_t b = bitoff + idx + (int64_t)mis * 8;
+    const uint32_t *wp = (const uint32_t *)(bm - mis) + (b >> 5);
+    const uint32_t v = __builtin_amdgcn_alignbit(wp[1], wp[0], (uint32_t)(b & 31));
+    return cnt >= 32 ? v : (v & ((1u << cnt) - 1u));
 }
+// Branch-free streaming of 16-byte vectors with their validity bits.  The
+// loads of one vector (values + the two raw validity dwords) are issued with
+// no condition (the index is clamped; vectors past the end get zero bits) and
+// the bits are decoded only when used, so a tile's loads stay in flight while
+// the previous tile is worked on (callers alternate two VecIn sets instead of
+// copying one into the other, which would wait for the loads).
+struct VBits {
+    const uint32_t *base;       // 4-byte aligned base of the bitmap (the values when there is none)
+    int64_t bit0;               // bit index of element 0 from base
+    bool none;                  // no bitmap: every element valid
+};
+__device__ __forceinline__ VBits vbits_init(const uint8_t *bm, int64_t bitoff, const void *values) {
+    VBits b;
+    b.none = bm == nullptr;
+    const uint8_t *p = b.none ? (const uint8_t *)values : bm;
+    const uint32_t mis = (uint32_t)((uintptr_t)p & 3u);
+    b.base = (const uint32_t *)(p - mis);
+    b.bit0 = b.none ? 0 : bitoff + (int64_t)mis * 8;
+    return b;
+}
+template <typename T>
+struct VecIn {
+    static constexpr int VPT = Vec16<T>::N;
+    Vec16<T> v;
+    uint32_t w0, w1, sh;
+    bool in;
+    // vector vi of the column (nvec >= 1 whole vectors)
+    __device__ __forceinline__ void load(const Vec16<T> *vals, const VBits &vb, int64_t vi, int64_t nvec) {
+        in = vi < nvec;
+        const int64_t vc = in ? vi : 0;
+        v = vals[vc];
+        const int64_t b = vb.none ? 0 : vb.bit0 + vc * VPT;
+        const uint32_t *wp = vb.base + (b >> 5);
+        w0 = wp[0];
+        w1 = wp[1];
+        sh = (uint32_t)(b & 31);
+    }
+    __device__ __forceinline__ uint32_t bits(const VBits &vb) const {
+        constexpr uint32_t full = VPT >= 32 ? 0xFFFFFFFFu : ((1u << VPT) - 1u);
+        const uint32_t x = vb.none ? full : (__builtin_amdgcn_alignbit(w1, w0, sh) & full);
+        return in ? x : 0u;
+    }
+};
+
 __device__ __forceinline__ bool valid_bit(const uint8_t *bm, int64_t bitoff, int64_t idx) {
     if (bm == nullptr) return true;
     const int64_t b = bitoff + idx;

@@ -70,8 +70,8 @@ __device__ __forceinline__ BytesRef bytes_at(const sdp_bytes_column &c, int64_t 
 
 // 8 bytes starting at p (any alignment), zero beyond `avail` bytes.
 __device__ __forceinline__ uint64_t load8(const uint8_t *p, int64_t avail) {
-    const uintptr_t a = (uintptr_t)p;
-    const uint32_t *w = (const uint32_t *)(a & ~(uintptr_t)3);
+    const uint32_t a = (uint32_t)((uintptr_t)p & 3u);
+    const uint32_t *w = (const uint32_t *)(p - a);   // pointer arithmetic keeps it a global load
     const int sh = (int)(a & 3) * 8;
     const uint64_t lo = (uint64_t)w[0] | ((uint64_t)w[1] << 32);
     uint64_t v = lo >> sh;

@@ -305,31 +305,6 @@ struct P1Ctx {
     int64_t cap;
 };
 
-// U 16-byte vectors per thread of a grid-strided tile (+ their validity bits).
-// Streaming loops load the NEXT tile into a second VecTile before working on
-// the current one, so a wave always has a tile of loads in flight.
-template <typename T, int U, int NT>
-struct VecTile {
-    static constexpr int VPT = Vec16<T>::N;
-    Vec16<T> v[U];
-    uint32_t vb[U];
-    __device__ __forceinline__ void load(const sdp_column &col, int64_t tile, int64_t nvec) {
-        const Vec16<T> *vals = (const Vec16<T> *)col.d_values;
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-            const int64_t vi = tile * ((int64_t)NT * U) + (int64_t)u * NT + threadIdx.x;
-            if (vi < nvec) {
-                v[u] = vals[vi];
-                vb[u] = valid_bits(col.d_validity, col.validity_bit_offset, vi * VPT, VPT);
-            } else {
-                vb[u] = 0;
-#pragma unroll
-                for (int e = 0; e < VPT; ++e) v[u].v[e] = (T)0;
-            }
-        }
-    }
-};
-
 // One element; every lane of the wave calls this in lockstep (ballots inside).
 // Window counts use the key with skipped elements (null, NaN, padding) mapped
 // to key 0: no skipped element is above a bound or strictly inside a window,
@@ -436,18 +411,35 @@ __global__ void __launch_bounds__(P1_BLOCK, 4) pass1_kernel(sdp_column col, cons
     const int64_t tile_vecs = (int64_t)P1_BLOCK * U;
     const int64_t ntiles = (nvec + tile_vecs - 1) / tile_vecs;
     (void)vals;
-    VecTile<T, U, P1_BLOCK> cur, nxt;
-    if ((int64_t)blockIdx.x < ntiles) cur.load(col, blockIdx.x, nvec);
-    for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
-        const bool more = tile + gridDim.x < ntiles;
-        if (more) nxt.load(col, tile + gridDim.x, nvec);          // next tile in flight
+    // ping-pong tiles: tile i + 1 is loading while tile i is worked on
+    const VBits vbm = vbits_init(col.d_validity, col.validity_bit_offset, col.d_values);
+    VecIn<T> ta[U], tb[U];
+    auto load = [&](VecIn<T> (&x)[U], int64_t tile) {
+#pragma unroll
+        for (int u = 0; u < U; ++u) x[u].load(vals, vbm, tile * tile_vecs + (int64_t)u * P1_BLOCK + threadIdx.x, nvec);
+    };
+    auto work = [&](const VecIn<T> (&x)[U]) {
 #pragma unroll
         for (int u = 0; u < U; ++u) {
+            const uint32_t vbits = x[u].bits(vbm);
 #pragma unroll
-            for (int e = 0; e < VPT; ++e) p1_elem<T, WIN>(st, cx, cur.v[u].v[e], (cur.vb[u] >> e) & 1u);
+            for (int e = 0; e < VPT; ++e) p1_elem<T, WIN>(st, cx, x[u].v.v[e], (vbits >> e) & 1u);
         }
         p1_fold(st);
-        if (more) cur = nxt;
+    };
+    int64_t tile = blockIdx.x;
+    if (tile < ntiles) {
+        load(ta, tile);
+        while (true) {
+            load(tb, tile + gridDim.x);         // past the last tile: clamped, zero bits, never worked on
+            work(ta);
+            tile += gridDim.x;
+            if (tile >= ntiles) break;
+            load(ta, tile + gridDim.x);
+            work(tb);
+            tile += gridDim.x;
+            if (tile >= ntiles) break;
+        }
     }
     // tail elements (n % VPT) by the first wave of block 0
     if (blockIdx.x == 0 && threadIdx.x < WAVE) {
@@ -1066,16 +1058,33 @@ __global__ void __launch_bounds__(P2_BLOCK, 4) pass2_kernel(sdp_column col, doub
     const int64_t tile_vecs = (int64_t)P2_BLOCK * U;
     const int64_t ntiles = (nvec + tile_vecs - 1) / tile_vecs;
     (void)vals;
-    VecTile<T, U, P2_BLOCK> cur, nxt;
-    if ((int64_t)blockIdx.x < ntiles) cur.load(col, blockIdx.x, nvec);
-    for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
-        const bool more = tile + gridDim.x < ntiles;
-        if (more) nxt.load(col, tile + gridDim.x, nvec);          // next tile in flight
+    const VBits vbm = vbits_init(col.d_validity, col.validity_bit_offset, col.d_values);
+    VecIn<T> ta[U], tb[U];
+    auto load = [&](VecIn<T> (&x)[U], int64_t tile) {
 #pragma unroll
-        for (int u = 0; u < U; ++u)
+        for (int u = 0; u < U; ++u) x[u].load(vals, vbm, tile * tile_vecs + (int64_t)u * P2_BLOCK + threadIdx.x, nvec);
+    };
+    auto work = [&](const VecIn<T> (&x)[U]) {
 #pragma unroll
-            for (int e = 0; e < VPT; ++e) p2_elem<T, SMALL, MONO, NB>(st, c, s_hist, cur.v[u].v[e], (cur.vb[u] >> e) & 1u);
-        if (more) cur = nxt;
+        for (int u = 0; u < U; ++u) {
+            const uint32_t vbits = x[u].bits(vbm);
+#pragma unroll
+            for (int e = 0; e < VPT; ++e) p2_elem<T, SMALL, MONO, NB>(st, c, s_hist, x[u].v.v[e], (vbits >> e) & 1u);
+        }
+    };
+    int64_t tile = blockIdx.x;
+    if (tile < ntiles) {
+        load(ta, tile);
+        while (true) {
+            load(tb, tile + gridDim.x);         // next tile in flight (clamped past the end)
+            work(ta);
+            tile += gridDim.x;
+            if (tile >= ntiles) break;
+            load(ta, tile + gridDim.x);
+            work(tb);
+            tile += gridDim.x;
+            if (tile >= ntiles) break;
+        }
     }
     if (blockIdx.x == 0 && threadIdx.x < WAVE) {
         const int64_t i = nvec * VPT + threadIdx.x;
@@ -1183,37 +1192,37 @@ __global__ void __launch_bounds__(P2_BLOCK, 4) pass2_count_kernel(sdp_column col
     const Vec16<T> *vals = (const Vec16<T> *)col.d_values;
     constexpr int U = sizeof(T) >= 8 ? P2_UNROLL : (std::is_same<T, float>::value ? P2_UNROLL / 2 : 1);
     constexpr int64_t TV = (int64_t)P2_BLOCK * U;
-    Vec16<T> cv[U], nv[U];
-    uint32_t cb[U], nbits[U];
-    auto load = [&](int64_t vb, Vec16<T> (&v)[U], uint32_t (&b)[U]) {
+    // ping-pong tiles of this block's whole vectors [v0, v1)
+    const VBits vbm = vbits_init(col.d_validity, col.validity_bit_offset, col.d_values);
+    VecIn<T> ta[U], tb[U];
+    auto load = [&](VecIn<T> (&x)[U], int64_t vb) {
+#pragma unroll
+        for (int u = 0; u < U; ++u) x[u].load(vals, vbm, vb + (int64_t)u * P2_BLOCK + t, v1);
+    };
+    auto work = [&](const VecIn<T> (&x)[U]) {
 #pragma unroll
         for (int u = 0; u < U; ++u) {
-            const int64_t vi = vb + (int64_t)u * P2_BLOCK + t;
-            if (vi < v1) {
-                v[u] = vals[vi];
-                b[u] = valid_bits(col.d_validity, col.validity_bit_offset, vi * VPT, VPT);
-            } else {
-                b[u] = 0;
+            const uint32_t vbits = x[u].bits(vbm);
 #pragma unroll
-                for (int e = 0; e < VPT; ++e) v[u].v[e] = (T)0;
+            for (int e = 0; e < VPT; ++e) {
+                const bool valid = (vbits >> e) & 1u;
+                p2_elem<T, SMALL, MONO, NB>(st, c, s_hist, x[u].v.v[e], valid);
+                count(x[u].v.v[e], valid);
             }
         }
     };
-    if (v0 < v1) load(v0, cv, cb);
-    for (int64_t vb = v0; vb < v1; vb += TV) {
-        const bool more = vb + TV < v1;
-        if (more) load(vb + TV, nv, nbits);            // next tile in flight
-#pragma unroll
-        for (int u = 0; u < U; ++u)
-#pragma unroll
-            for (int e = 0; e < VPT; ++e) {
-                const bool valid = (cb[u] >> e) & 1u;
-                p2_elem<T, SMALL, MONO, NB>(st, c, s_hist, cv[u].v[e], valid);
-                count(cv[u].v[e], valid);
-            }
-        if (more) {
-#pragma unroll
-            for (int u = 0; u < U; ++u) { cv[u] = nv[u]; cb[u] = nbits[u]; }
+    int64_t vb = v0;
+    if (vb < v1) {
+        load(ta, vb);
+        while (true) {
+            load(tb, vb + TV);
+            work(ta);
+            vb += TV;
+            if (vb >= v1) break;
+            load(ta, vb + TV);
+            work(tb);
+            vb += TV;
+            if (vb >= v1) break;
         }
     }
     if (r1 == n && t < WAVE) {                         // the column's last n % VPT rows (last block)

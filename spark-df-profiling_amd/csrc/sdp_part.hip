@@ -75,8 +75,8 @@ __device__ __forceinline__ int64_t str_off(const sdp_bytes_column &c, int64_t ro
 // buffer is padded by 16 bytes), zero beyond `avail`
 __device__ __forceinline__ uint64_t gload8(const uint8_t *p, int64_t avail) {
     if (avail <= 0) return 0ull;
-    const uintptr_t a = (uintptr_t)p;
-    const uint32_t *w = (const uint32_t *)(a & ~(uintptr_t)3);
+    const uint32_t a = (uint32_t)((uintptr_t)p & 3u);
+    const uint32_t *w = (const uint32_t *)(p - a);   // pointer arithmetic keeps it a global load
     const uint32_t sh = (uint32_t)(a & 3);
     const uint32_t w0 = w[0], w1 = w[1], w2 = w[2];
     const uint64_t v = (uint64_t)__builtin_amdgcn_alignbyte(w1, w0, sh) |
@@ -179,37 +179,34 @@ __device__ __forceinline__ uint64_t fetch_key(const sdp_column &c, int64_t i, bo
 template <typename T, int NT, int RPT>
 struct RowTile {
     static constexpr bool VEC = !std::is_same<T, bool>::value;
+    using VT = typename std::conditional<VEC, T, uint8_t>::type;
     static constexpr int VPT = VEC ? Vec16<T>::N : 1;
     static constexpr int NV = VEC ? (RPT / VPT > 0 ? RPT / VPT : 1) : 1;
-    Vec16<typename std::conditional<VEC, T, uint8_t>::type> v[NV];
-    uint32_t vb[NV];
+    VecIn<VT> v[NV];            // values + raw validity words, decoded in hash()
     bool full;
 
-    __device__ __forceinline__ void load(const sdp_column &c, int64_t base, int64_t end) {
+    __device__ __forceinline__ void load(const sdp_column &c, const VBits &vbm, int64_t base, int64_t end) {
         full = VEC && (RPT % VPT == 0) && base + (int64_t)NT * RPT <= end && (base % VPT) == 0;
         if (!full) return;
-        const Vec16<typename std::conditional<VEC, T, uint8_t>::type> *vals =
-            (const Vec16<typename std::conditional<VEC, T, uint8_t>::type> *)c.d_values;
+        const Vec16<VT> *vals = (const Vec16<VT> *)c.d_values;
 #pragma unroll
-        for (int u = 0; u < NV; ++u) {
-            const int64_t vi = base / VPT + (int64_t)u * NT + threadIdx.x;
-            v[u] = vals[vi];
-            vb[u] = valid_bits(c.d_validity, c.validity_bit_offset, vi * VPT, VPT);
-        }
+        for (int u = 0; u < NV; ++u) v[u].load(vals, vbm, base / VPT + (int64_t)u * NT + threadIdx.x, INT64_MAX);
     }
-    __device__ __forceinline__ void hash(const sdp_column &c, int64_t base, int64_t end, uint64_t (&h)[RPT],
-                                         uint32_t &vmask) const {
+    __device__ __forceinline__ void hash(const sdp_column &c, const VBits &vbm, int64_t base, int64_t end,
+                                         uint64_t (&h)[RPT], uint32_t &vmask) const {
         vmask = 0;
         if constexpr (VEC) {
             if (full) {
 #pragma unroll
-                for (int u = 0; u < NV; ++u)
+                for (int u = 0; u < NV; ++u) {
+                    const uint32_t vb = v[u].bits(vbm);
 #pragma unroll
                     for (int e = 0; e < VPT; ++e) {
                         const int q = u * VPT + e;
-                        h[q] = mix64(key_of<T>(v[u].v[e]));
-                        vmask |= ((vb[u] >> e) & 1u) << q;
+                        h[q] = mix64(key_of<T>(v[u].v.v[e]));
+                        vmask |= ((vb >> e) & 1u) << q;
                     }
+                }
                 return;
             }
         }
@@ -267,11 +264,12 @@ __global__ void __launch_bounds__(CT) part_count_rows_u64_kernel(sdp_column col,
     uint64_t rows = 0, special = 0;
     const bool any_heavy = heavy.n > 0;
     RowTile<T, CT, C_RPT> tile;
+    const VBits vbm = vbits_init(col.d_validity, col.validity_bit_offset, col.d_values);
     for (int64_t base = r0; base < r1; base += CT * C_RPT) {
         uint64_t h[C_RPT];
         uint32_t vmask;
-        tile.load(col, base, r1);
-        tile.hash(col, base, r1, h, vmask);
+        tile.load(col, vbm, base, r1);
+        tile.hash(col, vbm, base, r1, h, vmask);
 #pragma unroll
         for (int q = 0; q < C_RPT; ++q) {
             if ((vmask >> q) & 1u) {
@@ -308,12 +306,13 @@ __global__ void __launch_bounds__(ST) part_scatter_rows_u64_kernel(sdp_column co
     lds_barrier();
     const bool any_heavy = heavy.n > 0;
     RowTile<T, ST, S_RPT> tile;
-    if (r0 < r1) tile.load(col, r0, r1);
+    const VBits vbm = vbits_init(col.d_validity, col.validity_bit_offset, col.d_values);
+    if (r0 < r1) tile.load(col, vbm, r0, r1);
     for (int64_t base = r0; base < r1; base += S_TILE) {
         uint64_t h[S_RPT];
         uint32_t vmask;
-        tile.hash(col, base, r1, h, vmask);
-        if (base + S_TILE < r1) tile.load(col, base + S_TILE, r1);      // next tile in flight
+        tile.hash(col, vbm, base, r1, h, vmask);
+        if (base + S_TILE < r1) tile.load(col, vbm, base + S_TILE, r1);      // next tile in flight
         uint32_t rank[S_RPT];
         uint32_t keep = 0;
 #pragma unroll
@@ -377,59 +376,6 @@ __device__ __forceinline__ uint64_t mask_bytes(uint64_t v, int64_t avail) {
     return avail <= 0 ? 0ull : (avail >= 8 ? v : (v & ((1ull << (8 * avail)) - 1ull)));
 }
 
-// The records of this thread's RPT rows of a byte tile (row = base + q*NT + t),
-// equal to bytes_record's.  Every load of the tile is issued before any value
-// is used -- validity and offsets first, then the <= 16 key bytes of each short
-// string as the <= 5 aligned dwords covering them -- so a tile costs about two
-// memory latencies instead of two per row.
-template <int NT, int RPT>
-__device__ __forceinline__ void bytes_tile(const sdp_bytes_column &col, int64_t base, int64_t end,
-                                           uint64_t (&k0)[RPT], uint64_t (&k1)[RPT], uint64_t (&meta)[RPT],
-                                           uint64_t (&h)[RPT], uint32_t &vmask) {
-    const int t = threadIdx.x;
-    int64_t o0[RPT], o1[RPT];
-    vmask = 0;
-#pragma unroll
-    for (int q = 0; q < RPT; ++q) {
-        const int64_t row = base + (int64_t)q * NT + t;
-        const bool ok = row < end && valid_bit(col.d_validity, col.validity_bit_offset, row);
-        vmask |= (uint32_t)ok << q;
-        o0[q] = ok ? str_off(col, row) : 0;
-        o1[q] = ok ? str_off(col, row + 1) : 0;
-    }
-    uint32_t w[RPT][5];
-#pragma unroll
-    for (int q = 0; q < RPT; ++q) {
-        const int64_t len = o1[q] - o0[q];
-        const uintptr_t a = (uintptr_t)(col.d_data + o0[q]);
-        const uint32_t *p = (const uint32_t *)(a & ~(uintptr_t)3);
-        const int64_t need = len <= SHORT_MAX ? (int64_t)((a & 3) + len + 3) >> 2 : 0;   // dwords covering the key
-#pragma unroll
-        for (int k = 0; k < 5; ++k) w[q][k] = (((vmask >> q) & 1u) && k < need) ? p[k] : 0u;
-    }
-#pragma unroll
-    for (int q = 0; q < RPT; ++q) {
-        k0[q] = k1[q] = meta[q] = h[q] = 0;
-        if (!((vmask >> q) & 1u)) continue;
-        const int64_t row = base + (int64_t)q * NT + t;
-        const int64_t len = o1[q] - o0[q];
-        if (len <= SHORT_MAX) {
-            const uint32_t sh = (uint32_t)((uintptr_t)(col.d_data + o0[q]) & 3);
-            const uint64_t v0 = (uint64_t)__builtin_amdgcn_alignbyte(w[q][1], w[q][0], sh) |
-                                ((uint64_t)__builtin_amdgcn_alignbyte(w[q][2], w[q][1], sh) << 32);
-            const uint64_t v1 = (uint64_t)__builtin_amdgcn_alignbyte(w[q][3], w[q][2], sh) |
-                                ((uint64_t)__builtin_amdgcn_alignbyte(w[q][4], w[q][3], sh) << 32);
-            k0[q] = mask_bytes(v0, len);
-            k1[q] = mask_bytes(v1, len - 8);
-            h[q] = bh_short(k0[q], k1[q], (uint64_t)len);
-        } else {
-            h[q] = hash_long_global(col.d_data + o0[q], len);
-            k0[q] = h[q];
-        }
-        meta[q] = ((uint64_t)min((int64_t)LEN_MAX, len) << 40) | (uint64_t)(row + 1);
-    }
-}
-
 // The same tile in two stages, so a kernel can issue the NEXT tile's validity
 // and offsets (stage A) before it fetches this tile's key bytes (stage B, which
 // depends on A) and works on them: one memory latency per tile instead of two.
@@ -452,18 +398,23 @@ __device__ __forceinline__ void bytes_tile_a(const sdp_bytes_column &col, int64_
         a.o1[q] = ok ? str_off(col, row + 1) : 0;
     }
 }
+
 template <int NT, int RPT>
 __device__ __forceinline__ void bytes_tile_b(const sdp_bytes_column &col, int64_t base, const BytesOffs<RPT> &a,
                                              uint64_t (&k0)[RPT], uint64_t (&k1)[RPT], uint64_t (&meta)[RPT],
                                              uint64_t (&h)[RPT]) {
+    // (a wave-cooperative variant -- each wave's span of key bytes read as
+    // coalesced 16-byte chunks and handed to the lanes by ds_bpermute -- was
+    // measured 12 % slower on the count pass: 8.8 -> 9.9 ms per 1e9 rows)
     const int t = threadIdx.x;
     uint32_t w[RPT][5];
 #pragma unroll
     for (int q = 0; q < RPT; ++q) {
         const int64_t len = a.o1[q] - a.o0[q];
-        const uintptr_t ad = (uintptr_t)(col.d_data + a.o0[q]);
-        const uint32_t *p = (const uint32_t *)(ad & ~(uintptr_t)3);
-        const int64_t need = len <= SHORT_MAX ? (int64_t)((ad & 3) + len + 3) >> 2 : 0;
+        const uint8_t *pb = col.d_data + a.o0[q];
+        const uint32_t ad = (uint32_t)((uintptr_t)pb & 3u);
+        const uint32_t *p = (const uint32_t *)(pb - ad);
+        const int64_t need = len <= SHORT_MAX ? (int64_t)(ad + len + 3) >> 2 : 0;
 #pragma unroll
         for (int k = 0; k < 5; ++k) w[q][k] = (((a.vmask >> q) & 1u) && k < need) ? p[k] : 0u;
     }
