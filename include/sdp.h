@@ -392,6 +392,18 @@ int sdp_part_rows(const sdp_column *col, const sdp_bytes_column *bcol, const sdp
                   int32_t b1, int32_t phase, uint32_t *d_hist, const uint64_t *d_offsets,
                   const sdp_records *d_out, uint64_t *d_heavy_counts, uint64_t *d_stats,
                   void *stream);
+/* Byte columns, one read of the strings (replaces sdp_part_rows phase 0 + 1 for
+ * bcol): every wave of every workgroup compacts the records of its strip of
+ * rows to d_out at the strip's first row position (d_out holds length records),
+ * counts the strip's level-1 buckets into d_hist[b * nchunks + chunk] and
+ * writes d_chunks[chunk] = {strip start, start + records, chunk, nchunks};
+ * heavy counts and d_stats[0] as sdp_part_rows phase 0.  The level-1 scatter
+ * is then sdp_part_recs(d_out, 1, d_chunks, nchunks, 0, b1, 1, ...) with the
+ * exclusive scan of d_hist.  nchunks = sdp_part_records_chunks(length). */
+int64_t sdp_part_records_chunks(int64_t length);
+int sdp_part_rows_records(const sdp_bytes_column *bcol, const sdp_heavy *heavy, int32_t b1,
+                          uint32_t *d_hist, sdp_chunk *d_chunks, const sdp_records *d_out,
+                          uint64_t *d_heavy_counts, uint64_t *d_stats, void *stream);
 /* L1 records -> sub-buckets by hash bits [64-b1-b2, 64-b1). */
 int sdp_part_recs(const sdp_records *in, int32_t is_bytes, const sdp_chunk *d_chunks,
                   int64_t nchunks, int32_t b1, int32_t b2, int32_t phase, uint32_t *d_hist,

@@ -381,36 +381,36 @@ __device__ __forceinline__ uint64_t mask_bytes(uint64_t v, int64_t avail) {
 // depends on A) and works on them: one memory latency per tile instead of two.
 template <int RPT>
 struct BytesOffs {
-    int64_t o0[RPT], o1[RPT];
+    int64_t o0[RPT];
+    uint32_t ln[RPT];                   // string length (strings of >= 4 GiB are not supported)
     uint32_t vmask;
 };
 template <int NT, int RPT>
 __device__ __forceinline__ void bytes_tile_a(const sdp_bytes_column &col, int64_t base, int64_t end,
-                                             BytesOffs<RPT> &a) {
-    const int t = threadIdx.x;
+                                             BytesOffs<RPT> &a, int t) {
     a.vmask = 0;
 #pragma unroll
     for (int q = 0; q < RPT; ++q) {
         const int64_t row = base + (int64_t)q * NT + t;
         const bool ok = row < end && valid_bit(col.d_validity, col.validity_bit_offset, row);
         a.vmask |= (uint32_t)ok << q;
-        a.o0[q] = ok ? str_off(col, row) : 0;
-        a.o1[q] = ok ? str_off(col, row + 1) : 0;
+        const int64_t b0 = ok ? str_off(col, row) : 0;
+        a.o0[q] = b0;
+        a.ln[q] = ok ? (uint32_t)(str_off(col, row + 1) - b0) : 0u;
     }
 }
 
 template <int NT, int RPT>
 __device__ __forceinline__ void bytes_tile_b(const sdp_bytes_column &col, int64_t base, const BytesOffs<RPT> &a,
                                              uint64_t (&k0)[RPT], uint64_t (&k1)[RPT], uint64_t (&meta)[RPT],
-                                             uint64_t (&h)[RPT]) {
+                                             uint64_t (&h)[RPT], int t) {
     // (a wave-cooperative variant -- each wave's span of key bytes read as
     // coalesced 16-byte chunks and handed to the lanes by ds_bpermute -- was
     // measured 12 % slower on the count pass: 8.8 -> 9.9 ms per 1e9 rows)
-    const int t = threadIdx.x;
     uint32_t w[RPT][5];
 #pragma unroll
     for (int q = 0; q < RPT; ++q) {
-        const int64_t len = a.o1[q] - a.o0[q];
+        const int64_t len = a.ln[q];
         const uint8_t *pb = col.d_data + a.o0[q];
         const uint32_t ad = (uint32_t)((uintptr_t)pb & 3u);
         const uint32_t *p = (const uint32_t *)(pb - ad);
@@ -423,7 +423,7 @@ __device__ __forceinline__ void bytes_tile_b(const sdp_bytes_column &col, int64_
         k0[q] = k1[q] = meta[q] = h[q] = 0;
         if (!((a.vmask >> q) & 1u)) continue;
         const int64_t row = base + (int64_t)q * NT + t;
-        const int64_t len = a.o1[q] - a.o0[q];
+        const int64_t len = a.ln[q];
         if (len <= SHORT_MAX) {
             const uint32_t sh = (uint32_t)((uintptr_t)(col.d_data + a.o0[q]) & 3);
             const uint64_t v0 = (uint64_t)__builtin_amdgcn_alignbyte(w[q][1], w[q][0], sh) |
@@ -472,12 +472,12 @@ __global__ void __launch_bounds__(B_CT) part_count_rows_bytes_kernel(sdp_bytes_c
     uint64_t rows = 0;
     constexpr int64_t STEP = (int64_t)B_CT * B_C_RPT;
     BytesOffs<B_C_RPT> oc, on;
-    if (r0 < r1) bytes_tile_a<B_CT, B_C_RPT>(col, r0, r1, oc);
+    if (r0 < r1) bytes_tile_a<B_CT, B_C_RPT>(col, r0, r1, oc, t);
     for (int64_t base = r0; base < r1; base += STEP) {
         uint64_t k0[B_C_RPT], k1[B_C_RPT], meta[B_C_RPT], h[B_C_RPT];
         const bool more = base + STEP < r1;
-        if (more) bytes_tile_a<B_CT, B_C_RPT>(col, base + STEP, r1, on);   // next tile's offsets in flight
-        bytes_tile_b<B_CT, B_C_RPT>(col, base, oc, k0, k1, meta, h);
+        if (more) bytes_tile_a<B_CT, B_C_RPT>(col, base + STEP, r1, on, t);   // next tile's offsets in flight
+        bytes_tile_b<B_CT, B_C_RPT>(col, base, oc, k0, k1, meta, h, t);
         const uint32_t vmask = oc.vmask;
         if (more) oc = on;
 #pragma unroll
@@ -513,17 +513,17 @@ __global__ void __launch_bounds__(B_ST) part_scatter_rows_bytes_kernel(sdp_bytes
     }
     lds_barrier();
     BytesOffs<B_S_RPT> oc, on;
-    if (r0 < r1) bytes_tile_a<B_ST, B_S_RPT>(col, r0, r1, oc);
+    if (r0 < r1) bytes_tile_a<B_ST, B_S_RPT>(col, r0, r1, oc, t);
     for (int64_t base = r0; base < r1; base += B_S_TILE) {
         uint64_t k0[B_S_RPT], k1[B_S_RPT], meta[B_S_RPT], h[B_S_RPT];
         uint32_t rank[B_S_RPT];
         int bk[B_S_RPT];
         uint32_t keep = 0;
         const bool more = base + B_S_TILE < r1;
-        bytes_tile_b<B_ST, B_S_RPT>(col, base, oc, k0, k1, meta, h);
+        bytes_tile_b<B_ST, B_S_RPT>(col, base, oc, k0, k1, meta, h, t);
         const uint32_t vmask = oc.vmask;
         // the next tile's offsets fly during this tile's LDS phases
-        if (more) bytes_tile_a<B_ST, B_S_RPT>(col, base + B_S_TILE, r1, on);
+        if (more) bytes_tile_a<B_ST, B_S_RPT>(col, base + B_S_TILE, r1, on, t);
 #pragma unroll
         for (int q = 0; q < B_S_RPT; ++q) {
             if ((vmask >> q) & 1u) {
@@ -573,6 +573,82 @@ __global__ void __launch_bounds__(B_ST) part_scatter_rows_bytes_kernel(sdp_bytes
 struct Chunk {
     int64_t start, end, hbase, hstride;
 };
+
+// ---- byte rows -> compacted records (one read of the strings) ----------------------
+// The string bytes are the expensive read of a byte column (offsets, then
+// unaligned key words, then the hash).  Counting level-1 buckets in one pass and
+// scattering in a second would read them twice; instead every wave turns its
+// own strip of rows into records written contiguously from the strip's first
+// row position (ballot + mbcnt compaction, no atomics), counts their level-1
+// buckets in a wave-private LDS histogram, and publishes its strip as a Chunk.
+// part_scatter_recs_kernel<true> (b1 = 0, b2 = level-1 bits) then moves the
+// records -- 24 B each, sequential reads -- into their buckets.  Heavy keys are
+// counted in LDS and never become records, as in the other row kernels.
+constexpr int BR_T = 256;                   // 4 waves, one strip each (<= 128 VGPRs: the
+                                            // 1024-block grid is resident in one round)
+constexpr int BR_W = BR_T / WAVE;
+constexpr int BR_RPT = 4;                   // rows per lane per tile
+
+struct BRecLds {
+    HeavyLdsT<true> heavy;
+    uint32_t hist[BR_W][MAXB];
+};
+
+__global__ void __launch_bounds__(BR_T, 4) part_records_rows_bytes_kernel(sdp_bytes_column col, HeavyArg heavy, int b1,
+                                                                       int64_t rows_per_block, uint32_t *hist,
+                                                                       Chunk *chunks, uint64_t *out_k0,
+                                                                       uint64_t *out_k1, uint64_t *out_meta,
+                                                                       uint64_t *heavy_counts, uint64_t *stats) {
+    __shared__ BRecLds s;
+    const int G = gridDim.x, g = blockIdx.x, t = threadIdx.x;
+    const int lane = lane_id(), w = t / WAVE;
+    const int nb = 1 << b1;
+    const int shift = 64 - b1;
+    const int64_t rpw = rows_per_block / BR_W;                     // a multiple of WAVE * BR_RPT
+    const int64_t s0 = min(col.length, (int64_t)g * rows_per_block + (int64_t)w * rpw);
+    const int64_t s1 = min(col.length, s0 + rpw);
+    heavy_build<true>(s.heavy, heavy);
+    for (int b = lane; b < nb; b += WAVE) s.hist[w][b] = 0;
+    lds_barrier();
+    uint64_t rows = 0;
+    int64_t cur = s0;                                               // next record slot of this strip
+    constexpr int64_t STEP = (int64_t)WAVE * BR_RPT;
+    BytesOffs<BR_RPT> oc, on;
+    if (s0 < s1) bytes_tile_a<WAVE, BR_RPT>(col, s0, s1, oc, lane);
+    for (int64_t base = s0; base < s1; base += STEP) {
+        uint64_t k0[BR_RPT], k1[BR_RPT], meta[BR_RPT], h[BR_RPT];
+        const bool more = base + STEP < s1;
+        if (more) bytes_tile_a<WAVE, BR_RPT>(col, base + STEP, s1, on, lane);   // next tile's offsets in flight
+        bytes_tile_b<WAVE, BR_RPT>(col, base, oc, k0, k1, meta, h, lane);
+        const uint32_t vmask = oc.vmask;
+        if (more) oc = on;
+#pragma unroll
+        for (int q = 0; q < BR_RPT; ++q) {
+            bool keep = false;
+            if ((vmask >> q) & 1u) {
+                ++rows;
+                const int hv = heavy_find_bytes(s.heavy, heavy.n, h[q], k0[q], k1[q], (uint32_t)(meta[q] >> 40));
+                if (hv >= 0) atomicAdd(&s.heavy.cnt[hv], 1u);
+                else keep = true;
+            }
+            const uint64_t m = __ballot(keep);
+            if (keep) {
+                const int64_t o = cur + lane_rank(m);
+                out_k0[o] = k0[q];
+                out_k1[o] = k1[q];
+                out_meta[o] = meta[q];
+                atomicAdd(&s.hist[w][b1 ? (int)(h[q] >> shift) : 0], 1u);
+            }
+            cur += __popcll(m);
+        }
+    }
+    const int64_t C = (int64_t)G * BR_W, c = (int64_t)g * BR_W + w;
+    lds_barrier();
+    for (int b = lane; b < nb; b += WAVE) hist[(int64_t)b * C + c] = s.hist[w][b];
+    if (lane == 0) chunks[c] = Chunk{s0, cur, c, C};
+    heavy_flush(s.heavy, heavy.n, heavy_counts);
+    block_add_u64(rows, &stats[0]);
+}
 
 template <bool BYTES>
 __global__ void __launch_bounds__(CT) part_count_recs_kernel(const uint64_t *in_k0, const uint64_t *in_k1,
@@ -1318,6 +1394,36 @@ int sdp_part_rows(const sdp_column *col, const sdp_bytes_column *bcol, const sdp
     default: return set_error(SDP_EINVAL, "part_rows: dtype %d", c.dtype);
     }
     return check_launch("part_rows_u64_kernel");
+}
+
+int64_t sdp_part_records_chunks(int64_t length) {
+    const int64_t rpb = sdp_part_rows_per_block(length, 1);
+    const int64_t grid = (length + rpb - 1) / rpb;
+    return (grid < 1 ? 1 : grid) * BR_W;
+}
+
+int sdp_part_rows_records(const sdp_bytes_column *bcol, const sdp_heavy *heavy, int32_t b1, uint32_t *d_hist,
+                          sdp_chunk *d_chunks, const sdp_records *d_out, uint64_t *d_heavy_counts, uint64_t *d_stats,
+                          void *stream) {
+    if (bcol == nullptr || b1 < 0 || b1 > 10 || d_hist == nullptr || d_chunks == nullptr || d_stats == nullptr ||
+        d_out == nullptr || d_out->d_k0 == nullptr || d_out->d_k1 == nullptr || d_out->d_meta == nullptr)
+        return set_error(SDP_EINVAL, "part_rows_records: args");
+    if (bcol->length >= (int64_t)RMASK40) return set_error(SDP_EINVAL, "part_rows_records: more than 2^40 rows");
+    HeavyArg hv{nullptr, nullptr, nullptr, nullptr, 0};
+    if (heavy && heavy->n > 0) {
+        if (heavy->n > HEAVY_MAX)
+            return set_error(SDP_EINVAL, "part_rows_records: %d heavy keys > %d", heavy->n, HEAVY_MAX);
+        hv = HeavyArg{heavy->d_h, heavy->d_k0, heavy->d_k1, heavy->d_meta, heavy->n};
+        if (hv.k0 == nullptr || hv.k1 == nullptr || hv.meta == nullptr || d_heavy_counts == nullptr)
+            return set_error(SDP_EINVAL, "part_rows_records: byte heavy keys need k0/k1/meta and counts");
+    }
+    const int64_t n = bcol->length;
+    const int64_t rpb = sdp_part_rows_per_block(n, 1);
+    const int grid = (int)((n + rpb - 1) / rpb < 1 ? 1 : (n + rpb - 1) / rpb);
+    hipLaunchKernelGGL(part_records_rows_bytes_kernel, dim3(grid), dim3(BR_T), 0, (hipStream_t)stream, *bcol, hv, b1,
+                       rpb, d_hist, (Chunk *)d_chunks, d_out->d_k0, d_out->d_k1, d_out->d_meta, d_heavy_counts,
+                       d_stats);
+    return check_launch("part_records_rows_bytes_kernel");
 }
 
 int sdp_part_recs(const sdp_records *in, int32_t is_bytes, const sdp_chunk *d_chunks, int64_t nchunks, int32_t b1,

@@ -21,6 +21,7 @@ Reference call sites replaced (all /root/reference/spark_df_profiling/):
 from __future__ import annotations
 
 import ctypes
+import os
 import math
 from fractions import Fraction
 from dataclasses import dataclass, field
@@ -45,6 +46,9 @@ U64 = (1 << 64) - 1
 PART_SAMPLE = 16384          # rows sampled for heavy keys (sdp_part_sample)
 HEAVY_MIN = 3                # sample occurrences that make a key heavy
 PART_CHUNK = 65536           # level-2 records per workgroup chunk
+# byte columns: strings read once into compacted records, then a record scatter
+# (SDP_BYTES_TWO_READS=1: the count + re-read scatter of round 1, for A/B runs)
+BYTES_ONE_READ = os.environ.get('SDP_BYTES_TWO_READS', '0') != '1'
 CAND_FULL_BUDGET = 1 << 30   # bytes of room-for-every-row candidate slots per pass-1 batch
 
 # Test knob for the quantile edge paths (never set in production):
@@ -936,12 +940,16 @@ class Engine:
         else:
             hn = h.cpu().numpy().view(np.uint64)
         pos = np.nonzero(hn != np.uint64(U64))[0]
+        n_valid = pos.size
         if isb and pos.size:
             pos = pos[(meta[pos] >> np.uint64(40)) <= np.uint64(16)]
         if pos.size == 0:
             return None
         u, first, cnt = np.unique(hn[pos], return_index=True, return_counts=True)
-        return self._heavy_struct(u, cnt, first, pos, keep, isb, meta)
+        hv = self._heavy_struct(u, cnt, first, pos, keep, isb, meta)
+        if hv is not None:        # sampled share of rows that become partition records
+            hv['rec_frac'] = (n_valid - hv['heavy_rows']) / float(len(hn))
+        return hv
 
     def _heavy_struct(self, u, cnt, first=None, pos=None, keep=None, isb=False, meta=None):
         """Heavy keys (>= HEAVY_MIN sample occurrences, at most HEAVY_MAX by
@@ -954,7 +962,7 @@ class Engine:
         if sel.size > nat.HEAVY_MAX:
             sel = sel[np.argsort(-cnt[sel], kind='stable')[:nat.HEAVY_MAX]]
         hv = {'h': self._h2d(u[sel].view(np.int64).copy()), 'n': int(sel.size),
-              'h_host': [int(x) for x in u[sel].tolist()]}
+              'h_host': [int(x) for x in u[sel].tolist()], 'heavy_rows': int(cnt[sel].sum())}
         if isb:
             rows = pos[first[sel]]
             hv['meta_host'] = [int(x) for x in meta[rows].tolist()]
@@ -1018,7 +1026,14 @@ class Engine:
         with_counts = with_counts or isb
         n = col.length
         target = sdp.sdp_part_bucket_target(int(isb), int(with_counts))
-        total_bits = max(0, math.ceil(math.log2(max(1.0, n / target))))
+        hv = self._heavy_keys(col, isb)
+        n_rec = n
+        if isb and hv is not None and 'rec_frac' in hv:
+            # byte columns: size the buckets for the records the sample predicts
+            # (heavy keys never become records), with margin; fewer hash bits
+            # mean longer runs per bucket in both scatters
+            n_rec = min(n, int(n * (1.25 * hv['rec_frac'] + 0.02)) + 1)
+        total_bits = max(0, math.ceil(math.log2(max(1.0, n_rec / target))))
         large = False
         if total_bits > 20 and not isb and not with_counts:
             # > 2^30 rows: 4x larger final buckets on the workgroup-table kernel
@@ -1029,19 +1044,32 @@ class Engine:
         if b2 > 10:
             return None
         nb1, nb2 = 1 << b1, 1 << b2
-        hv = self._heavy_keys(col, isb)
         rpb = sdp.sdp_part_rows_per_block(n, int(isb))
         grid = max(1, -(-n // rpb))
+        if isb and BYTES_ONE_READ and b1 > 0:
+            grid = sdp.sdp_part_records_chunks(n)           # one level-1 histogram per wave strip
         return {'col': col, 'isb': isb, 'with_counts': with_counts, 'large': large, 'b1': b1, 'b2': b2,
                 'nb1': nb1, 'nb2': nb2, 'stats': self._u64(68, zero=True), 'cs': None if isb else col.sdp(),
                 'bc': col.sdp_bytes() if isb else None, 'hv': hv,
                 'hcnt': self._u64(max(hv['n'] if hv else 1, 1), zero=True), 'grid': grid,
                 'h1': torch.empty(nb1 * grid, dtype=torch.int32, device=self.device),
-                'rb': col_read_bytes(col), 'recw': 24 if isb else 8}
+                'rb': col_read_bytes(col), 'recw': 24 if isb else 8,
+                'one_read': isb and BYTES_ONE_READ and b1 > 0}
 
     def _group_count(self, ctx):
-        """Level-1 bucket counts (sdp_part_rows phase 0)."""
+        """Level-1 bucket counts (sdp_part_rows phase 0).  Byte columns
+        (one_read): the strings are read once, into compacted per-strip
+        records that _group_middle scatters (sdp_part_rows_records)."""
         col, isb, hv = ctx['col'], ctx['isb'], ctx['hv']
+        if ctx['one_read']:
+            r0, keep0 = self._records(col.length, True)
+            chunks = torch.empty((ctx['grid'], 4), dtype=torch.int64, device=self.device)
+            nat.annotate(_label(col, 'records'), ctx['rb'])
+            sdp.sdp_part_rows_records(ctypes.byref(ctx['bc']), ctypes.byref(hv['struct']) if hv else None,
+                                      ctx['b1'], ptr(ctx['h1']), ptr(chunks), ctypes.byref(r0), ptr(ctx['hcnt']),
+                                      ptr(ctx['stats']), self._s())
+            ctx.update({'r0': r0, 'keep0': keep0, 'chunks0': chunks})
+            return
         nat.annotate(_label(col, 'count'), ctx['rb'])
         sdp.sdp_part_rows(self._gref(ctx), ctypes.byref(ctx['bc']) if isb else None,
                           ctypes.byref(hv['struct']) if hv else None, ctx['b1'], 0, ptr(ctx['h1']), None, None,
@@ -1080,7 +1108,13 @@ class Engine:
         hvref = ctypes.byref(hv['struct']) if hv else None
         nrec = int(bsn[-1])
         r1, keep1 = self._records(nrec, isb)
-        if nrec:
+        if ctx.get('one_read'):
+            if nrec:                  # level-1 scatter of the compacted strip records (sequential 24-byte reads)
+                nat.annotate('bytes/l1scatter', 2 * nrec * recw)
+                sdp.sdp_part_recs(ctypes.byref(ctx['r0']), 1, ptr(ctx['chunks0']), grid, 0, b1, 1, None, ptr(o1),
+                                  ctypes.byref(r1), s)
+            del ctx['r0'], ctx['keep0'], ctx['chunks0']
+        elif nrec:
             nat.annotate(_label(col, 'scatter'), rb + nrec * recw)
             sdp.sdp_part_rows(cref, bref, hvref, b1, 1, None, ptr(o1), ctypes.byref(r1), ptr(hcnt), ptr(stats), s)
         # level 2: each L1 bucket -> nb2 sub-buckets, chunk by chunk

@@ -83,6 +83,13 @@ def test_part_argument_checks_without_gpu():
         _native.sdp.sdp_scan_u32(None, 0, None, None, 0, None)
     assert _native.sdp.sdp_part_rows_per_block(10 ** 9, 0) % 4096 == 0
     assert _native.sdp.sdp_part_bucket_target(1, 1) == 2048
+    with pytest.raises(_native.NativeError, match='part_rows_records'):
+        _native.sdp.sdp_part_rows_records(None, None, 4, None, None, None, None, None, None)
+    # one chunk per wave strip: 4 per workgroup of the byte-row grid
+    n = 10 ** 9
+    rpb = _native.sdp.sdp_part_rows_per_block(n, 1)
+    assert _native.sdp.sdp_part_records_chunks(n) == 4 * (-(-n // rpb))
+    assert rpb % 1024 == 0
 
 
 def test_select_rounds_host_arithmetic():
