@@ -1059,7 +1059,26 @@ __global__ void __launch_bounds__(WV_W * WAVE) part_dedup_u64_wave_kernel(const 
 //   its record into the slot    3. everyone compares bytes and counts.
 // Different strings with equal 64-bit hashes raise stats[2] (the caller then
 // recounts the column on the exact global-table path).
+// One workgroup (144 KB of LDS) per CU: the first round of the workgroup's NEXT
+// bucket is loaded before the current bucket is grouped, so the bucket's memory
+// latency overlaps the LDS phases instead of idling the CU (the hash is
+// recomputed at use, which keeps both rounds within the 128-VGPR budget of a
+// 1024-thread workgroup); group slots are handed out one LDS atomic per wave.
 constexpr int D_RPT = 4;
+struct DRound {
+    uint64_t k0[D_RPT], k1[D_RPT], meta[D_RPT];
+};
+__device__ __forceinline__ void dedup_load_round(DRound &r, const uint64_t *in_k0, const uint64_t *in_k1,
+                                                 const uint64_t *in_meta, int64_t rb, int64_t hi) {
+#pragma unroll
+    for (int q = 0; q < D_RPT; ++q) {
+        const int64_t i = rb + (int64_t)q * DT + threadIdx.x;
+        const bool in = i < hi;
+        r.k0[q] = in ? in_k0[i] : 0ull;
+        r.k1[q] = in ? in_k1[i] : 0ull;
+        r.meta[q] = in ? in_meta[i] : 0ull;
+    }
+}
 __global__ void __launch_bounds__(DT) part_dedup_bytes_kernel(const uint64_t *in_k0, const uint64_t *in_k1,
                                                               const uint64_t *in_meta, const uint64_t *starts,
                                                               int64_t nbuckets, sdp_bytes_column col,
@@ -1074,97 +1093,109 @@ __global__ void __launch_bounds__(DT) part_dedup_bytes_kernel(const uint64_t *in
     const int t = threadIdx.x;
     uint64_t acc_groups = 0;
     bool acc_full = false, acc_coll = false;
-    for (int64_t f = blockIdx.x; f < nbuckets; f += gridDim.x) {
-        const int64_t lo = starts[f], hi = starts[f + 1];
+    int64_t f = blockIdx.x, lo = 0, hi = 0;
+    DRound cur, nxt;
+    if (f < nbuckets) {
+        lo = starts[f];
+        hi = starts[f + 1];
+        dedup_load_round(cur, in_k0, in_k1, in_meta, lo, hi);
+    }
+    for (; f < nbuckets; f += gridDim.x) {
+        const int64_t fn = f + gridDim.x;
+        int64_t lo_n = 0, hi_n = 0;
+        if (fn < nbuckets) {                                     // next bucket in flight
+            lo_n = starts[fn];
+            hi_n = starts[fn + 1];
+            dedup_load_round(nxt, in_k0, in_k1, in_meta, lo_n, hi_n);
+        }
         if (lo == hi) {
             if (t == 0) ngroups[f] = 0;
-            continue;
-        }
-        for (int i = t; i < D_B; i += DT) {
-            s_h[i] = EMPTY64;
-            s_cnt[i] = 0;
-        }
-        if (t == 0) { s_n = 0; s_full = 0; s_coll = 0; }
-        lds_barrier();
-        for (int64_t rb = lo; rb < hi; rb += (int64_t)DT * D_RPT) {
-            uint64_t k0[D_RPT], k1[D_RPT], meta[D_RPT], h[D_RPT];
-            int pos[D_RPT];
-            bool mine[D_RPT];
-#pragma unroll
-            for (int q = 0; q < D_RPT; ++q) {
-                const int64_t r = rb + (int64_t)q * DT + t;
-                pos[q] = -1;
-                mine[q] = false;
-                if (r < hi) {
-                    k0[q] = in_k0[r];
-                    k1[q] = in_k1[r];
-                    meta[q] = in_meta[r];
-                    h[q] = rec_hash(k0[q], k1[q], meta[q]);
-                }
+        } else {
+            for (int i = t; i < D_B; i += DT) {
+                s_h[i] = EMPTY64;
+                s_cnt[i] = 0;
             }
+            if (t == 0) { s_n = 0; s_full = 0; s_coll = 0; }
+            lds_barrier();
+            for (int64_t rb = lo; rb < hi; rb += (int64_t)DT * D_RPT) {
+                if (rb != lo) dedup_load_round(cur, in_k0, in_k1, in_meta, rb, hi);   // buckets beyond one round
+                int pos[D_RPT];
+                uint32_t mine = 0;
 #pragma unroll
-            for (int q = 0; q < D_RPT; ++q) {
-                const int64_t r = rb + (int64_t)q * DT + t;
-                if (r >= hi) continue;
-                // EMPTY64 is the empty marker: remap that one hash value
-                const uint64_t hk = h[q] == EMPTY64 ? 0xFFFFFFFFFFFFFFFEull : h[q];
-                h[q] = hk;
-                uint32_t p = (uint32_t)hk & (D_B - 1);
-                for (int probe = 0; probe < D_B; ++probe) {
-                    uint64_t cur = s_h[p];
-                    if (cur == EMPTY64) {
-                        cur = atomicCAS((unsigned long long *)&s_h[p], (unsigned long long)EMPTY64,
-                                        (unsigned long long)hk);
-                        if (cur == EMPTY64) { pos[q] = (int)p; mine[q] = true; break; }
+                for (int q = 0; q < D_RPT; ++q) {
+                    pos[q] = -1;
+                    const int64_t r = rb + (int64_t)q * DT + t;
+                    if (r >= hi) continue;
+                    // EMPTY64 is the empty marker: remap that one hash value
+                    const uint64_t h = rec_hash(cur.k0[q], cur.k1[q], cur.meta[q]);
+                    const uint64_t hk = h == EMPTY64 ? 0xFFFFFFFFFFFFFFFEull : h;
+                    uint32_t p = (uint32_t)hk & (D_B - 1);
+                    for (int probe = 0; probe < D_B; ++probe) {
+                        uint64_t c = s_h[p];
+                        if (c == EMPTY64) {
+                            c = atomicCAS((unsigned long long *)&s_h[p], (unsigned long long)EMPTY64,
+                                          (unsigned long long)hk);
+                            if (c == EMPTY64) { pos[q] = (int)p; mine |= 1u << q; break; }
+                        }
+                        if (c == hk) { pos[q] = (int)p; break; }
+                        p = (p + 1) & (D_B - 1);
                     }
-                    if (cur == hk) { pos[q] = (int)p; break; }
-                    p = (p + 1) & (D_B - 1);
+                    if (pos[q] < 0) s_full = 1;
                 }
-                if (pos[q] < 0) s_full = 1;
-            }
-            lds_barrier();
+                lds_barrier();
 #pragma unroll
-            for (int q = 0; q < D_RPT; ++q)
-                if (mine[q]) {
-                    s_k0[pos[q]] = k0[q];
-                    s_k1[pos[q]] = k1[q];
-                    s_meta[pos[q]] = meta[q];
-                }
-            lds_barrier();
+                for (int q = 0; q < D_RPT; ++q)
+                    if ((mine >> q) & 1u) {
+                        s_k0[pos[q]] = cur.k0[q];
+                        s_k1[pos[q]] = cur.k1[q];
+                        s_meta[pos[q]] = cur.meta[q];
+                    }
+                lds_barrier();
 #pragma unroll
-            for (int q = 0; q < D_RPT; ++q) {
-                if (pos[q] < 0) continue;
-                const int p = pos[q];
-                bool eq;
-                if (mine[q]) {
-                    eq = true;
-                } else {
-                    const uint64_t om = s_meta[p];
-                    eq = (om >> 40) == (meta[q] >> 40) && s_k0[p] == k0[q] && s_k1[p] == k1[q];
-                    if (eq && (meta[q] >> 40) > SHORT_MAX)
-                        eq = rows_equal_global(col, (int64_t)(om & RMASK40) - 1, (int64_t)(meta[q] & RMASK40) - 1);
+                for (int q = 0; q < D_RPT; ++q) {
+                    if (pos[q] < 0) continue;
+                    const int p = pos[q];
+                    bool eq;
+                    if ((mine >> q) & 1u) {
+                        eq = true;
+                    } else {
+                        const uint64_t om = s_meta[p];
+                        eq = (om >> 40) == (cur.meta[q] >> 40) && s_k0[p] == cur.k0[q] && s_k1[p] == cur.k1[q];
+                        if (eq && (cur.meta[q] >> 40) > SHORT_MAX)
+                            eq = rows_equal_global(col, (int64_t)(om & RMASK40) - 1,
+                                                   (int64_t)(cur.meta[q] & RMASK40) - 1);
+                    }
+                    if (eq) atomicAdd(&s_cnt[p], 1u);
+                    else s_coll = 1;
                 }
-                if (eq) atomicAdd(&s_cnt[p], 1u);
-                else s_coll = 1;
+                lds_barrier();
+            }
+            for (int i0 = 0; i0 < D_B; i0 += DT) {                 // every thread runs every round: ballots
+                const int i = i0 + t;
+                const uint64_t hk = s_h[i];
+                const bool g = hk != EMPTY64;
+                const uint64_t m = __ballot(g);
+                uint32_t base = 0;
+                if (lane_id() == 0 && m) base = atomicAdd(&s_n, (uint32_t)__popcll(m));
+                base = __shfl(base, 0, WAVE);
+                if (g) {
+                    const uint32_t p = base + (uint32_t)lane_rank(m);
+                    out_key[lo + p] = ((hk >> 40) << 40) | (s_meta[i] & RMASK40);
+                    out_cnt[lo + p] = s_cnt[i];
+                }
+            }
+            lds_barrier();
+            if (t == 0) {
+                ngroups[f] = s_n;
+                acc_groups += s_n;
+                acc_full |= s_full != 0;
+                acc_coll |= s_coll != 0;
             }
             lds_barrier();
         }
-        for (int i = t; i < D_B; i += DT) {
-            const uint64_t hk = s_h[i];
-            if (hk != EMPTY64) {
-                const uint32_t p = atomicAdd(&s_n, 1u);
-                out_key[lo + p] = ((hk >> 40) << 40) | (s_meta[i] & RMASK40);
-                out_cnt[lo + p] = s_cnt[i];
-            }
-        }
-        lds_barrier();
-        if (t == 0) {
-            ngroups[f] = s_n;
-            acc_groups += s_n;
-            acc_full |= s_full != 0;
-            acc_coll |= s_coll != 0;
-        }
-        lds_barrier();
+        lo = lo_n;
+        hi = hi_n;
+        cur = nxt;
     }
     if (t == 0) {
         if (acc_groups) atomicAdd((unsigned long long *)&stats[4 + (blockIdx.x & 63)], (unsigned long long)acc_groups);
