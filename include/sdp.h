@@ -70,6 +70,11 @@ typedef struct sdp_qplan {
     double   shift;                    /* moment shift K (sample median)           */
     int32_t  n_windows;
     int32_t  n_sample;                 /* valid, non-NaN sample elements           */
+    /* bit w set: window w keeps its bounds exclusive (candidates strictly inside,
+     * keys equal to a bound counted apart) -- a bound key repeated in the sample
+     * or lo == 0; windows with the bit clear take bound keys as candidates. */
+    int32_t  excl_mask;
+    int32_t  _pad;
 } sdp_qplan;
 
 /* Pass-1 result: replaces describe.py:143-144 (count), :193-201 (one agg of
@@ -89,9 +94,10 @@ typedef struct sdp_pass1_result {
     double   s4;                       /* sum (x-K)^4                              */
     /* per quantile window w */
     uint64_t w_gt[SDP_MAX_WINDOWS];    /* #(key > hi)                              */
-    uint64_t w_eq_lo[SDP_MAX_WINDOWS]; /* #(key == lo)                             */
-    uint64_t w_eq_hi[SDP_MAX_WINDOWS]; /* #(key == hi), 0 when hi == lo            */
-    uint64_t w_in[SDP_MAX_WINDOWS];    /* #(lo < key < hi) = candidates            */
+    uint64_t w_eq_lo[SDP_MAX_WINDOWS]; /* #(key == lo); 0 for inclusive windows    */
+    uint64_t w_eq_hi[SDP_MAX_WINDOWS]; /* #(key == hi), 0 when hi == lo or incl.   */
+    uint64_t w_in[SDP_MAX_WINDOWS];    /* candidates: #(lo < key < hi), or         */
+                                       /* #(lo <= key <= hi) (excl_mask bit clear) */
     uint32_t w_overflow;               /* bit w: a block overflowed its slots       */
     uint32_t _pad;
 } sdp_pass1_result;
@@ -146,14 +152,17 @@ int sdp_quantile_plan_batch(uint64_t *d_samples, int32_t n_sample, int32_t n_col
 #define SDP_PASS1_WAVES 4     /* waves per pass-1 workgroup = candidate segments per block */
 
 /* Fused pass 1 over one numeric column (see sdp_pass1_result).  Candidates
- * (keys strictly inside window w) go to wave-private slot ranges: segment
+ * (keys inside window w) go to wave-private slot ranges: segment
  * s = (w*grid + b)*SDP_PASS1_WAVES + wave holds d_cand[s*slot_capacity ...], its
  * count (clamped to slot_capacity; overflow flagged in w_overflow) in
  * d_cand_counts[s].  slot_capacity 0 = the plan has no windows (moments and min/max
- * only). */
+ * only).  flags & SDP_PASS1_INCLUSIVE: the caller has read *d_plan and no used
+ * window has its excl_mask bit set -- every window then collects its bound keys
+ * as candidates (w_eq_lo = w_eq_hi = 0), which costs fewer compares per row. */
+#define SDP_PASS1_INCLUSIVE 1
 int sdp_pass1(const sdp_column *col, const sdp_qplan *d_plan, void *d_work,
               int64_t work_bytes, uint64_t *d_cand, uint32_t *d_cand_counts,
-              int64_t slot_capacity, sdp_pass1_result *d_result, void *stream);
+              int64_t slot_capacity, int32_t flags, sdp_pass1_result *d_result, void *stream);
 
 /* Grid size sdp_pass1 uses for `length` rows (host-only). */
 int32_t sdp_pass1_grid(int64_t length, int32_t dtype);

@@ -125,6 +125,8 @@ __global__ void __launch_bounds__(1024) quantile_plan_kernel(uint64_t *sample, i
     sdp_qplan p;
     for (int w = 0; w < SDP_MAX_WINDOWS; ++w) { p.lo[w] = 0; p.hi[w] = EMPTY64; p.in_sample[w] = 0; }
     p.n_sample = m;
+    p.excl_mask = 0;
+    p._pad = 0;
     if (m == 0) {
         p.n_windows = np > 0 ? 1 : 0;
         p.shift = 0.0;
@@ -134,6 +136,9 @@ __global__ void __launch_bounds__(1024) quantile_plan_kernel(uint64_t *sample, i
     const uint64_t med = s[(m - 1) / 2];
     p.shift = is_float ? key_f64(med) : (double)key_i64(med);
     int nw = 0;
+    // a bound key seen twice in the sample may be frequent: that window keeps
+    // exclusive bounds (its bound copies are counted, not collected)
+    auto dup = [&](int i) { return (i > 0 && s[i - 1] == s[i]) || (i + 1 < m && s[i + 1] == s[i]); };
     for (int t = 0; t < np && t < SDP_MAX_WINDOWS; ++t) {
         const double q = probs[t];
         const double r = q * (double)(m - 1);
@@ -143,11 +148,14 @@ __global__ void __launch_bounds__(1024) quantile_plan_kernel(uint64_t *sample, i
         if (ih > m - 1) ih = m - 1;
         const uint64_t lo = (il == 0) ? 0ull : s[il];
         const uint64_t hi = (ih == m - 1) ? EMPTY64 : s[ih];
+        const bool ex = lo == 0ull || (il > 0 && dup(il)) || (ih < m - 1 && dup(ih));
         if (nw > 0 && lo <= p.hi[nw - 1]) {
             if (hi > p.hi[nw - 1]) p.hi[nw - 1] = hi;
+            if (ex) p.excl_mask |= 1 << (nw - 1);
         } else {
             p.lo[nw] = lo;
             p.hi[nw] = hi;
+            if (ex) p.excl_mask |= 1 << nw;
             ++nw;
         }
     }
@@ -230,7 +238,7 @@ __global__ void __launch_bounds__(1024) quantile_refine_kernel(const uint64_t *s
     uint32_t acc = 0;
     for (int w = 0; w < nw; ++w) { seg0[w] = acc; acc += s_in[w]; }
     uint64_t nlo[SDP_MAX_WINDOWS], nhi[SDP_MAX_WINDOWS];
-    int nn = 0;
+    int nn = 0, nex = 0;
     for (int t = 0; t < np && t < SDP_MAX_WINDOWS; ++t) {
         const double q = probs[t];
         const double r = q * (double)(m2 - 1);
@@ -243,11 +251,19 @@ __global__ void __launch_bounds__(1024) quantile_refine_kernel(const uint64_t *s
         int il = (int)floor(r) - d - (int)s_below[w], ih = (int)ceil(r) + d - (int)s_below[w];
         const uint64_t l = il <= 0 ? p.lo[w] : s[seg0[w] + il];
         const uint64_t h = ih >= cw - 1 ? p.hi[w] : s[seg0[w] + ih];
+        // exclusive bounds: an S1 bound kept from an exclusive S1 window, lo == 0,
+        // or a bound key repeated among the S2 keys of its window
+        const int a0 = (int)seg0[w], a1 = a0 + cw;
+        auto dup2 = [&](int i) { return (i > a0 && s[i - 1] == s[i]) || (i + 1 < a1 && s[i + 1] == s[i]); };
+        const bool s1ex = ((p.excl_mask >> w) & 1) != 0;
+        const bool ex = l == 0ull || (il <= 0 ? s1ex : dup2(a0 + il)) || (ih >= cw - 1 ? s1ex : dup2(a0 + ih));
         if (nn > 0 && l <= nhi[nn - 1]) {
             if (h > nhi[nn - 1]) nhi[nn - 1] = h;
+            if (ex) nex |= 1 << (nn - 1);
         } else {
             nlo[nn] = l;
             nhi[nn] = h;
+            if (ex) nex |= 1 << nn;
             ++nn;
         }
     }
@@ -267,6 +283,7 @@ __global__ void __launch_bounds__(1024) quantile_refine_kernel(const uint64_t *s
     }
     p.n_windows = nn;
     p.n_sample = (int32_t)m2;
+    p.excl_mask = nex;
     *plan = p;
 }
 
@@ -312,7 +329,7 @@ struct P1Ctx {
 // epilogue (n_skip), as are eqhi counts of windows with lo == hi -- so each
 // window costs two compare-and-carry counts, one equality count and the
 // inside test, with no per-element validity masking.
-template <typename T, bool WIN>
+template <typename T, bool WIN, bool INCL = false>
 __device__ __forceinline__ void p1_elem(P1Thread &st, const P1Ctx &cx, T x, bool valid) {
     const double xd = Elem<T>::d(x);
     const bool isnan_ = Elem<T>::is_float && (xd != xd);
@@ -345,6 +362,28 @@ __device__ __forceinline__ void p1_elem(P1Thread &st, const P1Ctx &cx, T x, bool
     }
     if (!WIN) return;                   // no quantile windows (date/timestamp min/max)
     const uint64_t key = ok ? Elem<T>::key(x) : 0ull;
+    if constexpr (INCL) {
+        // Inclusive windows (every bound key rare in the sample, lo > 0): one
+        // count #(key < lo) -- held in gt[] and turned into #(key > hi) in the
+        // epilogue -- and candidates lo <= key <= hi: 2 compares fewer per
+        // window than the exclusive form below.  Skipped elements (key 0) are
+        // below every lo; unused windows have lo > hi (never inside).
+#pragma unroll
+        for (int w = 0; w < SDP_MAX_WINDOWS; ++w) {
+            const uint64_t lo = cx.lo[w], hi = cx.hi[w];
+            st.gt[w] += (uint32_t)(key < lo);
+            const uint64_t m = __builtin_amdgcn_uicmpl(key, lo, 35 /*UGE*/) & __builtin_amdgcn_uicmpl(key, hi, 37 /*ULE*/);
+            if (m) {
+                const uint32_t c = st.wcur[w];
+                if ((m >> lane_id()) & 1u) {
+                    const uint32_t pos = c + (uint32_t)lane_rank(m);
+                    if ((int64_t)pos < cx.cap) cx.seg[w][pos] = key;
+                }
+                st.wcur[w] = c + (uint32_t)__popcll(m);
+            }
+        }
+        return;
+    }
     // Every window slot is evaluated: unused ones have lo = hi = UINT64_MAX
     // (nothing inside, nothing above; their counts are never read), which
     // keeps the loop free of per-window branches.
@@ -373,7 +412,7 @@ __device__ __forceinline__ void p1_fold(P1Thread &st) {
     st.t1 = st.t3 = 0.0;
 }
 
-template <typename T, bool WIN>
+template <typename T, bool WIN, bool INCL = false>
 __global__ void __launch_bounds__(P1_BLOCK, 4) pass1_kernel(sdp_column col, const sdp_qplan *plan,
                                                          P1Partial *partials, uint64_t *cand,
                                                          uint32_t *cand_counts, int64_t cap) {
@@ -384,7 +423,7 @@ __global__ void __launch_bounds__(P1_BLOCK, 4) pass1_kernel(sdp_column col, cons
 #pragma unroll
     for (int w = 0; w < SDP_MAX_WINDOWS; ++w) {
         cx.lo[w] = w < cx.nw ? plan->lo[w] : EMPTY64;
-        cx.hi[w] = w < cx.nw ? plan->hi[w] : EMPTY64;
+        cx.hi[w] = w < cx.nw ? plan->hi[w] : (INCL ? EMPTY64 - 1 : EMPTY64);
         const int64_t seg = ((int64_t)w * gridDim.x + blockIdx.x) * P1_WPB + (threadIdx.x / WAVE);
         cx.seg[w] = cand + seg * cap;
     }
@@ -423,7 +462,7 @@ __global__ void __launch_bounds__(P1_BLOCK, 4) pass1_kernel(sdp_column col, cons
         for (int u = 0; u < U; ++u) {
             const uint32_t vbits = x[u].bits(vbm);
 #pragma unroll
-            for (int e = 0; e < VPT; ++e) p1_elem<T, WIN>(st, cx, x[u].v.v[e], (vbits >> e) & 1u);
+            for (int e = 0; e < VPT; ++e) p1_elem<T, WIN, INCL>(st, cx, x[u].v.v[e], (vbits >> e) & 1u);
         }
         p1_fold(st);
     };
@@ -447,7 +486,7 @@ __global__ void __launch_bounds__(P1_BLOCK, 4) pass1_kernel(sdp_column col, cons
         const bool inb = i < n;
         T x = inb ? ((const T *)col.d_values)[i] : (T)0;
         const bool valid = inb && valid_bit(col.d_validity, col.validity_bit_offset, i);
-        p1_elem<T, WIN>(st, cx, x, valid);
+        p1_elem<T, WIN, INCL>(st, cx, x, valid);
         p1_fold(st);
     }
 
@@ -475,12 +514,17 @@ __global__ void __launch_bounds__(P1_BLOCK, 4) pass1_kernel(sdp_column col, cons
         const uint64_t skip = wave_sum_u64(st.n_skip);
 #pragma unroll
         for (int w = 0; w < W_; ++w) {
-            const uint64_t g = wave_sum_u64(st.gt[w]);
+            uint64_t g = wave_sum_u64(st.gt[w]);
             uint64_t e1 = wave_sum_u64(st.eqlo[w]);
             uint64_t e2 = wave_sum_u64(st.eqhi[w]);
-            if (cx.lo[w] == 0) e1 -= skip;                  // skipped elements carry key 0
-            if (cx.hi[w] == 0) e2 -= skip;
-            if (cx.hi[w] == cx.lo[w]) e2 = 0;               // one bound: counted as eqlo only
+            if (INCL) {                                     // g = #(key < lo), skipped elements included
+                g = c0 - (g - skip) - st.wcur[w];           // -> #(key > hi)
+                e1 = e2 = 0;
+            } else {
+                if (cx.lo[w] == 0) e1 -= skip;              // skipped elements carry key 0
+                if (cx.hi[w] == 0) e2 -= skip;
+                if (cx.hi[w] == cx.lo[w]) e2 = 0;           // one bound: counted as eqlo only
+            }
             if (lane == 0) {
                 s_u[wid][4 + w] = g; s_u[wid][4 + W_ + w] = e1; s_u[wid][4 + 2 * W_ + w] = e2;
                 s_u[wid][4 + 3 * W_ + w] = st.wcur[w];
@@ -1370,7 +1414,7 @@ extern "C" int sdp_quantile_plan_batch(uint64_t *d_samples, int32_t n_sample, in
 }
 
 extern "C" int sdp_pass1(const sdp_column *col, const sdp_qplan *d_plan, void *d_work, int64_t work_bytes,
-                         uint64_t *d_cand, uint32_t *d_cand_counts, int64_t slot_capacity,
+                         uint64_t *d_cand, uint32_t *d_cand_counts, int64_t slot_capacity, int32_t flags,
                          sdp_pass1_result *d_result, void *stream) {
     int rc = check_col(col, "sdp_pass1");
     if (rc) return rc;
@@ -1381,7 +1425,11 @@ extern "C" int sdp_pass1(const sdp_column *col, const sdp_qplan *d_plan, void *d
     if (slot_capacity < 0 || slot_capacity > 0xFFFFFFFFll) return set_error(SDP_EINVAL, "sdp_pass1: slot_capacity");
     hipStream_t s = (hipStream_t)stream;
     P1Partial *parts = (P1Partial *)d_work;
-    if (slot_capacity > 0) {
+    if (slot_capacity > 0 && (flags & SDP_PASS1_INCLUSIVE)) {
+        SDP_DISPATCH_NUMERIC(col->dtype,
+            hipLaunchKernelGGL((pass1_kernel<T, true, true>), dim3(grid), dim3(P1_BLOCK), 0, s, *col, d_plan, parts,
+                               d_cand, d_cand_counts, slot_capacity));
+    } else if (slot_capacity > 0) {
         SDP_DISPATCH_NUMERIC(col->dtype,
             hipLaunchKernelGGL((pass1_kernel<T, true>), dim3(grid), dim3(P1_BLOCK), 0, s, *col, d_plan, parts, d_cand,
                                d_cand_counts, slot_capacity));

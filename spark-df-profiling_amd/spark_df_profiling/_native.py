@@ -65,7 +65,8 @@ class SdpChunk(ctypes.Structure):
 class SdpQPlan(ctypes.Structure):
     _fields_ = [('lo', ctypes.c_uint64 * MAX_WINDOWS), ('hi', ctypes.c_uint64 * MAX_WINDOWS),
                 ('in_sample', ctypes.c_int32 * MAX_WINDOWS), ('shift', ctypes.c_double),
-                ('n_windows', ctypes.c_int32), ('n_sample', ctypes.c_int32)]
+                ('n_windows', ctypes.c_int32), ('n_sample', ctypes.c_int32),
+                ('excl_mask', ctypes.c_int32), ('_pad', ctypes.c_int32)]
 
 
 class SdpPass1Result(ctypes.Structure):
@@ -118,7 +119,7 @@ _SIGNATURES = {
     'sdp_quantile_plan': (ctypes.c_int, [_P, _I32, _P, _I32, _I32, _P, _P]),
     'sdp_quantile_plan_batch': (ctypes.c_int, [_P, _I32, _I32, _P, _I32, _P, _P, _P]),
     'sdp_quantile_refine_batch': (ctypes.c_int, [_P, _I32, _I32, _P, _I32, _P, _P]),
-    'sdp_pass1': (ctypes.c_int, [_COL, _P, _P, _I64, _P, _P, _I64, _P, _P]),
+    'sdp_pass1': (ctypes.c_int, [_COL, _P, _P, _I64, _P, _P, _I64, _I32, _P, _P]),
     'sdp_compact_candidates': (ctypes.c_int, [_P, _P, _I32, _I64, _P, _P, _P, _P]),
     'sdp_radix_hist': (ctypes.c_int, [_P, _P, _U64, _I32, _P, _P]),
     'sdp_radix_filter': (ctypes.c_int, [_P, _P, _U64, _I32, _P, _P, _P]),

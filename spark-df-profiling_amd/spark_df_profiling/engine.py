@@ -49,6 +49,8 @@ PART_CHUNK = 65536           # level-2 records per workgroup chunk
 # byte columns: strings read once into compacted records, then a record scatter
 # (SDP_BYTES_TWO_READS=1: the count + re-read scatter of round 1, for A/B runs)
 BYTES_ONE_READ = os.environ.get('SDP_BYTES_TWO_READS', '0') != '1'
+# pass 1 with inclusive quantile windows where the plan allows (SDP_PASS1_EXCL=1: never, for A/B runs)
+PASS1_INCLUSIVE = os.environ.get('SDP_PASS1_EXCL', '0') != '1'
 CAND_FULL_BUDGET = 1 << 30   # bytes of room-for-every-row candidate slots per pass-1 batch
 
 # Test knob for the quantile edge paths (never set in production):
@@ -279,9 +281,11 @@ class Engine:
         if res_dev is None:
             res_dev = self._bytes(ctypes.sizeof(nat.SdpPass1Result))
         cs = col.sdp()
+        # inclusive windows when no used window needs exclusive bounds (see sdp_qplan.excl_mask)
+        flags = 1 if (nw and PASS1_INCLUSIVE and not (plan.excl_mask & ((1 << nw) - 1))) else 0
         nat.annotate(_label(col), col_read_bytes(col))
         sdp.sdp_pass1(ctypes.byref(cs), ptr(plan_dev), ptr(work), work.numel(), ptr(cand), ptr(cand_counts), cap,
-                      ptr(res_dev), self._s())
+                      flags, ptr(res_dev), self._s())
         return {'cand': cand, 'counts': cand_counts, 'nseg': nseg, 'cap': cap, 'res_dev': res_dev}
 
     def pass1(self, col: DeviceColumn, plan_dev, plan):
@@ -853,6 +857,7 @@ class Engine:
             for i, p in enumerate(plans):
                 for w in range(p.n_windows):
                     p.hi[w] = p.lo[w]
+                p.excl_mask = (1 << nat.MAX_WINDOWS) - 1      # (lo, lo): nothing inside, every rank missed
                 plans_dev[i * psz:(i + 1) * psz] = self._to_dev(p)
         rsz = ctypes.sizeof(nat.SdpPass1Result)
         res_all = self._bytes(len(cols) * rsz)
