@@ -149,6 +149,20 @@ int sdp_quantile_plan_batch(uint64_t *d_samples, int32_t n_sample, int32_t n_col
                             const double *probs, int32_t n_probs, const int32_t *d_is_float,
                             sdp_qplan *d_plans, void *stream);
 
+/* Spark 2.x percentile_approx emulation (opt-in; describe(quantile_mode='gk')):
+ * the element ApproximatePercentile's QuantileSummaries returns for
+ * percentile_approx(c, p, accuracy) (describe.py:205-206) when the column's
+ * rows form n_partitions Spark partitions [p*n/P, (p+1)*n/P) whose partial
+ * digests are merged in partition order.  float/double columns; nulls and NaN
+ * are dropped (na.drop).  d_out[k] = the value for d_probs[k] (NaN when the
+ * column has no value); d_status = {error (0 ok, 1/2 summary capacity), values,
+ * samples}.  Sequential by nature (one workgroup per partition), so a
+ * correctness mode rather than the default exact-rank path. */
+int64_t sdp_gk_workspace_bytes(int32_t n_partitions);
+int sdp_gk_quantiles(const sdp_column *col, int32_t n_partitions, int32_t accuracy,
+                     const double *d_probs, int32_t n_probs, void *d_work, int64_t work_bytes,
+                     double *d_out, int64_t *d_status, void *stream);
+
 #define SDP_PASS1_WAVES 4     /* waves per pass-1 workgroup = candidate segments per block */
 
 /* Fused pass 1 over one numeric column (see sdp_pass1_result).  Candidates

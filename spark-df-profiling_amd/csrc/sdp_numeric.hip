@@ -1950,3 +1950,379 @@ extern "C" int sdp_pass2(const sdp_column *col, double mean, const double *d_edg
     hipLaunchKernelGGL(pass2_merge_kernel, dim3(1), dim3(MERGE_T), 0, s, pm, pc, grid, bins, d_result, d_hist);
     return check_launch("pass2_merge_kernel");
 }
+
+// ============================================================================
+// Spark 2.x percentile_approx emulation (opt-in; describe(quantile_mode='gk'))
+// ============================================================================
+// Replaces describe.py:205-206's percentile_approx(c, p) element by element
+// for a given partitioning: ApproximatePercentile's QuantileSummaries
+// (relativeError = 1/accuracy, head buffer 50000, compress threshold 10000),
+// restated from Spark 2.1-2.4 (oracle/gk.py holds the CPU restatement the
+// tests compare against, bit for bit).  One workgroup per Spark partition walks
+// the partition's rows in order: every 50000 non-null, non-NaN values form a
+// head batch, sorted in LDS chunks and merged; the batch is merged into the
+// samples by binary-search ranks (all threads), then compressImmut's greedy
+// scan runs on one thread (it is sequential by definition).  A second kernel
+// merges the partition summaries in partition order and answers the queries.
+// The GK state is tiny; the cost is the sequential compress scans, which makes
+// this a correctness mode, not the default (the default returns the exact
+// element at rank ceil(pN), inside Spark's rank window).
+constexpr int GK_T = 1024;
+constexpr int GK_HEAD = 50000;          // QuantileSummaries.defaultHeadSize
+constexpr int GK_COMPRESS = 10000;      // defaultCompressThreshold (every full head exceeds it)
+constexpr int GK_CHUNK = 12500;         // a head is sorted as four LDS chunks (<= SORT_MAX)
+constexpr int64_t GK_CAP = 1 << 18;     // samples per partition buffer
+constexpr int64_t GK_HBUF = 65536;      // head keys per buffer
+
+struct GkPart {                         // one partition's state in the workspace
+    int64_t len, count, which, status;  // samples, values seen, current buffer (0/1), error
+};
+struct GkView {                         // structure-of-arrays samples
+    double *v;
+    int64_t *g, *d;
+};
+
+__device__ __forceinline__ uint64_t gk_key(double v) {          // java.lang.Double.compare order
+    const uint64_t b = (uint64_t)__double_as_longlong(v);
+    return (b >> 63) ? ~b : (b | 0x8000000000000000ull);
+}
+__device__ __forceinline__ double gk_val(uint64_t k) {
+    return __longlong_as_double((long long)((k >> 63) ? (k & 0x7FFFFFFFFFFFFFFFull) : ~k));
+}
+
+// workspace layout: [P] GkPart | per partition: headA, headB (GK_HBUF u64 each),
+// two sample buffers (GK_CAP x (v, g, d)) | merge: two buffers of 2*GK_CAP samples
+__host__ __device__ inline int64_t gk_part_bytes() { return 2 * GK_HBUF * 8 + 2 * GK_CAP * 24; }
+__host__ __device__ inline int64_t gk_head_off(int P) { return ((int64_t)P * (int64_t)sizeof(GkPart) + 255) / 256 * 256; }
+__device__ GkView gk_view(uint8_t *base, int64_t cap) {
+    GkView w;
+    w.v = (double *)base;
+    w.g = (int64_t *)(base + cap * 8);
+    w.d = (int64_t *)(base + cap * 16);
+    return w;
+}
+
+// number of a[0..n) (numerically non-decreasing) with a[i] < x (strict) or <= x
+__device__ __forceinline__ int64_t gk_count_lt(const double *a, int64_t n, double x, bool le) {
+    int64_t lo = 0, hi = n;
+    while (lo < hi) {
+        const int64_t mid = (lo + hi) >> 1;
+        if (le ? (a[mid] <= x) : (a[mid] < x)) lo = mid + 1; else hi = mid;
+    }
+    return lo;
+}
+__device__ __forceinline__ int64_t gk_count_key(const uint64_t *a, int64_t n, uint64_t x, bool le) {
+    int64_t lo = 0, hi = n;
+    while (lo < hi) {
+        const int64_t mid = (lo + hi) >> 1;
+        if (le ? (a[mid] <= x) : (a[mid] < x)) lo = mid + 1; else hi = mid;
+    }
+    return lo;
+}
+
+// compressImmut(in[0..L), thr) by thread 0 into out[w..L) (written from the end);
+// the caller copies it to the front.  Returns w (all threads).
+__device__ int64_t gk_compress(const GkView in, int64_t L, double thr, GkView out, int64_t *s_w) {
+    if (threadIdx.x == 0) {
+        int64_t w = L;
+        if (L > 0) {
+            double hv = in.v[L - 1];
+            int64_t hg = in.g[L - 1], hd = in.d[L - 1];
+            for (int64_t i = L - 2; i >= 1; --i) {
+                const int64_t g1 = in.g[i];
+                if ((double)(g1 + hg + hd) < thr) {
+                    hg += g1;
+                } else {
+                    --w; out.v[w] = hv; out.g[w] = hg; out.d[w] = hd;
+                    hv = in.v[i]; hg = g1; hd = in.d[i];
+                }
+            }
+            --w; out.v[w] = hv; out.g[w] = hg; out.d[w] = hd;
+            if (in.v[0] <= hv && L > 1) { --w; out.v[w] = in.v[0]; out.g[w] = in.g[0]; out.d[w] = in.d[0]; }
+        }
+        *s_w = w;
+    }
+    __syncthreads();
+    return *s_w;
+}
+__device__ void gk_copy(const GkView src, int64_t from, int64_t n, GkView dst) {
+    for (int64_t i = threadIdx.x; i < n; i += blockDim.x) {
+        dst.v[i] = src.v[from + i]; dst.g[i] = src.g[from + i]; dst.d[i] = src.d[from + i];
+    }
+    __syncthreads();
+}
+
+// sorted head keys (hn) merged into samples cur[0..len) -> nxt[0..len + hn)
+// (withHeadBufferInserted), count = values before this head
+__device__ void gk_insert(const uint64_t *H, int64_t hn, const GkView cur, int64_t len, int64_t count, double eps,
+                          GkView nxt) {
+    for (int64_t i = threadIdx.x; i < len; i += blockDim.x) {
+        // batch values strictly below s_i come first (s_i <= x emits s_i before x)
+        int64_t lo = 0, hi = hn;
+        const double s = cur.v[i];
+        while (lo < hi) { const int64_t mid = (lo + hi) >> 1; if (gk_val(H[mid]) < s) lo = mid + 1; else hi = mid; }
+        const int64_t p = i + lo;
+        nxt.v[p] = s; nxt.g[p] = cur.g[i]; nxt.d[p] = cur.d[i];
+    }
+    for (int64_t j = threadIdx.x; j < hn; j += blockDim.x) {
+        const double x = gk_val(H[j]);
+        const int64_t c = gk_count_lt(cur.v, len, x, true);
+        const int64_t p = j + c;
+        const bool zero = p == 0 || (j == hn - 1 && c == len);
+        nxt.v[p] = x; nxt.g[p] = 1;
+        nxt.d[p] = zero ? 0 : (int64_t)floor(2 * eps * (double)(count + j + 1));
+    }
+    __syncthreads();
+}
+
+// sort H[0..hn) (hn <= GK_HEAD): four LDS chunks, then two rounds of merges via B
+__device__ void gk_sort_head(uint64_t *H, uint64_t *B, int64_t hn, uint64_t *s) {
+    int64_t cs[5];
+    int nc = 0;
+    for (int64_t st = 0; st < hn; st += GK_CHUNK) {
+        const int m = (int)min((int64_t)GK_CHUNK, hn - st);
+        for (int i = threadIdx.x; i < m; i += blockDim.x) s[i] = H[st + i];
+        __syncthreads();
+        block_sort_keys(s, m);
+        for (int i = threadIdx.x; i < m; i += blockDim.x) H[st + i] = s[i];
+        __syncthreads();
+        cs[nc++] = st;
+    }
+    cs[nc] = hn;
+    uint64_t *src = H, *dst = B;
+    for (int width = 1; width < nc; width <<= 1) {
+        for (int a = 0; a < nc; a += 2 * width) {
+            const int64_t l0 = cs[a], l1 = cs[min(a + width, nc)], r1 = cs[min(a + 2 * width, nc)];
+            const int64_t nl = l1 - l0, nr = r1 - l1;
+            for (int64_t i = threadIdx.x; i < nl + nr; i += blockDim.x) {
+                if (i < nl) {
+                    const uint64_t x = src[l0 + i];
+                    dst[l0 + i + gk_count_key(src + l1, nr, x, false)] = x;
+                } else {
+                    const int64_t j = i - nl;
+                    const uint64_t x = src[l1 + j];
+                    dst[l0 + j + gk_count_key(src + l0, nl, x, true)] = x;
+                }
+            }
+        }
+        __syncthreads();
+        uint64_t *t = src; src = dst; dst = t;
+    }
+    if (src != H) {
+        for (int64_t i = threadIdx.x; i < hn; i += blockDim.x) H[i] = src[i];
+        __syncthreads();
+    }
+}
+
+template <typename T>
+__global__ void __launch_bounds__(GK_T) gk_partition_kernel(sdp_column col, int32_t P, double eps, uint8_t *work) {
+    __shared__ uint64_t s[SORT_MAX];
+    __shared__ uint32_t s_wsum[GK_T / WAVE];
+    __shared__ int64_t s_next, s_w;
+    const int p = blockIdx.x, t = threadIdx.x, lane = lane_id(), wv = t / WAVE;
+    GkPart *parts = (GkPart *)work;
+    uint8_t *mine = work + gk_head_off(P) + (int64_t)p * gk_part_bytes();
+    uint64_t *H = (uint64_t *)mine, *B = H + GK_HBUF;
+    GkView buf[2] = {gk_view(mine + 2 * GK_HBUF * 8, GK_CAP), gk_view(mine + 2 * GK_HBUF * 8 + GK_CAP * 24, GK_CAP)};
+    const int64_t n = col.length;
+    const int64_t r1 = (int64_t)(((__int128)(p + 1) * n) / P);
+    int64_t row = (int64_t)(((__int128)p * n) / P);
+    int64_t len = 0, count = 0, status = 0;
+    int cur = 0;
+    bool any = false;
+    const T *vals = (const T *)col.d_values;
+    while (true) {
+        // next head: up to GK_HEAD non-null, non-NaN values in row order
+        int64_t hn = 0;
+        while (hn < GK_HEAD && row < r1) {
+            const int64_t i = row + t;
+            bool ok = false;
+            double x = 0.0;
+            if (i < r1 && valid_bit(col.d_validity, col.validity_bit_offset, i)) {
+                x = Elem<T>::d(vals[i]);
+                ok = !(x != x);
+            }
+            const uint64_t m = __ballot(ok);
+            if (lane == 0) s_wsum[wv] = (uint32_t)__popcll(m);
+            __syncthreads();
+            uint32_t before = 0, total = 0;
+            for (int k = 0; k < GK_T / WAVE; ++k) { const uint32_t c = s_wsum[k]; before += k < wv ? c : 0; total += c; }
+            const int64_t take = min((int64_t)total, GK_HEAD - hn);
+            const int64_t rk = before + lane_rank(m);
+            if (ok && rk < take) H[hn + rk] = gk_key(x);
+            if (ok && rk == take - 1 && take < (int64_t)total) s_next = i + 1;
+            if (t == 0 && take == (int64_t)total) s_next = min(row + GK_T, r1);
+            __syncthreads();
+            row = s_next;
+            hn += take;
+            __syncthreads();
+        }
+        const bool full = hn == GK_HEAD;
+        if (hn > 0) {
+            any = true;
+            if (len + hn > GK_CAP) { status = 1; break; }
+            gk_sort_head(H, B, hn, s);
+            gk_insert(H, hn, buf[cur], len, count, eps, buf[cur ^ 1]);
+            len += hn;
+            count += hn;
+            // compress (every full head reaches the threshold; a final partial head is
+            // compressed by the serializing compress() below)
+            if (full && len >= GK_COMPRESS) {
+                const int64_t w = gk_compress(buf[cur ^ 1], len, 2 * eps * (double)count, buf[cur], &s_w);
+                gk_copy(buf[cur], w, len - w, buf[cur ^ 1]);
+                len -= w;
+            }
+            cur ^= 1;
+        }
+        if (!full) break;
+    }
+    if (status == 0 && any) {               // the partial aggregate is serialized compressed
+        const int64_t w = gk_compress(buf[cur], len, 2 * eps * (double)count, buf[cur ^ 1], &s_w);
+        gk_copy(buf[cur ^ 1], w, len - w, buf[cur]);
+        len -= w;
+    }
+    if (t == 0) {
+        parts[p].len = len;
+        parts[p].count = count;
+        parts[p].which = cur;
+        parts[p].status = status;
+    }
+}
+
+// one workgroup: stable-merge the partition summaries in partition order
+// (QuantileSummaries.merge), then query every probability
+__device__ void gk_zero_fix(GkView a, int64_t n, GkView tmp) {
+    // numerically sorted samples may hold 0.0 before -0.0: put the zero run in
+    // Double.compare order (stable), as sortBy(_.value) sees it
+    if (threadIdx.x == 0) {
+        const int64_t z0 = gk_count_lt(a.v, n, 0.0, false), z1 = gk_count_lt(a.v, n, 0.0, true);
+        int64_t k = 0;
+        for (int pass = 0; pass < 2; ++pass)
+            for (int64_t i = z0; i < z1; ++i) {
+                const bool neg = (__double_as_longlong(a.v[i]) >> 63) != 0;
+                if (neg == (pass == 0)) { tmp.v[k] = a.v[i]; tmp.g[k] = a.g[i]; tmp.d[k] = a.d[i]; ++k; }
+            }
+        for (int64_t i = 0; i < k; ++i) { a.v[z0 + i] = tmp.v[i]; a.g[z0 + i] = tmp.g[i]; a.d[z0 + i] = tmp.d[i]; }
+    }
+    __syncthreads();
+}
+__global__ void __launch_bounds__(GK_T) gk_merge_query_kernel(int32_t P, double eps, uint8_t *work,
+                                                              const double *probs, int32_t np, double *out,
+                                                              int64_t *status) {
+    __shared__ int64_t s_w;
+    GkPart *parts = (GkPart *)work;
+    uint8_t *mbase = work + gk_head_off(P) + (int64_t)P * gk_part_bytes();
+    const int64_t MC = 2 * GK_CAP;
+    GkView M = gk_view(mbase, MC), X = gk_view(mbase + MC * 24, MC);
+    int64_t m = 0, cm = 0, st = 0;
+    for (int p = 0; p < P; ++p) {
+        const GkPart gp = parts[p];
+        if (gp.status) { st = gp.status; break; }
+        if (gp.count == 0) continue;
+        uint8_t *mine = work + gk_head_off(P) + (int64_t)p * gk_part_bytes();
+        GkView pv = gk_view(mine + 2 * GK_HBUF * 8 + gp.which * GK_CAP * 24, GK_CAP);
+        if (cm == 0) {
+            gk_copy(pv, 0, gp.len, M);
+            m = gp.len;
+            cm = gp.count;
+            continue;
+        }
+        if (m + gp.len > MC) { st = 2; break; }
+        gk_zero_fix(M, m, X);
+        gk_zero_fix(pv, gp.len, X);
+        // stable merge by Double.compare: M's samples first among equal keys
+        for (int64_t i = threadIdx.x; i < m + gp.len; i += blockDim.x) {
+            int64_t q;
+            double v;
+            int64_t g, d;
+            if (i < m) {
+                v = M.v[i]; g = M.g[i]; d = M.d[i];
+                const uint64_t k = gk_key(v);
+                int64_t lo = 0, hi = gp.len;
+                while (lo < hi) { const int64_t mid = (lo + hi) >> 1; if (gk_key(pv.v[mid]) < k) lo = mid + 1; else hi = mid; }
+                q = i + lo;
+            } else {
+                const int64_t j = i - m;
+                v = pv.v[j]; g = pv.g[j]; d = pv.d[j];
+                const uint64_t k = gk_key(v);
+                int64_t lo = 0, hi = m;
+                while (lo < hi) { const int64_t mid = (lo + hi) >> 1; if (gk_key(M.v[mid]) <= k) lo = mid + 1; else hi = mid; }
+                q = j + lo;
+            }
+            X.v[q] = v; X.g[q] = g; X.d[q] = d;
+        }
+        __syncthreads();
+        const int64_t L = m + gp.len;
+        const int64_t w = gk_compress(X, L, 2 * eps * (double)cm, M, &s_w);   // threshold: the receiver's count
+        gk_copy(M, w, L - w, X);
+        gk_copy(X, 0, L - w, M);
+        m = L - w;
+        cm += gp.count;
+    }
+    if (threadIdx.x != 0) return;
+    status[0] = st;
+    status[1] = cm;
+    status[2] = m;
+    for (int k = 0; k < np; ++k) {
+        const double q = probs[k];
+        double r = __builtin_nan("");
+        if (st == 0 && m > 0) {
+            if (q <= eps) {
+                r = M.v[0];
+            } else if (q >= 1 - eps) {
+                r = M.v[m - 1];
+            } else {
+                const int64_t rank = (int64_t)(int32_t)ceil(q * (double)cm);
+                const double target = ceil(eps * (double)cm);
+                int64_t min_rank = 0;
+                r = M.v[m - 1];
+                for (int64_t i = 1; i < m - 1; ++i) {
+                    min_rank += M.g[i];
+                    const int64_t max_rank = min_rank + M.d[i];
+                    if ((double)max_rank - target <= (double)rank && (double)rank <= (double)min_rank + target) {
+                        r = M.v[i];
+                        break;
+                    }
+                }
+            }
+        }
+        out[k] = r;
+    }
+}
+
+extern "C" int64_t sdp_gk_workspace_bytes(int32_t n_partitions) {
+    if (n_partitions < 1) return -1;
+    return gk_head_off(n_partitions) + (int64_t)n_partitions * gk_part_bytes() + 2 * (2 * GK_CAP) * 24;
+}
+
+extern "C" int sdp_gk_quantiles(const sdp_column *col, int32_t n_partitions, int32_t accuracy, const double *d_probs,
+                                int32_t n_probs, void *d_work, int64_t work_bytes, double *d_out, int64_t *d_status,
+                                void *stream) {
+    int rc = check_col(col, "sdp_gk_quantiles");
+    if (rc) return rc;
+    if (n_partitions < 1 || n_partitions > 65535) return set_error(SDP_EINVAL, "sdp_gk_quantiles: n_partitions %d", n_partitions);
+    if (accuracy < 1) return set_error(SDP_EINVAL, "sdp_gk_quantiles: accuracy %d", accuracy);
+    if (n_probs < 0 || d_out == nullptr || d_status == nullptr || (n_probs > 0 && d_probs == nullptr))
+        return set_error(SDP_EINVAL, "sdp_gk_quantiles: outputs");
+    if (work_bytes < sdp_gk_workspace_bytes(n_partitions))
+        return set_error(SDP_ECAP, "sdp_gk_quantiles: workspace %lld < %lld", (long long)work_bytes,
+                         (long long)sdp_gk_workspace_bytes(n_partitions));
+    const double eps = 1.0 / (double)accuracy;
+    hipStream_t s = (hipStream_t)stream;
+    switch (col->dtype) {
+    case SDP_F64:
+        hipLaunchKernelGGL(gk_partition_kernel<double>, dim3(n_partitions), dim3(GK_T), 0, s, *col, n_partitions, eps,
+                           (uint8_t *)d_work);
+        break;
+    case SDP_F32:
+        hipLaunchKernelGGL(gk_partition_kernel<float>, dim3(n_partitions), dim3(GK_T), 0, s, *col, n_partitions, eps,
+                           (uint8_t *)d_work);
+        break;
+    default: return set_error(SDP_EINVAL, "sdp_gk_quantiles: dtype %d is not float/double", col->dtype);
+    }
+    rc = check_launch("gk_partition_kernel");
+    if (rc) return rc;
+    hipLaunchKernelGGL(gk_merge_query_kernel, dim3(1), dim3(GK_T), 0, s, n_partitions, eps, (uint8_t *)d_work, d_probs,
+                       n_probs, d_out, d_status);
+    return check_launch("gk_merge_query_kernel");
+}

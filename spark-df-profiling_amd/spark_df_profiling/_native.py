@@ -158,6 +158,8 @@ _SIGNATURES = {
     'sdp_part_rows': (ctypes.c_int, [_COL, _BCOL, _HVY, _I32, _I32, _P, _P, _REC, _P, _P, _P]),
     'sdp_part_recs': (ctypes.c_int, [_REC, _I32, _P, _I64, _I32, _I32, _I32, _P, _P, _REC, _P]),
     'sdp_part_records_chunks': (_I64, [_I64]),
+    'sdp_gk_workspace_bytes': (_I64, [_I32]),
+    'sdp_gk_quantiles': (ctypes.c_int, [_COL, _I32, _I32, _P, _I32, _P, _I64, _P, _P, _P]),
     'sdp_part_rows_records': (ctypes.c_int, [_BCOL, _HVY, _I32, _P, _P, _REC, _P, _P, _P]),
     'sdp_part_dedup': (ctypes.c_int, [_REC, _I32, _BCOL, _P, _I64, _I32, _P, _P, _P, _P, _P]),
     'sdp_part_compact': (ctypes.c_int, [_P, _P, _P, _P, _P, _I64, _P, _P, _P]),
@@ -173,7 +175,7 @@ _SIGNATURES = {
 
 _VALUE_FUNCS = {'sdp_last_error', 'sdp_version', 'sdp_pass1_workspace_bytes', 'sdp_pass2_workspace_bytes',
                 'sdp_pass1_grid', 'sdp_gram_workspace_bytes', 'sdp_part_rows_per_block', 'sdp_part_bucket_target',
-                'sdp_part_records_chunks',
+                'sdp_part_records_chunks', 'sdp_gk_workspace_bytes',
                 'sdp_scan_workspace_bytes', 'sdp_bitmap_workspace_bytes', 'sdp_select_kth_workspace_bytes',
                 'sdp_select_rounds', 'sdp_pass2_count_workspace_bytes'}
 _STATUS_FUNCS = set(_SIGNATURES) - _VALUE_FUNCS

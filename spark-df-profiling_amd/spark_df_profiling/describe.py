@@ -271,11 +271,20 @@ def describe(df, bins=10, corr_reject=0.9, **kwargs):
     (k_vals, t_freq): ``comm`` (a comm.TorchComm for a row-sharded table -- each
     rank passes its own row range), ``device``, ``plots`` (default True:
     histogram PNGs as the reference stores them) and ``raw`` (a dict that
-    receives the per-column engine outputs, e.g. exact histogram counts)."""
+    receives the per-column engine outputs, e.g. exact histogram counts),
+    ``quantile_mode`` ('exact', the default: float quantiles are the element at
+    rank ceil(pN), inside percentile_approx's rank window; 'gk': Spark 2.x's
+    percentile_approx element for ``spark_partitions`` contiguous partitions,
+    restated from QuantileSummaries -- single rank only)."""
     comm = kwargs.pop('comm', None)
     device = kwargs.pop('device', None)
     plots = kwargs.pop('plots', True)
     raw = kwargs.pop('raw', None)
+    quantile_mode = kwargs.pop('quantile_mode', 'exact')
+    if quantile_mode not in ('exact', 'gk'):
+        raise ValueError("quantile_mode must be 'exact' or 'gk'")
+    gk = {'partitions': int(kwargs.pop('spark_partitions', 1)),
+          'accuracy': int(kwargs.pop('accuracy', 10000))} if quantile_mode == 'gk' else None
     table = as_device_table(df, device)
     engine = Engine(device=device, comm=comm)
     import torch
@@ -308,6 +317,8 @@ def describe(df, bins=10, corr_reject=0.9, **kwargs):
         return res, fut
 
     workers = column_workers(engine, kwargs.pop('workers', None))
+    if gk is not None:
+        workers = 1                      # the GK quantiles ride the whole-table numeric stage
     if workers == 1:
         # whole-table stages: pass 1 of every numeric column (two readbacks),
         # then every column's order statistics and pass 2 (two more) -- the
@@ -321,7 +332,7 @@ def describe(df, bins=10, corr_reject=0.9, **kwargs):
         if world == 1:
             group_cols = {i for i, pth in enumerate(engine.distinct_paths(num_cols, hints, bounds)) if pth == 'group'}
         stats = engine.numeric_stats_batch(num_cols, packs, bins, [k_vals.get(c.name, 2) for c in num_cols],
-                                           group_cols=group_cols)
+                                           group_cols=group_cols, gk=gk)
         for col, pack, st in zip(num_cols, packs, stats):
             bundles[col.name]['p1_pack'] = pack
             if st is not None:

@@ -737,7 +737,31 @@ class Engine:
                            'n_low': int(v[1]), 'n_unbinned': int(v[2]), 'hist': v[3:].astype(np.int64)})
         return result
 
-    def numeric_stats_batch(self, cols, packs, bins=10, ks=None, probs=PROBS, group_cols=()):
+    def gk_quantiles(self, col: DeviceColumn, probs=PROBS, partitions=1, accuracy=10000):
+        """percentile_approx(c, p, accuracy) (describe.py:205-206) as Spark 2.x's
+        ApproximatePercentile returns it when the column's rows form `partitions`
+        contiguous Spark partitions merged in partition order (sdp_gk_quantiles;
+        oracle/gk.py restates the algorithm).  Single rank: a sharded table's
+        partitions would have to be merged across ranks in order."""
+        if self.comm.world > 1:
+            raise NotImplementedError('quantile_mode="gk" runs on a single rank')
+        partitions = int(partitions)
+        wb = sdp.sdp_gk_workspace_bytes(partitions)
+        work = self._bytes(wb)
+        pr = self._h2d(np.asarray(probs, dtype=np.float64))
+        out = torch.empty(max(len(probs), 1), dtype=torch.float64, device=self.device)
+        status = self._u64(3, zero=True)
+        cs = col.sdp()
+        nat.annotate('gk', col_read_bytes(col))
+        sdp.sdp_gk_quantiles(ctypes.byref(cs), partitions, int(accuracy), ptr(pr), len(probs), ptr(work), wb,
+                             ptr(out), ptr(status), self._s())
+        st = status.cpu().numpy()
+        if st[0]:
+            raise RuntimeError('sdp_gk_quantiles: summary capacity exceeded (status %d)' % int(st[0]))
+        vals = out.cpu().numpy()
+        return {p: float(v) for p, v in zip(probs, vals)}
+
+    def numeric_stats_batch(self, cols, packs, bins=10, ks=None, probs=PROBS, group_cols=(), gk=None):
         """numeric_stats of every column (None for a column with no non-null
         value) with two host readbacks in all.  A bins value the reference
         rejects (describe.py:46 with bins=1) is recorded per column and raised
@@ -751,6 +775,10 @@ class Engine:
         p2_items, p2_idx = [], []
         for i, (qs, fb) in zip(live, qres):
             col, p1 = cols[i], packs[i][0]
+            if gk is not None and col.is_float:
+                # Spark's percentile_approx element (opt-in): also the q1/q3 of
+                # the outlier thresholds, as describe.py:212-223 uses them
+                qs = self.gk_quantiles(col, probs, gk.get('partitions', 1), gk.get('accuracy', 10000))
             mom = moments(p1, not col.is_float)
             st = NumericStats(count=p1['count'], n_valid=p1['n_valid'], n_nan=p1['n_nan'], n_zero=p1['n_zero'],
                               **mom)
