@@ -252,6 +252,8 @@ def label_kernels(label):
         if dt == 'bytes':
             return ['sdp::part_%s_rows_bytes_kernel' % st]
         return ['sdp::part_%s_rows_u64_kernel<%s>' % (st, _DT.get(dt, dt))]
+    if name == 'sdp_part_rows_records':
+        return ['sdp::part_records_rows_bytes_kernel']
     if name == 'sdp_part_dedup':
         return ['sdp::part_dedup_bytes_kernel'] if dt == 'bytes' else ['sdp::part_dedup_u64']
     if name in ('sdp_pass1', 'sdp_pass2', 'sdp_pass2_count'):
@@ -264,7 +266,7 @@ def label_kernels(label):
 # PMC traffic summary the bench reads `roofline.traffic` from, chosen by name
 # (never by file mtime, which a git checkout scrambles): the newest committed
 # summary of the default workload (tools/gpu_traffic.sh -> tools/traffic_summary.py).
-TRAFFIC_SUMMARY = {'c3': 'profiles/r02a_c3_traffic.json', 'c5': 'profiles/r02a_c5_traffic.json'}
+TRAFFIC_SUMMARY = {'c3': 'profiles/r02e_c3_traffic.json', 'c5': 'profiles/r02e_c5_traffic.json'}
 
 
 def pmc_traffic(label, path):
