@@ -379,6 +379,8 @@ __device__ __forceinline__ uint64_t mask_bytes(uint64_t v, int64_t avail) {
 // The same tile in two stages, so a kernel can issue the NEXT tile's validity
 // and offsets (stage A) before it fetches this tile's key bytes (stage B, which
 // depends on A) and works on them: one memory latency per tile instead of two.
+typedef uint32_t u32x4a4 __attribute__((ext_vector_type(4), aligned(4)));
+
 template <int RPT>
 struct BytesOffs {
     int64_t o0[RPT];
@@ -415,8 +417,13 @@ __device__ __forceinline__ void bytes_tile_b(const sdp_bytes_column &col, int64_
         const uint32_t ad = (uint32_t)((uintptr_t)pb & 3u);
         const uint32_t *p = (const uint32_t *)(pb - ad);
         const int64_t need = len <= SHORT_MAX ? (int64_t)(ad + len + 3) >> 2 : 0;
-#pragma unroll
-        for (int k = 0; k < 5; ++k) w[q][k] = (((a.vmask >> q) & 1u) && k < need) ? p[k] : 0u;
+        // words 0-3 as ONE 16-byte load (dword-aligned: unaligned-access mode;
+        // the data buffer's 16 padding bytes cover it), word 4 only when the
+        // string reaches it -- two load instructions per row instead of five
+        const bool ok = ((a.vmask >> q) & 1u) && need > 0;
+        const u32x4a4 v = ok ? *(const u32x4a4 *)p : u32x4a4{0u, 0u, 0u, 0u};
+        w[q][0] = v.x; w[q][1] = v.y; w[q][2] = v.z; w[q][3] = v.w;
+        w[q][4] = (ok && need > 4) ? p[4] : 0u;
     }
 #pragma unroll
     for (int q = 0; q < RPT; ++q) {
