@@ -341,10 +341,12 @@ def describe(df, bins=10, corr_reject=0.9, **kwargs):
                 # column that turns out CONST (one distinct value) is never NUM
                 if plots and st.error is None and owner[col.name] == rank and not _const_numeric(st):
                     early_plots[col.name] = _submit_plot(st)
-        if world == 1:
-            # every NUM column's countDistinct with shared readbacks
-            for col, d in zip(num_cols, engine.distinct_batch(num_cols, hints, bounds)):
-                bundles[col.name]['distinct_pre'] = d
+        # every NUM column's countDistinct with shared readbacks (and, sharded,
+        # shared collectives)
+        dist = engine.distinct_batch(num_cols, hints, bounds) if world == 1 else \
+            engine.distinct_batch_sharded(num_cols, hints, bounds)
+        for col, d in zip(num_cols, dist):
+            bundles[col.name]['distinct_pre'] = d
     if workers > 1:
         done = _describe_concurrent(engine, table.columns, one, workers)
     else:

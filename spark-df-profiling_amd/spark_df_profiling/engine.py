@@ -1278,105 +1278,161 @@ class Engine:
         return out
 
     def group_sharded(self, col):
-        """countDistinct (describe.py:143) of a fixed-width column of a
+        """group_sharded_batch of one column."""
+        return self.group_sharded_batch([col])[0]
+
+    def group_sharded_batch(self, cols):
+        """countDistinct (describe.py:143) of fixed-width columns of a
         row-sharded table, on the partitioning kernels: level-1 buckets (top
         B1 hash bits) are owned by contiguous rank ranges, so after the local
         bucket scatter ONE all-to-all of 8-byte records hands every owner all
         records of its buckets; level 2 and the LDS de-duplication then run on
         the owner, and the group counts are all-reduced.  Heavy keys come from
         the pooled samples of all ranks (the same set everywhere) and are
-        counted locally and all-reduced.  Returns None when the owner tables
-        overflow (the caller takes the table-exchange path)."""
+        counted locally and all-reduced.  The columns share their host round
+        trips and small collectives: ONE readback of every column's level-1
+        bucket starts, ONE all-gather of every column's bucket sizes (which
+        also give every rank its receive counts, so each all-to-all needs no
+        count exchange), ONE all-reduce + readback of every column's group
+        statistics.  Entries are None where the owner tables overflow (the
+        caller takes the table-exchange path)."""
         comm, world, rank = self.comm, self.comm.world, self.comm.rank
-        n = col.length
+        if not cols:
+            return []
         s = self._s()
         B1 = 10
         nb1 = 1 << B1
-        n_all = int(comm.allreduce_sum(torch.tensor([n], dtype=torch.int64, device=self.device)).item())
+        n_all = int(comm.allreduce_sum(torch.tensor([cols[0].length], dtype=torch.int64,
+                                                     device=self.device)).item())
         target = sdp.sdp_part_bucket_target(0, 0)
         b2 = min(10, max(1, math.ceil(math.log2(max(2.0, n_all / nb1 / target)))))
         nb2 = 1 << b2
-        stats = self._u64(68, zero=True)
-        cs = col.sdp()
-        hv = self._heavy_keys(col, False, gather=True)
-        hvref = ctypes.byref(hv['struct']) if hv else None
-        hcnt = self._u64(max(hv['n'] if hv else 1, 1), zero=True)
-        # level 1 on this rank's rows
-        rpb = sdp.sdp_part_rows_per_block(max(n, 1), 0)
-        grid = max(1, -(-n // rpb))
-        h1 = torch.zeros(nb1 * grid, dtype=torch.int32, device=self.device)
-        rb = col_read_bytes(col)
-        if n:
-            nat.annotate(_label(col, 'count'), rb)
-            sdp.sdp_part_rows(ctypes.byref(cs), None, hvref, B1, 0, ptr(h1), None, None, ptr(hcnt), ptr(stats), s)
-        o1 = self._scan(h1)
-        bs = o1[0:nb1 * grid:grid].cpu().numpy().astype(np.int64)
-        nrec = int(o1[-1].item())
-        bs = np.append(bs, nrec)
-        r1, keep1 = self._records(nrec, False)
-        if nrec:
-            nat.annotate(_label(col, 'scatter'), rb + nrec * 8)
-            sdp.sdp_part_rows(ctypes.byref(cs), None, hvref, B1, 1, None, ptr(o1), ctypes.byref(r1), ptr(hcnt),
-                              ptr(stats), s)
-        # ownership: rank r owns buckets [lo[r], lo[r + 1])
         lo = [(r * nb1) // world for r in range(world + 1)]
-        send = [int(bs[lo[r + 1]] - bs[lo[r]]) for r in range(world)]
-        sizes = torch.from_numpy(np.diff(bs)).to(self.device)
-        all_sizes = torch.stack(comm.allgather(sizes)).cpu().numpy()          # [world, nb1]
-        recv = comm.alltoallv(keep1[0][:nrec], send)
-        del keep1, r1
-        my = list(range(lo[rank], lo[rank + 1]))
-        # received layout: source-rank-major, my buckets in order inside each part
-        part_tot = all_sizes[:, lo[rank]:lo[rank + 1]].sum(axis=1)
-        part_base = np.concatenate([[0], np.cumsum(part_tot)[:-1]]).astype(np.int64)
-        segs = []                                                            # (bucket idx, start, end)
-        for bi, b in enumerate(my):
-            for src in range(world):
-                st0 = part_base[src] + all_sizes[src, lo[rank]:b].sum()
-                m = int(all_sizes[src, b])
-                for c0 in range(0, m, PART_CHUNK):
-                    segs.append((bi, st0 + c0, st0 + min(m, c0 + PART_CHUNK)))
-        nmy = len(my)
-        nrecv = int(recv.numel())
-        groups_local = 0
-        if nrecv:
-            seg = np.array(segs, dtype=np.int64)
-            nch = np.bincount(seg[:, 0], minlength=nmy).astype(np.int64)
-            k0 = np.concatenate([[0], np.cumsum(nch)[:-1]]).astype(np.int64)
-            K = int(nch.sum())
-            j = np.arange(K, dtype=np.int64) - k0[seg[:, 0]]
-            ch = np.empty((K, 4), dtype=np.int64)
-            ch[:, 0], ch[:, 1] = seg[:, 1], seg[:, 2]
-            ch[:, 2] = nb2 * k0[seg[:, 0]] + j
-            ch[:, 3] = nch[seg[:, 0]]
-            chunks = torch.from_numpy(ch).to(self.device)
-            rin = nat.SdpRecords(recv.data_ptr(), None, None)
-            h2 = torch.empty(nb2 * K, dtype=torch.int32, device=self.device)
-            nat.annotate('u64/count', nrecv * 8)
-            sdp.sdp_part_recs(ctypes.byref(rin), 0, ptr(chunks), K, B1, b2, 0, ptr(h2), None, None, s)
-            o2 = self._scan(h2)
-            rf, keepf = self._records(nrecv, False)
-            nat.annotate('u64/scatter', 2 * nrecv * 8)
-            sdp.sdp_part_recs(ctypes.byref(rin), 0, ptr(chunks), K, B1, b2, 1, None, ptr(o2), ctypes.byref(rf), s)
-            del recv, h2
-            sidx = (nb2 * k0[:, None] + np.arange(nb2)[None, :] * nch[:, None]).reshape(-1)
-            sidx = np.append(sidx, nb2 * K)
-            starts = o2[torch.from_numpy(sidx).to(self.device)].contiguous()
-            ngroups = torch.zeros(nmy * nb2, dtype=torch.int32, device=self.device)
-            nat.annotate('u64', nrecv * 8)
-            sdp.sdp_part_dedup(ctypes.byref(rf), 0, None, ptr(starts), nmy * nb2,
-                               4 if id(col) in self._near_unique else 0, None, None, ptr(ngroups),
-                               ptr(stats), s)
-        st = stats.clone()
-        st[4] = st[4:68].sum()
-        tot = comm.allreduce_sum(torch.cat([st[:5], hcnt[:max(hv['n'], 1)] if hv else hcnt[:1]]))
-        t = self._host_u64(tot)
-        if t[2] or t[3]:
-            return None
-        heavy_present = sum(1 for c in t[5:5 + (hv['n'] if hv else 0)] if c)
-        groups = t[4] + heavy_present + (1 if t[1] else 0)
-        return {'bytes': False, 'dense': False, 'rows': t[0], 'max_key_rows': 0, 'col': col, 'groups': groups,
-                'groups_local': groups, 'sharded': True}
+        ctxs = []
+        for col in cols:                                  # level 1 counts of every column, no readback
+            n = col.length
+            hv = self._heavy_keys(col, False, gather=True)
+            ctx = {'col': col, 'n': n, 'cs': col.sdp(), 'hv': hv, 'stats': self._u64(68, zero=True),
+                   'hcnt': self._u64(max(hv['n'] if hv else 1, 1), zero=True), 'rb': col_read_bytes(col)}
+            ctx['hvref'] = ctypes.byref(hv['struct']) if hv else None
+            rpb = sdp.sdp_part_rows_per_block(max(n, 1), 0)
+            grid = max(1, -(-n // rpb))
+            h1 = torch.zeros(nb1 * grid, dtype=torch.int32, device=self.device)
+            if n:
+                nat.annotate(_label(col, 'count'), ctx['rb'])
+                sdp.sdp_part_rows(ctypes.byref(ctx['cs']), None, ctx['hvref'], B1, 0, ptr(h1), None, None,
+                                  ptr(ctx['hcnt']), ptr(ctx['stats']), s)
+            ctx['o1'] = self._scan(h1)
+            ctx['bsn_dev'] = torch.cat([ctx['o1'][0:nb1 * grid:grid], ctx['o1'][-1:]])
+            ctxs.append(ctx)
+        flat = torch.cat([c['bsn_dev'] for c in ctxs]).cpu().numpy().astype(np.int64)
+        bss = [flat[i * (nb1 + 1):(i + 1) * (nb1 + 1)] for i in range(len(ctxs))]
+        sizes = torch.from_numpy(np.stack([np.diff(bs) for bs in bss]).reshape(-1)).to(self.device)
+        all_sizes = torch.stack(comm.allgather(sizes)).cpu().numpy().reshape(world, len(ctxs), nb1)
+        my0, my1 = lo[rank], lo[rank + 1]
+        nmy = my1 - my0
+        for ci, (ctx, bs) in enumerate(zip(ctxs, bss)):
+            col, stats = ctx['col'], ctx['stats']
+            nrec = int(bs[-1])
+            r1, keep1 = self._records(nrec, False)
+            if nrec:
+                nat.annotate(_label(col, 'scatter'), ctx['rb'] + nrec * 8)
+                sdp.sdp_part_rows(ctypes.byref(ctx['cs']), None, ctx['hvref'], B1, 1, None, ptr(ctx['o1']),
+                                  ctypes.byref(r1), ptr(ctx['hcnt']), ptr(stats), s)
+            del ctx['o1'], ctx['bsn_dev']
+            send = [int(bs[lo[r + 1]] - bs[lo[r]]) for r in range(world)]
+            S = all_sizes[:, ci, my0:my1]                                   # [world, nmy]
+            part_tot = S.sum(axis=1)
+            recv = comm.alltoallv_known(keep1[0][:nrec], send, [int(x) for x in part_tot])
+            del keep1, r1
+            nrecv = int(recv.numel())
+            if nrecv:
+                # received layout: source-rank-major, my buckets in order inside each
+                # part; chunks of <= PART_CHUNK records, ordered (bucket, source, chunk)
+                part_base = np.concatenate([[0], np.cumsum(part_tot)[:-1]]).astype(np.int64)
+                st0 = part_base[:, None] + np.concatenate([np.zeros((world, 1), np.int64),
+                                                          np.cumsum(S, axis=1)[:, :-1]], axis=1)
+                cnt = -(-S // PART_CHUNK)                                   # chunks per (source, bucket)
+                cb, csrc = cnt.T.reshape(-1), np.tile(np.arange(world), nmy)
+                bi_of = np.repeat(np.arange(nmy), world)
+                rep_b, rep_src = np.repeat(bi_of, cb), np.repeat(csrc, cb)
+                first = np.concatenate([[0], np.cumsum(cb)[:-1]])
+                jj = np.arange(int(cb.sum()), dtype=np.int64) - np.repeat(first, cb)
+                seg_start = st0[rep_src, rep_b] + jj * PART_CHUNK
+                seg_end = np.minimum(st0[rep_src, rep_b] + S[rep_src, rep_b], seg_start + PART_CHUNK)
+                nch = np.bincount(rep_b, minlength=nmy).astype(np.int64)
+                k0 = np.concatenate([[0], np.cumsum(nch)[:-1]]).astype(np.int64)
+                K = int(nch.sum())
+                j = np.arange(K, dtype=np.int64) - k0[rep_b]
+                ch = np.empty((K, 4), dtype=np.int64)
+                ch[:, 0], ch[:, 1] = seg_start, seg_end
+                ch[:, 2] = nb2 * k0[rep_b] + j
+                ch[:, 3] = nch[rep_b]
+                chunks = self._h2d(ch)
+                rin = nat.SdpRecords(recv.data_ptr(), None, None)
+                h2 = torch.empty(nb2 * K, dtype=torch.int32, device=self.device)
+                nat.annotate('u64/count', nrecv * 8)
+                sdp.sdp_part_recs(ctypes.byref(rin), 0, ptr(chunks), K, B1, b2, 0, ptr(h2), None, None, s)
+                o2 = self._scan(h2)
+                rf, keepf = self._records(nrecv, False)
+                nat.annotate('u64/scatter', 2 * nrecv * 8)
+                sdp.sdp_part_recs(ctypes.byref(rin), 0, ptr(chunks), K, B1, b2, 1, None, ptr(o2),
+                                  ctypes.byref(rf), s)
+                del recv, h2
+                sidx = (nb2 * k0[:, None] + np.arange(nb2)[None, :] * nch[:, None]).reshape(-1)
+                sidx = np.append(sidx, nb2 * K)
+                starts = o2[self._h2d(sidx)].contiguous()
+                ngroups = torch.zeros(nmy * nb2, dtype=torch.int32, device=self.device)
+                nat.annotate('u64', nrecv * 8)
+                sdp.sdp_part_dedup(ctypes.byref(rf), 0, None, ptr(starts), nmy * nb2,
+                                   4 if id(col) in self._near_unique else 0, None, None, ptr(ngroups),
+                                   ptr(stats), s)
+                del keepf, rf
+        # every column's group statistics in one all-reduce and one readback
+        parts, spans = [], []
+        for ctx in ctxs:
+            st = ctx['stats'].clone()
+            st[4] = st[4:68].sum()
+            hv = ctx['hv']
+            h = ctx['hcnt'][:max(hv['n'], 1)] if hv else ctx['hcnt'][:1]
+            spans.append((sum(p.numel() for p in parts), h.numel()))
+            parts += [st[:5], h]
+        t = self._host_u64(comm.allreduce_sum(torch.cat(parts)))
+        out = []
+        for ctx, (o, hn) in zip(ctxs, spans):
+            tt = t[o:o + 5 + hn]
+            if tt[2] or tt[3]:
+                out.append(None)
+                continue
+            hv = ctx['hv']
+            heavy_present = sum(1 for c in tt[5:5 + (hv['n'] if hv else 0)] if c)
+            groups = tt[4] + heavy_present + (1 if tt[1] else 0)
+            out.append({'bytes': False, 'dense': False, 'rows': tt[0], 'max_key_rows': 0, 'col': ctx['col'],
+                        'groups': groups, 'groups_local': groups, 'sharded': True})
+        return out
+
+    def distinct_batch_sharded(self, cols, hints, bounds):
+        """distinct_batch on a row-sharded table (every rank calls it with the
+        same columns; hints/bounds come from the merged pass 1): bitmaps for
+        small integral ranges, the global-table exchange for small key ranges,
+        group_sharded_batch for the rest (shared round trips)."""
+        comm = self.comm
+        n_all = int(comm.allreduce_sum(torch.tensor([cols[0].length if cols else 0], dtype=torch.int64,
+                                                    device=self.device)).item()) if cols else 0
+        out = [None] * len(cols)
+        grp = []
+        for i, (col, hint, bd) in enumerate(zip(cols, hints, bounds)):
+            if (bd is not None and col.kind == 'fixed' and col.dtype in self.BITMAP_DTYPES
+                    and bd[1] - bd[0] + 1 <= nat.BITMAP_MAX_BITS):
+                out[i] = self.distinct_bitmap(col, bd[0], bd[1] - bd[0] + 1)
+            elif hint is not None and hint * 4 <= max(n_all, 1):
+                out[i] = self._distinct_fixed_table(col, False, hint)['groups']
+            else:
+                grp.append(i)
+        for i, tab in zip(grp, self.group_sharded_batch([cols[i] for i in grp])):
+            out[i] = tab['groups'] if tab is not None else \
+                self._distinct_fixed_table(cols[i], False, hints[i])['groups']
+        return out
 
     def _scan(self, counts_i32):
         """Exclusive scan of int32 counts -> int64 offsets (n + 1 entries)."""
