@@ -144,7 +144,7 @@ def describe_1d(engine: Engine, col: DeviceColumn, nrows, bins, k, freq, bundle)
         tab = engine.distinct_fixed(col, with_counts=True)
         distinct, count = tab['groups'], tab['rows']
     else:                                          # string, binary, decimal
-        tab = engine.value_counts_bytes(col)
+        tab = bundle.pop('tab_pre', None) or engine.value_counts_bytes(col)
         distinct, count = tab['groups'], tab['rows']
 
     res = OrderedDict()
@@ -203,6 +203,14 @@ def _is_numeric(col):
     st = col.spark_type
     nested = ('array' in st) or ('struct' in st) or ('map' in st) or col.kind == 'nested'
     return col.kind != 'null' and not nested and (st in INT_TYPES or st in ('float', 'double'))
+
+
+def _is_byte_keyed(col):
+    """describe_1d's string/binary/decimal branch (value counts on byte keys)."""
+    st = col.spark_type
+    nested = ('array' in st) or ('struct' in st) or ('map' in st) or col.kind == 'nested'
+    return (col.kind == 'bytes' and not nested and st not in INT_TYPES and st not in ('float', 'double')
+            and st not in DATE_TYPES)
 
 
 def _numeric_series(st, nrows):
@@ -347,6 +355,11 @@ def describe(df, bins=10, corr_reject=0.9, **kwargs):
             engine.distinct_batch_sharded(num_cols, hints, bounds)
         for col, d in zip(num_cols, dist):
             bundles[col.name]['distinct_pre'] = d
+        if world == 1:
+            # every string/binary/decimal column's value counts with shared readbacks
+            byte_cols = [c for c in table.columns if _is_byte_keyed(c)]
+            for col, tab in zip(byte_cols, engine.value_counts_bytes_batch(byte_cols)):
+                bundles[col.name]['tab_pre'] = tab
     if workers > 1:
         done = _describe_concurrent(engine, table.columns, one, workers)
     else:

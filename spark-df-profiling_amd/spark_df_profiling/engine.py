@@ -950,6 +950,15 @@ class Engine:
         so every rank picks the same heavy keys."""
         if not isb and gather == (self.comm.world > 1) and self._heavy_pre and id(col) in self._heavy_pre:
             return self._heavy_pre.pop(id(col))        # sampled with pass 1 (numeric_pass1_batch)
+        smp = self._heavy_sample_launch(col, isb, gather)
+        if smp['readback'] is not None:
+            host = smp['readback'].cpu().numpy().view(np.uint64)
+        else:
+            host = smp['h'].cpu().numpy().view(np.uint64)
+        return self._heavy_keys_finish(smp, host)
+
+    def _heavy_sample_launch(self, col, isb, gather=False):
+        """Queue the heavy-key sample of `col` (no readback)."""
         ns = min(PART_SAMPLE, max(col.length, 1))
         if gather and self.comm.world > 1:
             ns = max(1, min(PART_SAMPLE // self.comm.world, col.length))   # pooled: PART_SAMPLE in all
@@ -966,12 +975,31 @@ class Engine:
             sdp.sdp_part_sample(ctypes.byref(col.sdp()), None, ns, ptr(h), None, s)
         if gather and self.comm.world > 1:
             h = torch.cat(self.comm.allgatherv(h))
+        # sample hashes (and byte-key metas) leave the device in one piece
+        readback = torch.cat([h, keep[2][:ns]]) if (isb and keep is not None) else None
+        return {'h': h, 'keep': keep, 'ns': ns, 'isb': isb, 'readback': readback}
+
+    def _heavy_keys_batch(self, cols):
+        """_heavy_keys of several byte columns with ONE readback of all samples."""
+        smps = [self._heavy_sample_launch(c, True) for c in cols]
+        parts = [sm['readback'] if sm['readback'] is not None else sm['h'] for sm in smps]
+        if not parts:
+            return []
+        flat = torch.cat(parts).cpu().numpy().view(np.uint64)
+        out, off = [], 0
+        for sm, p in zip(smps, parts):
+            out.append(self._heavy_keys_finish(sm, flat[off:off + p.numel()]))
+            off += p.numel()
+        return out
+
+    def _heavy_keys_finish(self, smp, host):
+        """Heavy keys from the host copy of a sample (see _heavy_sample_launch)."""
+        h, keep, ns, isb = smp['h'], smp['keep'], smp['ns'], smp['isb']
         meta = None
-        if isb and keep is not None:            # sample hashes and metas in one readback
-            both = torch.cat([h, keep[2][:ns]]).cpu().numpy().view(np.uint64)
-            hn, meta = both[:h.numel()], both[h.numel():]
+        if isb and keep is not None:
+            hn, meta = host[:h.numel()], host[h.numel():]
         else:
-            hn = h.cpu().numpy().view(np.uint64)
+            hn = host
         pos = np.nonzero(hn != np.uint64(U64))[0]
         n_valid = pos.size
         if isb and pos.size:
@@ -1052,14 +1080,18 @@ class Engine:
             off += m
         return out
 
-    def _group_prepare(self, col, with_counts):
+    _NO_HV = object()
+
+    def _group_prepare(self, col, with_counts, hv=_NO_HV):
         """Geometry and buffers of the two-level partitioning of `col` (None
-        when the column needs more than 20 hash bits of buckets)."""
+        when the column needs more than 20 hash bits of buckets); `hv` = heavy
+        keys already sampled (_heavy_keys_batch)."""
         isb = col.kind == 'bytes'
         with_counts = with_counts or isb
         n = col.length
         target = sdp.sdp_part_bucket_target(int(isb), int(with_counts))
-        hv = self._heavy_keys(col, isb)
+        if hv is Engine._NO_HV:
+            hv = self._heavy_keys(col, isb)
         n_rec = n
         if isb and hv is not None and 'rec_frac' in hv:
             # byte columns: size the buckets for the records the sample predicts
@@ -1515,6 +1547,37 @@ class Engine:
             if tab is not None:
                 return self._exchange_bytes(tab) if self.comm.world > 1 else tab
         return self.value_counts_bytes_table(col)
+
+    def value_counts_bytes_batch(self, cols):
+        """value_counts_bytes of several byte columns on one rank with shared
+        readbacks: ONE readback of every column's heavy-key sample, then per
+        column the one-read records, the bucket-start readback and the
+        scatters/dedup, and ONE readback of every column's group statistics."""
+        out = [None] * len(cols)
+        if self.comm.world > 1:
+            return [self.value_counts_bytes(c) for c in cols]
+        big = [i for i, c in enumerate(cols) if c.length >= (1 << 16)]
+        hvs = self._heavy_keys_batch([cols[i] for i in big])
+        done = []
+        for i, hv in zip(big, hvs):
+            ctx = self._group_prepare(cols[i], True, hv=hv)
+            if ctx is None:
+                continue
+            self._group_count(ctx)
+            self._group_scan(ctx)
+            self._group_middle(ctx, ctx['bsn_dev'].cpu().numpy().astype(np.int64))
+            done.append((i, ctx))
+        if done:
+            sizes = [ctx['stats_dev'].numel() for _, ctx in done]
+            allst = self._host_u64(torch.cat([ctx['stats_dev'] for _, ctx in done]))
+            off = 0
+            for (i, ctx), m in zip(done, sizes):
+                out[i] = self._group_end(ctx, allst[off:off + m], True)
+                off += m
+        for i, c in enumerate(cols):                 # small columns, collisions, table overflow
+            if out[i] is None:
+                out[i] = self.value_counts_bytes_table(c)
+        return out
 
     def value_counts_bytes_table(self, col, row_counts=None, exchanged=False, capacity=None):
         """Global open-addressing byte-key table (fallback / multi-rank path)."""
