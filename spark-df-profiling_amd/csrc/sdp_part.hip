@@ -291,9 +291,14 @@ __global__ void __launch_bounds__(CT) part_count_rows_u64_kernel(sdp_column col,
 template <typename T>
 __global__ void __launch_bounds__(ST) part_scatter_rows_u64_kernel(sdp_column col, HeavyArg heavy, int b1,
                                                                    int64_t rows_per_block, const uint64_t *offs,
-                                                                   uint64_t *out_h) {
+                                                                   uint64_t *out_h, int xcd_map) {
     __shared__ ScatterLds s;
-    const int G = gridDim.x, g = blockIdx.x, t = threadIdx.x;
+    const int G = gridDim.x, t = threadIdx.x;
+    // XCD-aware: workgroups are dealt to the 8 XCDs round robin; with the map,
+    // one XCD's workgroups take consecutive row blocks, so in every bucket the
+    // runs it writes at once are adjacent (one L2 sees both halves of a line
+    // two blocks share, and the XCD's write stream stays within fewer pages)
+    const int g = (xcd_map && G % 8 == 0) ? (int)((blockIdx.x % 8) * (G / 8) + blockIdx.x / 8) : (int)blockIdx.x;
     const int nb = 1 << b1;
     const int shift = 64 - b1;
     const int64_t r0 = (int64_t)g * rows_per_block;
@@ -712,14 +717,21 @@ __global__ void __launch_bounds__(ST) part_scatter_recs_kernel(const uint64_t *i
                                                                const uint64_t *in_meta, const Chunk *chunks,
                                                                int64_t nchunks, int b1, int b2, const uint64_t *offs,
                                                                uint64_t *out_k0, uint64_t *out_k1,
-                                                               uint64_t *out_meta) {
+                                                               uint64_t *out_meta, int xcd_map) {
     constexpr int RPT = BYTES ? B_S_RPT : S_RPT;
     constexpr int TILE = ST * RPT;
     __shared__ RecsLds<BYTES> s;
     const int t = threadIdx.x;
     const int nb = 1 << b2;
     const int shift = 64 - b1 - b2;
-    for (int64_t c = blockIdx.x; c < nchunks; c += gridDim.x) {
+    // XCD-aware (as in the row scatter): each XCD takes one contiguous range of
+    // chunks, so the chunks it runs at once are neighbours in every sub-bucket
+    const bool xm = xcd_map && gridDim.x % 8 == 0;
+    const int64_t per = xm ? (nchunks + 7) / 8 : nchunks;
+    const int64_t c0 = xm ? (int64_t)(blockIdx.x % 8) * per + blockIdx.x / 8 : (int64_t)blockIdx.x;
+    const int64_t c1 = xm ? min(nchunks, (int64_t)(blockIdx.x % 8 + 1) * per) : nchunks;
+    const int64_t cstep = xm ? gridDim.x / 8 : gridDim.x;
+    for (int64_t c = c0; c < c1; c += cstep) {
         const Chunk ch = chunks[c];
         for (int b = t; b < nb; b += ST) {
             s.hist[b] = 0;
@@ -1346,13 +1358,20 @@ static int grid_of(int64_t items, int64_t cap) {
     return (int)(items < cap ? items : cap);
 }
 
+// SDP_XCD_MAP=0 turns the XCD-aware workgroup mapping of the scatters off (A/B runs)
+static int xcd_map_enabled() {
+    const char *e = getenv("SDP_XCD_MAP");
+    return (e && e[0] == '0') ? 0 : 1;
+}
+
 template <typename T>
 static void launch_rows_u64(int phase, int grid, hipStream_t s, const sdp_column &c, HeavyArg hv, int b1, int64_t rpb,
                             uint32_t *hist, const uint64_t *offs, uint64_t *out, uint64_t *hc, uint64_t *st) {
     if (phase == 0)
         hipLaunchKernelGGL((part_count_rows_u64_kernel<T>), dim3(grid), dim3(CT), 0, s, c, hv, b1, rpb, hist, hc, st);
     else
-        hipLaunchKernelGGL((part_scatter_rows_u64_kernel<T>), dim3(grid), dim3(ST), 0, s, c, hv, b1, rpb, offs, out);
+        hipLaunchKernelGGL((part_scatter_rows_u64_kernel<T>), dim3(grid), dim3(ST), 0, s, c, hv, b1, rpb, offs, out,
+                           xcd_map_enabled());
 }
 
 }  // namespace sdp
@@ -1481,14 +1500,14 @@ int sdp_part_recs(const sdp_records *in, int32_t is_bytes, const sdp_chunk *d_ch
                                ch, nchunks, b1, b2, d_hist);
         else
             hipLaunchKernelGGL(part_scatter_recs_kernel<true>, dim3(grid), dim3(ST), 0, s, in->d_k0, in->d_k1,
-                               in->d_meta, ch, nchunks, b1, b2, d_offsets, o0, o1, o2);
+                               in->d_meta, ch, nchunks, b1, b2, d_offsets, o0, o1, o2, xcd_map_enabled());
     } else {
         if (phase == 0)
             hipLaunchKernelGGL(part_count_recs_kernel<false>, dim3(grid), dim3(CT), 0, s, in->d_k0, nullptr, nullptr,
                                ch, nchunks, b1, b2, d_hist);
         else
             hipLaunchKernelGGL(part_scatter_recs_kernel<false>, dim3(grid), dim3(ST), 0, s, in->d_k0, nullptr, nullptr,
-                               ch, nchunks, b1, b2, d_offsets, o0, nullptr, nullptr);
+                               ch, nchunks, b1, b2, d_offsets, o0, nullptr, nullptr, xcd_map_enabled());
     }
     return check_launch("part_recs_kernel");
 }
