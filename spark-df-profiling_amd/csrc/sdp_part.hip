@@ -662,6 +662,51 @@ __global__ void __launch_bounds__(BR_T, 4) part_records_rows_bytes_kernel(sdp_by
     block_add_u64(rows, &stats[0]);
 }
 
+// fixed keys: 16-byte loads of record pairs (an even record index; the pairs
+// that straddle a chunk edge are read element by element), then one LDS atomic
+// per record
+__global__ void __launch_bounds__(CT) part_count_recs_u64_kernel(const uint64_t *in_k0, const Chunk *chunks,
+                                                                 int64_t nchunks, int b1, int b2, uint32_t *hist) {
+    constexpr int PP = 8;                       // record pairs per thread per step
+    __shared__ uint32_t s_hist[MAXB];
+    const int t = threadIdx.x;
+    const int nb = 1 << b2;
+    const int shift = 64 - b1 - b2;
+    for (int64_t c = blockIdx.x; c < nchunks; c += gridDim.x) {
+        const Chunk ch = chunks[c];
+        for (int b = t; b < nb; b += CT) s_hist[b] = 0;
+        lds_barrier();
+        const int64_t a0 = ch.start & ~(int64_t)1;
+        for (int64_t base = a0; base < ch.end; base += (int64_t)CT * PP * 2) {
+            uint64_t x[PP][2];
+            int64_t rr[PP];
+#pragma unroll
+            for (int q = 0; q < PP; ++q) {
+                const int64_t r = base + 2 * ((int64_t)q * CT + t);
+                rr[q] = r;
+                if (r >= ch.start && r + 1 < ch.end) {
+                    const ulonglong2 v = *(const ulonglong2 *)(in_k0 + r);
+                    x[q][0] = v.x; x[q][1] = v.y;
+                } else {
+                    x[q][0] = (r >= ch.start && r < ch.end) ? in_k0[r] : 0ull;
+                    x[q][1] = (r + 1 >= ch.start && r + 1 < ch.end) ? in_k0[r + 1] : 0ull;
+                }
+            }
+#pragma unroll
+            for (int q = 0; q < PP; ++q)
+#pragma unroll
+                for (int e = 0; e < 2; ++e) {
+                    const int64_t r = rr[q] + e;
+                    if (r >= ch.start && r < ch.end)
+                        atomicAdd(&s_hist[(int)((x[q][e] >> shift) & (uint64_t)(nb - 1))], 1u);
+                }
+        }
+        lds_barrier();
+        for (int b = t; b < nb; b += CT) hist[ch.hbase + (int64_t)b * ch.hstride] = s_hist[b];
+        lds_barrier();
+    }
+}
+
 template <bool BYTES>
 __global__ void __launch_bounds__(CT) part_count_recs_kernel(const uint64_t *in_k0, const uint64_t *in_k1,
                                                              const uint64_t *in_meta, const Chunk *chunks,
@@ -1503,8 +1548,15 @@ int sdp_part_recs(const sdp_records *in, int32_t is_bytes, const sdp_chunk *d_ch
                                in->d_meta, ch, nchunks, b1, b2, d_offsets, o0, o1, o2, xcd_map_enabled());
     } else {
         if (phase == 0)
-            hipLaunchKernelGGL(part_count_recs_kernel<false>, dim3(grid), dim3(CT), 0, s, in->d_k0, nullptr, nullptr,
-                               ch, nchunks, b1, b2, d_hist);
+        {
+            const char *e = getenv("SDP_COUNT_PAIRS");
+            if (e && e[0] == '0')
+                hipLaunchKernelGGL(part_count_recs_kernel<false>, dim3(grid), dim3(CT), 0, s, in->d_k0, nullptr,
+                                   nullptr, ch, nchunks, b1, b2, d_hist);
+            else
+                hipLaunchKernelGGL(part_count_recs_u64_kernel, dim3(grid), dim3(CT), 0, s, in->d_k0, ch, nchunks, b1,
+                                   b2, d_hist);
+        }
         else
             hipLaunchKernelGGL(part_scatter_recs_kernel<false>, dim3(grid), dim3(ST), 0, s, in->d_k0, nullptr, nullptr,
                                ch, nchunks, b1, b2, d_offsets, o0, nullptr, nullptr, xcd_map_enabled());
