@@ -162,6 +162,17 @@ int64_t sdp_gk_workspace_bytes(int32_t n_partitions);
 int sdp_gk_quantiles(const sdp_column *col, int32_t n_partitions, int32_t accuracy,
                      const double *d_probs, int32_t n_probs, void *d_work, int64_t work_bytes,
                      double *d_out, int64_t *d_status, void *stream);
+/* The two halves of sdp_gk_quantiles, for a row-sharded table: every rank
+ * builds the digests of its own partitions (sdp_gk_partitions), the digests
+ * are gathered into one workspace laid out as sdp_gk_layout describes
+ * (out4 = {first partition state, bytes per partition, offset of the sample
+ * buffers, samples per buffer}; a partition state is int64 {len, count,
+ * buffer, status}), and sdp_gk_merge merges them in partition order. */
+int sdp_gk_layout(int32_t n_partitions, int64_t *out4);
+int sdp_gk_partitions(const sdp_column *col, int32_t n_partitions, int32_t accuracy, void *d_work,
+                      int64_t work_bytes, void *stream);
+int sdp_gk_merge(int32_t n_partitions, int32_t accuracy, const double *d_probs, int32_t n_probs,
+                 void *d_work, int64_t work_bytes, double *d_out, int64_t *d_status, void *stream);
 
 #define SDP_PASS1_WAVES 4     /* waves per pass-1 workgroup = candidate segments per block */
 

@@ -2295,6 +2295,51 @@ extern "C" int64_t sdp_gk_workspace_bytes(int32_t n_partitions) {
     return gk_head_off(n_partitions) + (int64_t)n_partitions * gk_part_bytes() + 2 * (2 * GK_CAP) * 24;
 }
 
+extern "C" int sdp_gk_layout(int32_t n_partitions, int64_t *out4) {
+    if (n_partitions < 1 || out4 == nullptr) return set_error(SDP_EINVAL, "sdp_gk_layout: args");
+    out4[0] = gk_head_off(n_partitions);        // partition p's state at out4[0] + p * out4[1]
+    out4[1] = gk_part_bytes();
+    out4[2] = 2 * GK_HBUF * 8;                  // sample buffer b of a partition at + out4[2] + b * out4[3] * 24
+    out4[3] = GK_CAP;                           // (v[cap] f64, g[cap] i64, d[cap] i64)
+    return SDP_OK;
+}
+
+extern "C" int sdp_gk_partitions(const sdp_column *col, int32_t n_partitions, int32_t accuracy, void *d_work,
+                                 int64_t work_bytes, void *stream) {
+    int rc = check_col(col, "sdp_gk_partitions");
+    if (rc) return rc;
+    if (n_partitions < 1 || n_partitions > 65535) return set_error(SDP_EINVAL, "sdp_gk_partitions: n_partitions %d", n_partitions);
+    if (accuracy < 1) return set_error(SDP_EINVAL, "sdp_gk_partitions: accuracy %d", accuracy);
+    if (work_bytes < sdp_gk_workspace_bytes(n_partitions))
+        return set_error(SDP_ECAP, "sdp_gk_partitions: workspace %lld < %lld", (long long)work_bytes,
+                         (long long)sdp_gk_workspace_bytes(n_partitions));
+    const double eps = 1.0 / (double)accuracy;
+    hipStream_t s = (hipStream_t)stream;
+    switch (col->dtype) {
+    case SDP_F64:
+        hipLaunchKernelGGL(gk_partition_kernel<double>, dim3(n_partitions), dim3(GK_T), 0, s, *col, n_partitions, eps,
+                           (uint8_t *)d_work);
+        break;
+    case SDP_F32:
+        hipLaunchKernelGGL(gk_partition_kernel<float>, dim3(n_partitions), dim3(GK_T), 0, s, *col, n_partitions, eps,
+                           (uint8_t *)d_work);
+        break;
+    default: return set_error(SDP_EINVAL, "sdp_gk_partitions: dtype %d is not float/double", col->dtype);
+    }
+    return check_launch("gk_partition_kernel");
+}
+
+extern "C" int sdp_gk_merge(int32_t n_partitions, int32_t accuracy, const double *d_probs, int32_t n_probs,
+                            void *d_work, int64_t work_bytes, double *d_out, int64_t *d_status, void *stream) {
+    if (n_partitions < 1 || n_partitions > 65535 || accuracy < 1) return set_error(SDP_EINVAL, "sdp_gk_merge: args");
+    if (n_probs < 0 || d_out == nullptr || d_status == nullptr || (n_probs > 0 && d_probs == nullptr))
+        return set_error(SDP_EINVAL, "sdp_gk_merge: outputs");
+    if (work_bytes < sdp_gk_workspace_bytes(n_partitions)) return set_error(SDP_ECAP, "sdp_gk_merge: workspace");
+    hipLaunchKernelGGL(gk_merge_query_kernel, dim3(1), dim3(GK_T), 0, (hipStream_t)stream, n_partitions,
+                       1.0 / (double)accuracy, (uint8_t *)d_work, d_probs, n_probs, d_out, d_status);
+    return check_launch("gk_merge_query_kernel");
+}
+
 extern "C" int sdp_gk_quantiles(const sdp_column *col, int32_t n_partitions, int32_t accuracy, const double *d_probs,
                                 int32_t n_probs, void *d_work, int64_t work_bytes, double *d_out, int64_t *d_status,
                                 void *stream) {

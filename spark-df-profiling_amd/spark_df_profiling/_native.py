@@ -160,6 +160,9 @@ _SIGNATURES = {
     'sdp_part_records_chunks': (_I64, [_I64]),
     'sdp_gk_workspace_bytes': (_I64, [_I32]),
     'sdp_gk_quantiles': (ctypes.c_int, [_COL, _I32, _I32, _P, _I32, _P, _I64, _P, _P, _P]),
+    'sdp_gk_layout': (ctypes.c_int, [_I32, _P]),
+    'sdp_gk_partitions': (ctypes.c_int, [_COL, _I32, _I32, _P, _I64, _P]),
+    'sdp_gk_merge': (ctypes.c_int, [_I32, _I32, _P, _I32, _P, _I64, _P, _P, _P]),
     'sdp_part_rows_records': (ctypes.c_int, [_BCOL, _HVY, _I32, _P, _P, _REC, _P, _P, _P]),
     'sdp_part_dedup': (ctypes.c_int, [_REC, _I32, _BCOL, _P, _I64, _I32, _P, _P, _P, _P, _P]),
     'sdp_part_compact': (ctypes.c_int, [_P, _P, _P, _P, _P, _I64, _P, _P, _P]),

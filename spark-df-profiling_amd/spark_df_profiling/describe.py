@@ -283,7 +283,8 @@ def describe(df, bins=10, corr_reject=0.9, **kwargs):
     ``quantile_mode`` ('exact', the default: float quantiles are the element at
     rank ceil(pN), inside percentile_approx's rank window; 'gk': Spark 2.x's
     percentile_approx element for ``spark_partitions`` contiguous partitions,
-    restated from QuantileSummaries -- single rank only)."""
+    restated from QuantileSummaries; on a sharded table each rank's rows form
+    spark_partitions / world of them)."""
     comm = kwargs.pop('comm', None)
     device = kwargs.pop('device', None)
     plots = kwargs.pop('plots', True)

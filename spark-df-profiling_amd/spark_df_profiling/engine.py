@@ -743,9 +743,9 @@ class Engine:
         contiguous Spark partitions merged in partition order (sdp_gk_quantiles;
         oracle/gk.py restates the algorithm).  Single rank: a sharded table's
         partitions would have to be merged across ranks in order."""
-        if self.comm.world > 1:
-            raise NotImplementedError('quantile_mode="gk" runs on a single rank')
         partitions = int(partitions)
+        if self.comm.world > 1:
+            return self._gk_quantiles_sharded(col, probs, partitions, accuracy)
         wb = sdp.sdp_gk_workspace_bytes(partitions)
         work = self._bytes(wb)
         pr = self._h2d(np.asarray(probs, dtype=np.float64))
@@ -760,6 +760,62 @@ class Engine:
             raise RuntimeError('sdp_gk_quantiles: summary capacity exceeded (status %d)' % int(st[0]))
         vals = out.cpu().numpy()
         return {p: float(v) for p, v in zip(probs, vals)}
+
+    def _gk_quantiles_sharded(self, col, probs, partitions, accuracy):
+        """gk_quantiles of a row-sharded column: rank r's rows form Spark
+        partitions r*k .. r*k + k - 1 (k = partitions / world, each a
+        contiguous share of the rank's rows); every rank builds its own
+        partition digests, the digests are all-gathered, and every rank merges
+        all of them in partition order (identical results everywhere)."""
+        comm, world = self.comm, self.comm.world
+        if partitions % world:
+            raise ValueError('spark_partitions must be a multiple of the number of ranks')
+        k = partitions // world
+
+        def layout(P):
+            lay = (ctypes.c_int64 * 4)()
+            sdp.sdp_gk_layout(P, ctypes.addressof(lay))
+            return [int(x) for x in lay]
+
+        s = self._s()
+        head, pb, boff, cap = layout(k)
+        wb = sdp.sdp_gk_workspace_bytes(k)
+        work = self._bytes(wb)
+        cs = col.sdp()
+        nat.annotate('gk', col_read_bytes(col))
+        sdp.sdp_gk_partitions(ctypes.byref(cs), k, int(accuracy), ptr(work), wb, s)
+        states = work[:k * 32].view(torch.int64).view(k, 4)
+        st = states.cpu().numpy()
+        pieces = [states.reshape(-1)]
+        for j in range(k):
+            n_j, which = int(st[j, 0]), int(st[j, 2])
+            base = head + j * pb + boff + which * cap * 24
+            for f in range(3):                       # v (f64 bits), g, d
+                pieces.append(work[base + f * cap * 8: base + f * cap * 8 + n_j * 8].view(torch.int64))
+        parts = comm.allgatherv(torch.cat(pieces))
+        head2, pb2, boff2, cap2 = layout(partitions)
+        wb2 = sdp.sdp_gk_workspace_bytes(partitions)
+        work2 = torch.zeros(wb2, dtype=torch.uint8, device=self.device)
+        hdr = torch.zeros((partitions, 4), dtype=torch.int64, device=self.device)
+        for r, pk in enumerate(parts):
+            sth = pk[:k * 4].view(k, 4).cpu().numpy()
+            off = k * 4
+            for j in range(k):
+                p, n_j = r * k + j, int(sth[j, 0])
+                hdr[p, 0], hdr[p, 1], hdr[p, 2], hdr[p, 3] = n_j, int(sth[j, 1]), 0, int(sth[j, 3])
+                base = head2 + p * pb2 + boff2
+                for f in range(3):
+                    work2[base + f * cap2 * 8: base + f * cap2 * 8 + n_j * 8].view(torch.int64)[:] = pk[off:off + n_j]
+                    off += n_j
+        work2[:partitions * 32].view(torch.int64)[:] = hdr.reshape(-1)
+        pr = self._h2d(np.asarray(probs, dtype=np.float64))
+        out = torch.empty(max(len(probs), 1), dtype=torch.float64, device=self.device)
+        status = self._u64(3, zero=True)
+        sdp.sdp_gk_merge(partitions, int(accuracy), ptr(pr), len(probs), ptr(work2), wb2, ptr(out), ptr(status), s)
+        stv = status.cpu().numpy()
+        if stv[0]:
+            raise RuntimeError('sdp_gk_merge: summary capacity exceeded (status %d)' % int(stv[0]))
+        return {p: float(v) for p, v in zip(probs, out.cpu().numpy())}
 
     def numeric_stats_batch(self, cols, packs, bins=10, ks=None, probs=PROBS, group_cols=(), gk=None):
         """numeric_stats of every column (None for a column with no non-null

@@ -23,6 +23,45 @@ import datagen
 from compare import assert_describe_equal
 
 
+def _check_gk(comm, rank, world, dev):
+    """quantile_mode='gk' on a row-sharded float column: rank r's rows form
+    Spark partitions r*k .. r*k+k-1 (k = 2 per rank), so the answer is
+    percentile_approx over those partitions in rank-major order."""
+    import numpy as np
+    from spark_df_profiling import describe
+    from spark_df_profiling.columns import DeviceTable
+    rng = np.random.default_rng(23)
+    n = 70_001
+    x = rng.lognormal(0.0, 1.5, n)
+    x[rng.random(n) < 0.01] = np.nan
+    x[::97] = 1.0                                    # a heavy value
+    valid = rng.random(n) > 0.02
+    t = pa.table({'x': pa.array(x, mask=~valid)})
+    full = DeviceTable.from_arrow(t, dev)
+    per = (n // world) // 16 * 16
+    bounds = [(r * per, n if r == world - 1 else (r + 1) * per) for r in range(world)]
+    start, stop = bounds[rank]
+    k = 2
+    got = describe(full.slice_rows(start, stop), comm=comm, plots=False, quantile_mode='gk',
+                   spark_partitions=k * world)
+    if rank != 0:
+        return 0
+    from oracle import gk
+    parts = []
+    for a, b in bounds:
+        parts += gk.split_rows(x[a:b], valid[a:b], k)
+    probs = [0.05, 0.25, 0.5, 0.75, 0.95]
+    want = gk.percentile_approx(parts, probs)
+    v = got['variables']
+    bad = [(p, v.loc['x', '%d%%' % int(p * 100)], w) for p, w in zip(probs, want)
+           if v.loc['x', '%d%%' % int(p * 100)] != w]
+    if bad:
+        print('[gk] MISMATCH world=%d %s' % (world, bad), flush=True)
+        return 1
+    print('[gk] OK world=%d' % world, flush=True)
+    return 0
+
+
 def main():
     backend = sys.argv[1] if len(sys.argv) > 1 else 'gloo'
     rank = int(os.environ['RANK'])
@@ -81,6 +120,8 @@ def main():
             except AssertionError as e:
                 failures += 1
                 print('[%s] MISMATCH world=%d\n%s' % (name, world, e), flush=True)
+    if not only or 'gk' in only:
+        failures += _check_gk(comm, rank, world, dev)
     dist.barrier()
     dist.destroy_process_group()
     if rank == 0:

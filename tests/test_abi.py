@@ -92,6 +92,19 @@ def test_part_argument_checks_without_gpu():
     assert rpb % 1024 == 0
 
 
+def test_gk_layout_host_arithmetic():
+    """sdp_gk_layout (host-only): the workspace offsets the sharded GK merge
+    writes gathered digests into."""
+    import ctypes
+    from spark_df_profiling._native import sdp
+    lay = (ctypes.c_int64 * 4)()
+    sdp.sdp_gk_layout(3, ctypes.addressof(lay))
+    head, pb, boff, cap = list(lay)
+    assert head >= 3 * 32 and head % 256 == 0
+    assert pb == boff + 2 * cap * 24 and cap >= 60000
+    assert sdp.sdp_gk_workspace_bytes(3) >= head + 3 * pb
+
+
 def test_select_rounds_host_arithmetic():
     """sdp_select_rounds (host-only): 11-bit radix rounds a select over
     [lo, hi] needs -- every rank of a sharded select runs exactly this many
