@@ -38,6 +38,9 @@ from .columns import DeviceColumn, decimal_from_key
 PROBS = (0.05, 0.25, 0.5, 0.75, 0.95)          # describe.py:207
 SAMPLE_TOTAL = 16384
 SAMPLE2_TOTAL = 131072        # second sample narrowing the quantile windows (sdp_quantile_refine_batch)
+# third sample narrowing them again (its in-window keys, ~4 % of it, must fit
+# the refine kernel's 16 K-key LDS sort; 0 disables)
+SAMPLE3_TOTAL = int(os.environ.get('SDP_SAMPLE3', 360448))
 SORT_MAX = 16384
 GSORT_MAX = 8192
 TOPK = 50                                       # describe.py:259
@@ -913,6 +916,15 @@ class Engine:
             if world > 1:
                 s2 = torch.cat([p.view(len(cols), ns2) for p in self.comm.allgather(s2)], dim=1).contiguous()
             sdp.sdp_quantile_refine_batch(ptr(s2), ns2 * world, len(cols), ptr(pr), len(probs), ptr(plans_dev), s)
+            ns3 = SAMPLE3_TOTAL // world
+            if ns3 > ns2 and (world > 1 or min(c.length for c in cols) > SAMPLE2_TOTAL):
+                s3 = self._u64(len(cols) * ns3)
+                for i, col in enumerate(cols):
+                    cs = col.sdp()
+                    sdp.sdp_sample_keys(ctypes.byref(cs), ns3, ptr(s3[i * ns3:]), s)
+                if world > 1:
+                    s3 = torch.cat([p.view(len(cols), ns3) for p in self.comm.allgather(s3)], dim=1).contiguous()
+                sdp.sdp_quantile_refine_batch(ptr(s3), ns3 * world, len(cols), ptr(pr), len(probs), ptr(plans_dev), s)
         # heavy-key samples of the columns the partitioning path will group
         # (single rank, >= 64 K rows), sorted on the GPU and read back with the
         # plans; the host finds the heavy keys while pass 1 runs

@@ -6,7 +6,7 @@ mkdir -p gpurun_out
 export TMPDIR=/tmp
 T=${1:-pk}; STAGE=${2:-group}; COL=${3:-str_card1e8}
 timeout -s KILL 300 rocprofv3 --kernel-trace --output-format csv \
-  --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_LDS_BANK_CONFLICT \
+  --pmc ${PMC:-SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_LDS_BANK_CONFLICT} \
   --kernel-include-regex 'sdp::' -d gpurun_out/${T}_pmc -o run -- python3 tools/kbench.py $STAGE 1000000000 1 $COL \
   > gpurun_out/${T}_pmc.log 2>&1 || { tail -5 gpurun_out/${T}_pmc.log; exit 1; }
 python3 - gpurun_out/${T}_pmc > gpurun_out/${T}_pmc.txt <<'PY'
@@ -17,6 +17,9 @@ for f in glob.glob(sys.argv[1] + '/**/*counter_collection.csv', recursive=True):
         k = r['Kernel_Name'].split('(')[0].replace('void ', '')[:60]
         v[k][r['Counter_Name']] += float(r['Counter_Value'])
 for k, c in v.items():
+    if 'SQ_WAVE_CYCLES' not in c:
+        print('%-60s %s' % (k, '  '.join('%s %.4g' % kv for kv in sorted(c.items()))))
+        continue
     wc = c['SQ_WAVE_CYCLES'] or 1
     print('%-60s wave_cyc %.3g  wait_any %.2f  wait_inst %.2f  active %.2f  valu %.2f  lds %.2f  bankconf/lds %.2f' % (
         k, wc, c['SQ_WAIT_ANY'] / wc, c['SQ_WAIT_INST_ANY'] / wc, c['SQ_ACTIVE_INST_ANY'] / wc,

@@ -26,6 +26,8 @@ for r in range(reps):
         e._distinct_fixed_table(col) if col.kind != 'bytes' else e.value_counts_bytes_table(col, capacity=cap)
     elif what == 'pass1':
         e.numeric_pass1(col)
+    elif what == 'pass1b':                   # the describe() path: batched plans with refined windows
+        e.numeric_pass1_batch([col])
     elif what == 'pass2':
         e.numeric_stats(col)
     elif what == 'gram':
