@@ -372,13 +372,15 @@ __device__ __forceinline__ void p1_elem(P1Thread &st, const P1Ctx &cx, T x, bool
         for (int w = 0; w < SDP_MAX_WINDOWS; ++w) {
             const uint64_t lo = cx.lo[w], hi = cx.hi[w];
             st.gt[w] += (uint32_t)(key < lo);
-            const uint64_t m = __builtin_amdgcn_uicmpl(key, lo, 35 /*UGE*/) & __builtin_amdgcn_uicmpl(key, hi, 37 /*ULE*/);
+            // the lane's own compare result is both the ballot and the store's
+            // exec mask (no lane-bit test of the ballot)
+            const bool ge = key >= lo, le = key <= hi;
+            const bool in = ge & le;
+            const uint64_t m = __builtin_amdgcn_ballot_w64(ge) & __builtin_amdgcn_ballot_w64(le);
             if (m) {
                 const uint32_t c = st.wcur[w];
-                if ((m >> lane_id()) & 1u) {
-                    const uint32_t pos = c + (uint32_t)lane_rank(m);
-                    if ((int64_t)pos < cx.cap) cx.seg[w][pos] = key;
-                }
+                const uint32_t pos = c + (uint32_t)lane_rank(m);
+                if (in && (int64_t)pos < cx.cap) cx.seg[w][pos] = key;
                 st.wcur[w] = c + (uint32_t)__popcll(m);
             }
         }
@@ -393,14 +395,13 @@ __device__ __forceinline__ void p1_elem(P1Thread &st, const P1Ctx &cx, T x, bool
         st.gt[w] += (uint32_t)(key > hi);
         st.eqlo[w] += (uint32_t)(key == lo);
         st.eqhi[w] += (uint32_t)(key == hi);
-        // lane masks straight from the compares (no bool round trip through a VGPR)
-        const uint64_t m = __builtin_amdgcn_uicmpl(key, lo, 34 /*UGT*/) & __builtin_amdgcn_uicmpl(key, hi, 36 /*ULT*/);
+        const bool gt = key > lo, lt = key < hi;
+        const bool in = gt & lt;
+        const uint64_t m = __builtin_amdgcn_ballot_w64(gt) & __builtin_amdgcn_ballot_w64(lt);
         if (m) {   // wave-uniform; no atomics: this wave owns its slot range
             const uint32_t c = st.wcur[w];
-            if ((m >> lane_id()) & 1u) {
-                const uint32_t pos = c + (uint32_t)lane_rank(m);
-                if ((int64_t)pos < cx.cap) cx.seg[w][pos] = key;
-            }
+            const uint32_t pos = c + (uint32_t)lane_rank(m);
+            if (in && (int64_t)pos < cx.cap) cx.seg[w][pos] = key;
             st.wcur[w] = c + (uint32_t)__popcll(m);
         }
     }
