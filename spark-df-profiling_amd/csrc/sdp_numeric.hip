@@ -173,17 +173,19 @@ __global__ void __launch_bounds__(1024) quantile_plan_kernel(uint64_t *sample, i
 }
 
 // Window refinement from a second, larger sample S2 (one workgroup per column).
-// The S1 windows are +-(4 sigma + 2) sample ranks of a 16 K sample; S2's keys
-// that fall inside those windows (~11 % of S2) are sorted in LDS, and around
-// each probability a window of +-(4 sigma2 + 2) S2 ranks is taken inside its S1
-// window, so windows shrink by sqrt(n2 / n1) at the same miss probability.
-// S2 keys below each window are counted to place the ranks.  If the in-window
-// keys exceed the LDS sort, or a rank lands outside every S1 window, the S1
-// plan stands (windows are a performance device: a miss falls back exactly).
+// The S1 windows are +-(4 sigma + 2) sample ranks of the previous sample; S2's
+// keys are counted per window, the windows whose S2 keys fit the LDS sort
+// together (in window order) are chosen, their keys sorted, and around each
+// probability in a chosen window a window of +-(4 sigma2 + 2) S2 ranks is taken
+// inside it, so windows shrink by sqrt(n2 / n1) at the same miss probability.
+// A probability in an unchosen window (a heavy value's window holding a large
+// share of S2) keeps that S1 window.  S2 keys below each window place the
+// ranks.  If a rank lands outside every S1 window the S1 plan stands (windows
+// are a performance device: a miss falls back exactly).
 __global__ void __launch_bounds__(1024) quantile_refine_kernel(const uint64_t *samples2, int32_t ns2,
                                                                const double *probs, int32_t np, sdp_qplan *plans) {
     __shared__ uint64_t s[SORT_MAX];
-    __shared__ uint32_t s_cnt, s_valid;
+    __shared__ uint32_t s_cnt, s_valid, s_chosen;
     __shared__ uint32_t s_below[SDP_MAX_WINDOWS], s_in[SDP_MAX_WINDOWS];
     const uint64_t *sample2 = samples2 + (int64_t)blockIdx.x * ns2;
     sdp_qplan *plan = plans + blockIdx.x;
@@ -201,22 +203,15 @@ __global__ void __launch_bounds__(1024) quantile_refine_kernel(const uint64_t *s
     uint32_t valid = 0, below[SDP_MAX_WINDOWS], inw[SDP_MAX_WINDOWS];
 #pragma unroll
     for (int w = 0; w < SDP_MAX_WINDOWS; ++w) below[w] = inw[w] = 0;
-    for (int i = threadIdx.x; i < ns2; i += blockDim.x) {
+    for (int i = threadIdx.x; i < ns2; i += blockDim.x) {        // pass 1: counts
         const uint64_t k = sample2[i];
         if (k == EMPTY64) continue;                  // null / NaN rows of the sample
         ++valid;
-        bool in = false;
 #pragma unroll
         for (int w = 0; w < SDP_MAX_WINDOWS; ++w) {
             if (w >= nw) break;
             below[w] += k < lo[w];
-            const bool iw = k >= lo[w] && k <= hi[w];
-            inw[w] += iw;
-            in = in || iw;
-        }
-        if (in) {
-            const uint32_t pos = atomicAdd(&s_cnt, 1u);
-            if (pos < SORT_MAX) s[pos] = k;
+            inw[w] += k >= lo[w] && k <= hi[w];
         }
     }
     // block sums of the per-thread counters (fixed-order wave sums, then LDS atomics of 16 partials)
@@ -228,6 +223,30 @@ __global__ void __launch_bounds__(1024) quantile_refine_kernel(const uint64_t *s
         if (lane_id() == 0 && w < nw) { atomicAdd(&s_below[w], b); atomicAdd(&s_in[w], c); }
     }
     __syncthreads();
+    if (threadIdx.x == 0) {                          // windows whose keys fit the sort, in order
+        uint32_t acc = 0, ch = 0;
+        for (int w = 0; w < nw; ++w)
+            if (acc + s_in[w] <= (uint32_t)SORT_MAX) { acc += s_in[w]; ch |= 1u << w; }
+        s_chosen = ch;
+    }
+    __syncthreads();
+    const uint32_t chosen = s_chosen;
+    if (chosen == 0) return;                         // the S1 plan stands
+    for (int i = threadIdx.x; i < ns2; i += blockDim.x) {        // pass 2: keys of the chosen windows
+        const uint64_t k = sample2[i];
+        if (k == EMPTY64) continue;
+        bool in = false;
+#pragma unroll
+        for (int w = 0; w < SDP_MAX_WINDOWS; ++w) {
+            if (w >= nw) break;
+            in = in || (((chosen >> w) & 1u) && k >= lo[w] && k <= hi[w]);
+        }
+        if (in) {
+            const uint32_t pos = atomicAdd(&s_cnt, 1u);
+            if (pos < SORT_MAX) s[pos] = k;
+        }
+    }
+    __syncthreads();
     const uint32_t cnt = s_cnt;
     if (cnt > SORT_MAX || cnt == 0) return;        // the S1 plan stands
     block_sort_keys(s, (int)cnt);                  // windows are disjoint: window w's keys form one run
@@ -236,7 +255,7 @@ __global__ void __launch_bounds__(1024) quantile_refine_kernel(const uint64_t *s
     sdp_qplan p = *plan;
     uint32_t seg0[SDP_MAX_WINDOWS];
     uint32_t acc = 0;
-    for (int w = 0; w < nw; ++w) { seg0[w] = acc; acc += s_in[w]; }
+    for (int w = 0; w < nw; ++w) { seg0[w] = acc; if ((chosen >> w) & 1u) acc += s_in[w]; }
     uint64_t nlo[SDP_MAX_WINDOWS], nhi[SDP_MAX_WINDOWS];
     int nn = 0, nex = 0;
     for (int t = 0; t < np && t < SDP_MAX_WINDOWS; ++t) {
@@ -246,17 +265,25 @@ __global__ void __launch_bounds__(1024) quantile_refine_kernel(const uint64_t *s
         for (int v = 0; v < nw; ++v)
             if ((double)s_below[v] <= floor(r) && ceil(r) < (double)(s_below[v] + s_in[v])) { w = v; break; }
         if (w < 0) return;                         // a rank outside the S1 windows: keep the S1 plan
-        const int d = (int)ceil(4.0 * sqrt((double)m2 * q * (1.0 - q))) + 2;
-        const int cw = (int)s_in[w];
-        int il = (int)floor(r) - d - (int)s_below[w], ih = (int)ceil(r) + d - (int)s_below[w];
-        const uint64_t l = il <= 0 ? p.lo[w] : s[seg0[w] + il];
-        const uint64_t h = ih >= cw - 1 ? p.hi[w] : s[seg0[w] + ih];
-        // exclusive bounds: an S1 bound kept from an exclusive S1 window, lo == 0,
-        // or a bound key repeated among the S2 keys of its window
-        const int a0 = (int)seg0[w], a1 = a0 + cw;
-        auto dup2 = [&](int i) { return (i > a0 && s[i - 1] == s[i]) || (i + 1 < a1 && s[i + 1] == s[i]); };
         const bool s1ex = ((p.excl_mask >> w) & 1) != 0;
-        const bool ex = l == 0ull || (il <= 0 ? s1ex : dup2(a0 + il)) || (ih >= cw - 1 ? s1ex : dup2(a0 + ih));
+        uint64_t l, h;
+        bool ex;
+        if ((chosen >> w) & 1u) {
+            const int d = (int)ceil(4.0 * sqrt((double)m2 * q * (1.0 - q))) + 2;
+            const int cw = (int)s_in[w];
+            const int il = (int)floor(r) - d - (int)s_below[w], ih = (int)ceil(r) + d - (int)s_below[w];
+            l = il <= 0 ? p.lo[w] : s[seg0[w] + il];
+            h = ih >= cw - 1 ? p.hi[w] : s[seg0[w] + ih];
+            // exclusive bounds: an S1 bound kept from an exclusive S1 window, lo == 0,
+            // or a bound key repeated among the S2 keys of its window
+            const int a0 = (int)seg0[w], a1 = a0 + cw;
+            auto dup2 = [&](int i) { return (i > a0 && s[i - 1] == s[i]) || (i + 1 < a1 && s[i + 1] == s[i]); };
+            ex = l == 0ull || (il <= 0 ? s1ex : dup2(a0 + il)) || (ih >= cw - 1 ? s1ex : dup2(a0 + ih));
+        } else {                                   // kept as it was
+            l = p.lo[w];
+            h = p.hi[w];
+            ex = s1ex;
+        }
         if (nn > 0 && l <= nhi[nn - 1]) {
             if (h > nhi[nn - 1]) nhi[nn - 1] = h;
             if (ex) nex |= 1 << (nn - 1);
@@ -273,13 +300,18 @@ __global__ void __launch_bounds__(1024) quantile_refine_kernel(const uint64_t *s
         p.in_sample[w] = 0;
     }
     for (int w = 0; w < nn; ++w) {
-        // S2 keys strictly inside (lo, hi) by binary search on the sorted in-window keys
+        // S2 keys strictly inside (lo, hi): binary search on the sorted keys of
+        // the chosen windows, plus the (inclusive, so over-) counts of the
+        // unchosen S1 windows it overlaps -- the slot sizing reads this
         int a = 0, b = (int)cnt;
         while (a < b) { int mid = (a + b) >> 1; if (s[mid] < p.hi[w]) a = mid + 1; else b = mid; }
         const int below_hi = a;
         a = 0; b = (int)cnt;
         while (a < b) { int mid = (a + b) >> 1; if (s[mid] <= p.lo[w]) a = mid + 1; else b = mid; }
-        p.in_sample[w] = below_hi > a ? below_hi - a : 0;
+        uint32_t in_s = below_hi > a ? (uint32_t)(below_hi - a) : 0u;
+        for (int v = 0; v < nw; ++v)
+            if (!((chosen >> v) & 1u) && lo[v] <= p.hi[w] && hi[v] >= p.lo[w]) in_s += s_in[v];
+        p.in_sample[w] = (int32_t)in_s;
     }
     p.n_windows = nn;
     p.n_sample = (int32_t)m2;
