@@ -169,6 +169,69 @@ def make_c3_shard(rows_total, rank, world, device):
     return DeviceTable(cols, n)
 
 
+C4_LABELS = 5 * 10 ** 8
+_U64 = (1 << 64) - 1
+
+
+def _s64(c):
+    """A u64 constant as the int64 with the same bits."""
+    return c - (1 << 64) if c >= (1 << 63) else c
+
+
+def _srl(x, s):
+    """Logical right shift of int64 tensors holding u64 bits."""
+    return (x >> s) & ((1 << (64 - s)) - 1)
+
+
+def mix64_t(x):
+    """splitmix64's finalizer on int64 tensors with u64 semantics (wrapping
+    multiplies, logical shifts) -- the same map as tests/datagen.mix64_np."""
+    x = x ^ _srl(x, 30)
+    x = x * _s64(0xBF58476D1CE4E5B9)
+    x = x ^ _srl(x, 27)
+    x = x * _s64(0x94D049BB133111EB)
+    return x ^ _srl(x, 31)
+
+
+def _hex16_column(keys, device, chunk=1 << 26):
+    """utf8 (int64 offsets): each u64 key (int64 bits) -> its 16 lower-case hex digits."""
+    n = keys.numel()
+    offsets = torch.arange(n + 1, dtype=torch.int64, device=device) * 16
+    data = torch.zeros(16 * n + 16, dtype=torch.uint8, device=device)
+    hexd = _HEX.to(device)
+    shifts = torch.arange(60, -4, -4, dtype=torch.int64, device=device)
+    for s in range(0, n, chunk):
+        e = min(n, s + chunk)
+        nib = (keys[s:e, None] >> shifts[None, :]) & 15     # (sign-extending shift: the mask keeps the nibble)
+        data[16 * s:16 * e] = hexd[nib].reshape(-1)
+    return offsets, data
+
+
+def make_c4_shard(rows_total, rank, world, device, labels=C4_LABELS):
+    """`rows_total` rows, no nulls --
+      u32_range_i64  int64 U[0, 2^32)  (near-unique: D ~ 0.9e9 at 1e9 rows; NUM)
+      hex_id         utf8, the 16 hex digits of mix64(label), label ~ zipf(1.05)
+                     over `labels` labels (exact distinct + top-50; CAT)
+    generated in HBM from fixed seeds (the law of tests/datagen.c4_table)."""
+    from spark_df_profiling.columns import DeviceColumn, DeviceTable
+    from spark_df_profiling import _native as nat
+    per = rows_total // world
+    start = rank * per
+    n = per if rank < world - 1 else rows_total - start
+    g = _gen(SEED + 4001 * 1000 + rank, device)
+    c = DeviceColumn('u32_range_i64', 'bigint', n, 'fixed', nat.I64)
+    c.values = torch.randint(0, 2 ** 32, (n,), generator=g, device=device, dtype=torch.int64)
+    lab = _bounded_zipf(n, 1.05, labels, _gen(SEED + 4002 * 1000 + rank, device), device)
+    keys = mix64_t(lab)
+    del lab
+    h = DeviceColumn('hex_id', 'string', n, 'bytes')
+    h.offsets, h.data = _hex16_column(keys, device)
+    h.offset_width = 8
+    del keys
+    torch.cuda.synchronize()
+    return DeviceTable([c, h], n)
+
+
 C5_COLS = 512
 C5_FACTORS = 4
 
@@ -398,8 +461,9 @@ def main():
     ap.add_argument('--gpus', type=int, default=1)
     ap.add_argument('--steps', type=int, default=3)
     ap.add_argument('--warmup', type=int, default=1)
-    ap.add_argument('--workload', choices=('c3', 'c5'), default='c3',
-                    help='c3: 1e9 x 16 mixed (the metric); c5: 1e7 x 512 fp32 (Pearson on MFMA)')
+    ap.add_argument('--workload', choices=('c3', 'c4', 'c5'), default='c3',
+                    help='c3: 1e9 x 16 mixed (the metric); c4: 1e9-row high-cardinality int64 + hex ids '
+                         '(exact distinct + top-50); c5: 1e7 x 512 fp32 (Pearson on MFMA)')
     ap.add_argument('--rows', type=int, default=None)
     ap.add_argument('--cpu-sample-rows', type=int, default=1 << 24)
     ap.add_argument('--no-cpu-baseline', action='store_true')
@@ -409,7 +473,7 @@ def main():
                     help='columns profiled concurrently per GPU (default: SDP_COLUMN_WORKERS or 1)')
     args = ap.parse_args()
     if args.rows is None:
-        args.rows = 10 ** 9 if args.workload == 'c3' else 10 ** 7
+        args.rows = 10 ** 7 if args.workload == 'c5' else 10 ** 9
     traffic_path = args.traffic if args.traffic is not None else TRAFFIC_SUMMARY.get(args.workload)
 
     world = int(os.environ.get('WORLD_SIZE', '1'))
@@ -449,6 +513,8 @@ def main():
     t_gen = time.perf_counter()
     if args.workload == 'c3':
         table = make_c3_shard(args.rows, rank, world, device)
+    elif args.workload == 'c4':
+        table = make_c4_shard(args.rows, rank, world, device)
     else:
         table = make_c5_shard(args.rows, rank, world, device)
     t_gen = time.perf_counter() - t_gen
@@ -506,6 +572,9 @@ def main():
     if args.workload == 'c3':
         workload = ('C3: %d rows x 16 mixed columns (6 f64, 4 i64, 2 f32, 3 utf8, 1 date32), 5%% nulls, '
                     'row-sharded' % args.rows)
+    elif args.workload == 'c4':
+        workload = ('C4: %d rows: int64 U[0,2^32) + utf8 16-byte hex ids zipf(1.05) over 5e8 labels, '
+                    'exact distinct + top-50, row-sharded' % args.rows)
     else:
         workload = ('C5: %d rows x %d fp32 columns (low-rank factor + noise, no nulls), full describe() '
                     'with the Pearson matrix on fp64 MFMA' % (args.rows, ncols))

@@ -282,6 +282,13 @@ int sdp_compact_batch(const sdp_compact_task *d_tasks, int32_t q, int64_t max_ns
 int sdp_column_keys(const sdp_column *col, uint64_t *d_out, uint64_t *d_out_n,
                     void *stream);
 
+/* The same for the keys lo_key <= key <= hi_key only: the quantile fallback
+ * re-collects just the key range a missed rank lies in (between two pass-1
+ * windows, or one overflowed window), sized by pass 1's exact counts
+ * (replaces the whole-column copy for describe.py:203-208's order statistics). */
+int sdp_column_keys_range(const sdp_column *col, uint64_t lo_key, uint64_t hi_key,
+                          uint64_t *d_out, uint64_t *d_out_n, void *stream);
+
 /* Fused pass 2: mad, histogram over host-built CASE edges, outlier counts. */
 int sdp_pass2(const sdp_column *col, double mean, const double *d_edges,
               int32_t bins, int32_t edges_monotone, double hi_t, double lo_t,

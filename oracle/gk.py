@@ -36,6 +36,7 @@ import math
 import struct
 
 HEAD_SIZE = 50000
+INT_MAX = 2 ** 31 - 1
 COMPRESS_THRESHOLD = 10000
 
 
@@ -124,7 +125,7 @@ class Summary:
             return s[0][0]
         if q >= 1 - self.eps:
             return s[-1][0]
-        rank = int(math.ceil(q * self.count))
+        rank = min(int(math.ceil(q * self.count)), INT_MAX)     # Scala .toInt saturates
         target = math.ceil(self.eps * self.count)
         min_rank = 0
         for i in range(1, len(s) - 1):

@@ -992,8 +992,9 @@ __global__ void __launch_bounds__(1024) sort_small_batch_kernel(uint64_t *keys, 
     for (int i = threadIdx.x; i < n_each; i += blockDim.x) keys[i] = s[i];
 }
 
+// keys of the na.drop rows with lo <= key <= hi (the whole column: 0, UINT64_MAX)
 template <typename T>
-__global__ void column_keys_kernel(sdp_column col, uint64_t *out, uint64_t *out_n) {
+__global__ void column_keys_kernel(sdp_column col, uint64_t lo, uint64_t hi, uint64_t *out, uint64_t *out_n) {
     __shared__ uint64_t s_buf[STAGE];
     __shared__ uint32_t s_cnt;
     __shared__ uint64_t s_gbase;
@@ -1010,8 +1011,8 @@ __global__ void column_keys_kernel(sdp_column col, uint64_t *out, uint64_t *out_
         if (i < n && valid_bit(col.d_validity, col.validity_bit_offset, i)) {
             const T x = ((const T *)col.d_values)[i];
             const double xd = Elem<T>::d(x);
-            keep = xd == xd;
             k = Elem<T>::key(x);
+            keep = xd == xd && k >= lo && k <= hi;
         }
         stage_push(sg, keep, k, out, (unsigned long long *)out_n, it + 1 == iters);
     }
@@ -1886,13 +1887,19 @@ extern "C" int sdp_sort_small_batch(uint64_t *d_keys, int32_t n_each, int32_t n_
     return check_launch("sort_small_batch_kernel");
 }
 
-extern "C" int sdp_column_keys(const sdp_column *col, uint64_t *d_out, uint64_t *d_out_n, void *stream) {
-    int rc = check_col(col, "sdp_column_keys");
+extern "C" int sdp_column_keys_range(const sdp_column *col, uint64_t lo_key, uint64_t hi_key, uint64_t *d_out,
+                                     uint64_t *d_out_n, void *stream) {
+    int rc = check_col(col, "sdp_column_keys_range");
     if (rc) return rc;
+    if (d_out == nullptr || d_out_n == nullptr) return set_error(SDP_EINVAL, "sdp_column_keys_range: outputs");
     hipStream_t s = (hipStream_t)stream;
     SDP_DISPATCH_NUMERIC(col->dtype,
-        hipLaunchKernelGGL(column_keys_kernel<T>, dim3(1024), dim3(256), 0, s, *col, d_out, d_out_n));
+        hipLaunchKernelGGL(column_keys_kernel<T>, dim3(1024), dim3(256), 0, s, *col, lo_key, hi_key, d_out, d_out_n));
     return check_launch("column_keys_kernel");
+}
+
+extern "C" int sdp_column_keys(const sdp_column *col, uint64_t *d_out, uint64_t *d_out_n, void *stream) {
+    return sdp_column_keys_range(col, 0ull, ~0ull, d_out, d_out_n, stream);
 }
 
 extern "C" int64_t sdp_pass2_count_workspace_bytes(int64_t length, int32_t bins) {
@@ -2305,7 +2312,10 @@ __global__ void __launch_bounds__(GK_T) gk_merge_query_kernel(int32_t P, double 
             } else if (q >= 1 - eps) {
                 r = M.v[m - 1];
             } else {
-                const int64_t rank = (int64_t)(int32_t)ceil(q * (double)cm);
+                // Scala's Double.toInt saturates at Int.MaxValue (reachable once
+                // q * count >= 2^31; an out-of-range C++ cast would be undefined)
+                const double rr = ceil(q * (double)cm);
+                const int64_t rank = rr >= 2147483647.0 ? (int64_t)2147483647 : (int64_t)(int32_t)rr;
                 const double target = ceil(eps * (double)cm);
                 int64_t min_rank = 0;
                 r = M.v[m - 1];

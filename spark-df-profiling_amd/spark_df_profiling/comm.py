@@ -13,8 +13,9 @@ Every statistic resolves through one of three collectives:
 torch.distributed: backend 'nccl' is RCCL over xGMI on ROCm; 'gloo' is used by
 the CPU tests (tensors are moved to the host for the collective); it runs the
 same all_to_all_single calls as RCCL, on host copies.  RCCL itself refuses two
-ranks on one GPU ("Duplicate GPU detected", tools/rccl_probe.py), so the nccl
-branches run for the first time on a multi-GPU node.
+ranks on one GPU ("Duplicate GPU detected", tools/rccl_probe.py); a one-rank
+nccl group with force_sharded=True runs the same branches on one GPU
+(conftest.py starts tests/multirank_worker.py that way).
 """
 
 from __future__ import annotations
@@ -27,6 +28,7 @@ import torch
 class LocalComm:
     rank = 0
     world = 1
+    sharded = False
 
     def allgather(self, t: torch.Tensor) -> List[torch.Tensor]:
         return [t]
@@ -56,7 +58,15 @@ class LocalComm:
 
 
 class TorchComm:
-    def __init__(self, group=None):
+    """`sharded` selects the row-sharded code paths (per-round collectives,
+    owner exchanges).  It is on whenever world > 1; force_sharded=True (or
+    SDP_FORCE_SHARDED=1) turns it on for a one-rank group too, so the RCCL
+    branches -- stream-ordered in-place all-reduces, all_to_all_single on
+    device tensors, the owner exchanges -- run on a single GPU (RCCL refuses
+    two ranks on one device, tools/rccl_probe.py)."""
+
+    def __init__(self, group=None, force_sharded=None):
+        import os
         import torch.distributed as dist
         self.dist = dist
         self.group = group
@@ -64,11 +74,17 @@ class TorchComm:
         self.world = dist.get_world_size(group)
         self.backend = dist.get_backend(group)
         self.cpu = self.backend == 'gloo'
+        if force_sharded is None:
+            force_sharded = os.environ.get('SDP_FORCE_SHARDED', '0') == '1'
+        self.sharded = self.world > 1 or bool(force_sharded)
+        from collections import Counter
+        self.calls = Counter()          # collective -> times issued (tests check the branches ran)
 
     def _io(self, t):
         return t.cpu() if self.cpu else t
 
     def allgather(self, t):
+        self.calls['allgather'] += 1
         x = self._io(t.contiguous())
         outs = [torch.empty_like(x) for _ in range(self.world)]
         self.dist.all_gather(outs, x, group=self.group)
@@ -76,6 +92,7 @@ class TorchComm:
 
     def allgatherv(self, t):
         """all_gather of 1-D tensors whose lengths differ per rank."""
+        self.calls['allgatherv'] += 1
         n = torch.tensor([t.numel()], dtype=torch.int64, device=t.device)
         sizes = [int(s.item()) for s in self.allgather(n)]
         m = max(sizes) if sizes else 0
@@ -86,6 +103,7 @@ class TorchComm:
         return [o[:s] for o, s in zip(outs, sizes)]
 
     def allreduce_sum(self, t):
+        self.calls['allreduce_sum'] += 1
         x = self._io(t.contiguous()).clone()
         self.dist.all_reduce(x, op=self.dist.ReduceOp.SUM, group=self.group)
         return x.to(t.device)
@@ -93,6 +111,7 @@ class TorchComm:
     def allreduce_sum_(self, t):
         """In-place sum.  With RCCL the collective is ordered on the current
         stream and the host does not wait (device-driven radix rounds)."""
+        self.calls['allreduce_sum_'] += 1
         if self.cpu:
             x = t.cpu()
             self.dist.all_reduce(x, op=self.dist.ReduceOp.SUM, group=self.group)
@@ -103,6 +122,7 @@ class TorchComm:
 
     def alltoallv(self, send, send_counts):
         """send is laid out rank-major (send_counts[r] elements for rank r)."""
+        self.calls['alltoallv'] += 1
         # gloo runs the same all_to_all_single calls on host copies, so the
         # CPU tests exercise exactly the split logic RCCL sees
         dev = send.device
@@ -113,6 +133,7 @@ class TorchComm:
 
     def alltoallv_known(self, send, send_counts, recv_counts):
         """alltoallv when every rank already knows its receive counts."""
+        self.calls['alltoallv_known'] += 1
         dev = send.device
         x = self._io(send.contiguous())
         out = torch.empty(sum(recv_counts), dtype=send.dtype, device=x.device)
@@ -121,9 +142,11 @@ class TorchComm:
         return out.to(dev)
 
     def allgather_object(self, obj):
+        self.calls['allgather_object'] += 1
         out = [None] * self.world
         self.dist.all_gather_object(out, obj, group=self.group)
         return out
 
     def barrier(self):
+        self.calls['barrier'] += 1
         self.dist.barrier(group=self.group)

@@ -282,9 +282,9 @@ def describe(df, bins=10, corr_reject=0.9, **kwargs):
     receives the per-column engine outputs, e.g. exact histogram counts),
     ``quantile_mode`` ('exact', the default: float quantiles are the element at
     rank ceil(pN), inside percentile_approx's rank window; 'gk': Spark 2.x's
-    percentile_approx element for ``spark_partitions`` contiguous partitions,
-    restated from QuantileSummaries; on a sharded table each rank's rows form
-    spark_partitions / world of them)."""
+    percentile_approx element for ``spark_partitions`` contiguous partitions
+    (default: one per rank), restated from QuantileSummaries; on a sharded
+    table each rank's rows form spark_partitions / world of them)."""
     comm = kwargs.pop('comm', None)
     device = kwargs.pop('device', None)
     plots = kwargs.pop('plots', True)
@@ -292,10 +292,20 @@ def describe(df, bins=10, corr_reject=0.9, **kwargs):
     quantile_mode = kwargs.pop('quantile_mode', 'exact')
     if quantile_mode not in ('exact', 'gk'):
         raise ValueError("quantile_mode must be 'exact' or 'gk'")
-    gk = {'partitions': int(kwargs.pop('spark_partitions', 1)),
-          'accuracy': int(kwargs.pop('accuracy', 10000))} if quantile_mode == 'gk' else None
+    partitions = kwargs.pop('spark_partitions', None)
+    accuracy = int(kwargs.pop('accuracy', 10000))
     table = as_device_table(df, device)
     engine = Engine(device=device, comm=comm)
+    gk = None
+    if quantile_mode == 'gk':
+        # default: one Spark partition per rank; a sharded table's partitions
+        # are split evenly over the ranks (rank r holds k consecutive ones)
+        w = engine.comm.world
+        partitions = int(partitions) if partitions is not None else w
+        if partitions < 1 or partitions % w:
+            raise ValueError('spark_partitions (%d) must be a positive multiple of the number of ranks (%d)'
+                             % (partitions, w))
+        gk = {'partitions': partitions, 'accuracy': accuracy}
     import torch
     n_local = table.num_rows
     n = int(engine.comm.allreduce_sum(torch.tensor([n_local], dtype=torch.int64, device=engine.device)).item())
@@ -308,7 +318,7 @@ def describe(df, bins=10, corr_reject=0.9, **kwargs):
     ldesc = OrderedDict((col.name, None) for col in table.columns)
     pending = OrderedDict()
 
-    world, rank = engine.comm.world, engine.comm.rank
+    world, rank, sharded = engine.comm.world, engine.comm.rank, engine.comm.sharded
     owner = {col.name: i % world for i, col in enumerate(table.columns)}
 
     early_plots = {}
@@ -337,9 +347,11 @@ def describe(df, bins=10, corr_reject=0.9, **kwargs):
         p1s = [pk[0] for pk in packs]
         hints = [_distinct_hint(p1, c.spark_type) for c, p1 in zip(num_cols, p1s)]
         bounds = [(p1['imin'], p1['imax']) if p1['count'] else None for p1 in p1s]
-        group_cols = set()
-        if world == 1:
-            group_cols = {i for i, pth in enumerate(engine.distinct_paths(num_cols, hints, bounds)) if pth == 'group'}
+        # columns whose countDistinct partitions by hash: pass 2 also counts
+        # their level-1 buckets (one column read fewer)
+        paths = engine.distinct_paths_sharded(num_cols, hints, bounds, n) if sharded else \
+            engine.distinct_paths(num_cols, hints, bounds)
+        group_cols = {i for i, pth in enumerate(paths) if pth == 'group'}
         stats = engine.numeric_stats_batch(num_cols, packs, bins, [k_vals.get(c.name, 2) for c in num_cols],
                                            group_cols=group_cols, gk=gk)
         for col, pack, st in zip(num_cols, packs, stats):
@@ -352,15 +364,15 @@ def describe(df, bins=10, corr_reject=0.9, **kwargs):
                     early_plots[col.name] = _submit_plot(st)
         # every NUM column's countDistinct with shared readbacks (and, sharded,
         # shared collectives)
-        dist = engine.distinct_batch(num_cols, hints, bounds) if world == 1 else \
+        dist = engine.distinct_batch(num_cols, hints, bounds) if not sharded else \
             engine.distinct_batch_sharded(num_cols, hints, bounds)
         for col, d in zip(num_cols, dist):
             bundles[col.name]['distinct_pre'] = d
-        if world == 1:
-            # every string/binary/decimal column's value counts with shared readbacks
-            byte_cols = [c for c in table.columns if _is_byte_keyed(c)]
-            for col, tab in zip(byte_cols, engine.value_counts_bytes_batch(byte_cols)):
-                bundles[col.name]['tab_pre'] = tab
+        # every string/binary/decimal column's value counts with shared
+        # readbacks (sharded: then each column's owner exchange, in column order)
+        byte_cols = [c for c in table.columns if _is_byte_keyed(c)]
+        for col, tab in zip(byte_cols, engine.value_counts_bytes_batch(byte_cols)):
+            bundles[col.name]['tab_pre'] = tab
     if workers > 1:
         done = _describe_concurrent(engine, table.columns, one, workers)
     else:
@@ -371,7 +383,7 @@ def describe(df, bins=10, corr_reject=0.9, **kwargs):
             pending[name] = fut
 
     images = {name: (fut.result() if hasattr(fut, 'result') else fut) for name, fut in pending.items()}
-    if plots and world > 1:
+    if plots and sharded:
         # one exchange of the rendered strings (~2 x 20 KB per NUM column)
         for part in engine.comm.allgather_object(images):
             images.update(part)
@@ -403,7 +415,7 @@ def column_workers(engine, requested=None):
     its collectives in the same order."""
     import os
     w = requested if requested is not None else int(os.environ.get('SDP_COLUMN_WORKERS', '1'))
-    if engine.comm.world > 1 or engine.device.type != 'cuda':
+    if engine.comm.sharded or engine.device.type != 'cuda':
         return 1
     return max(1, int(w))
 

@@ -136,7 +136,7 @@ def exchange_bytes_groups(engine, tab):
 
 def merge_topk(comm, pairs, k):
     """Global top-k from every rank's local top-k list of (value, count)."""
-    if comm.world == 1:
+    if not comm.sharded:
         return pairs[:k]
     allp = comm.allgather_object(pairs)
     merged = [p for part in allp for p in part]
@@ -155,7 +155,7 @@ def _sortable(v):
 
 
 def merge_first_rows(comm, values, k):
-    if comm.world == 1:
+    if not comm.sharded:
         return values[:k]
     allv = comm.allgather_object(values)
     out = []

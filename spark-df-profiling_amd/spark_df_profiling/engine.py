@@ -182,11 +182,11 @@ class Engine:
         self.device = torch.device(device or 'cuda')
         self.comm = comm or LocalComm()
         self.stream = stream
+        self._heavy_pre = None          # id(col) -> heavy keys sampled with pass 1
+        self._near_unique = set()       # id(col) of columns >= 90 % distinct in that sample
+        self._counted = {}              # id(col) -> group context whose level-1 count pass 2 did
 
     # -- small helpers ----------------------------------------------------------
-    _heavy_pre = None
-    _near_unique = frozenset()
-    _counted = {}            # id(col) -> group context whose level-1 count pass 2 did
 
     def _s(self):
         return nat.stream_handle(self.stream)
@@ -298,7 +298,7 @@ class Engine:
 
     def merge_pass1(self, local: nat.SdpPass1Result):
         """All-gather the per-rank pass-1 states and merge them in rank order."""
-        if self.comm.world == 1:
+        if not self.comm.sharded:
             return merge_pass1_results([local])
         raw = torch.frombuffer(bytearray(bytes(local)), dtype=torch.uint8).to(self.device)
         parts = [nat.SdpPass1Result.from_buffer_copy(p.cpu().numpy().tobytes()) for p in self.comm.allgather(raw)]
@@ -350,133 +350,34 @@ class Engine:
 
     def resolve_quantiles(self, col, p1: dict, plan, cand_info, probs=PROBS):
         """Order statistics for each requested probability (describe.py:203-208)."""
-        return self._quantiles_finish(self._quantiles_launch(col, p1, plan, cand_info, probs))
+        return self.quantiles_batch([(col, p1, plan, cand_info)], probs)[0]
 
-    def _quantiles_launch(self, col, p1: dict, plan, cand_info, probs=PROBS):
+    @staticmethod
+    def _rank_key_range(r, p1, plan):
+        """The key range [a, b] (inclusive) and rank span [base, base + cnt) of
+        the na.drop keys that rank r (0-based) falls among when no window
+        resolves it: the gap between two pass-1 windows (or before the first /
+        after the last), or an overflowed window itself.  Exact from pass 1's
+        merged counts, identical on every rank."""
         n = p1['count']
-        is_int = not col.is_float
-        nw = plan.n_windows
-        needed = {}
-        for p in probs:
-            if is_int:
-                pos = (n - 1) * p
-                needed[p] = (pos, math.floor(pos), math.ceil(pos))
-            else:
-                needed[p] = (None, spark_percentile_approx_rank(n, p) - 1, None)
-        ranks = sorted({r for v in needed.values() for r in (v[1], v[2]) if r is not None})
-        dense = {}
-        values = {}
-        fallback = None
-        queued = []              # single rank: (rank, arr, arr_n, n_cap, k, lo, hi), selected on the device
-        for r in ranks:
-            key = None
-            for w in range(nw):
-                size = p1['w_eq_lo'][w] + p1['w_in'][w] + p1['w_eq_hi'][w]
-                below = n - p1['w_gt'][w] - size
-                if below <= r < below + size:
-                    rr = r - below
-                    lo, hi = plan.lo[w], plan.hi[w]
-                    if rr < p1['w_eq_lo'][w]:
-                        key = lo
-                    elif rr < p1['w_eq_lo'][w] + p1['w_in'][w]:
-                        if (p1['w_overflow'] >> w) & 1:
-                            break
-                        if w not in dense:
-                            dense[w] = self._compact(cand_info, w)
-                        arr, arr_n = dense[w]
-                        queued.append((r, arr, arr_n, arr.numel(), rr - p1['w_eq_lo'][w], lo, hi))
-                        key = 'queued'
-                    else:
-                        key = hi
-                    break
-            if key is None:                                    # window missed: exact fallback
-                if fallback is None:
-                    fallback = self._all_keys(col)
-                arr, arr_n = fallback
-                queued.append((r, arr, arr_n, arr.numel(), r, 0, EMPTY64))
-                key = 'queued'
-            values[r] = key
-        res = None
-        if queued and self.comm.world > 1:
-            res = self._select_sharded(queued)
-        elif queued:
-            # every select of the column runs back to back on the stream; one readback
-            cap = max(q[3] for q in queued)
-            work = self._bytes(sdp.sdp_select_kth_workspace_bytes(cap))
-            res = self._u64(len(queued))
-            for i, (r, arr, arr_n, ncap, kk, lo, hi) in enumerate(queued):
-                sdp.sdp_select_kth(ptr(arr), ptr(arr_n), ncap, int(kk), _u(lo), _u(hi), ptr(work), work.numel(),
-                                   ptr(res[i:]), self._s())
-        # dense / fallback arrays stay referenced until the results are read
-        return {'queued': queued, 'res': res, 'values': values, 'needed': needed, 'is_int': is_int,
-                'probs': probs, 'fallback': fallback, 'dense': dense}
+        a, start = 0, 0
+        for w in range(plan.n_windows):
+            size = p1['w_eq_lo'][w] + p1['w_in'][w] + p1['w_eq_hi'][w]
+            below = n - p1['w_gt'][w] - size
+            if r < below:
+                return a, _u(plan.lo[w]) - 1, start, below - start
+            if r < below + size:
+                return _u(plan.lo[w]), _u(plan.hi[w]), below, size
+            a, start = _u(plan.hi[w]) + 1, below + size
+        return a, EMPTY64, start, n - start
 
-    def _quantiles_finish(self, st):
-        values, needed, is_int = st['values'], st['needed'], st['is_int']
-        if st['queued']:
-            keys = self._host_u64(st['res'])
-            for (r, *_), key in zip(st['queued'], keys):
-                values[r] = key
-        probs, fallback = st['probs'], st['fallback']
-        out = {}
-        for p in probs:
-            pos, lo_r, hi_r = needed[p]
-            if is_int:
-                lk, hk = key_to_int(values[lo_r]), key_to_int(values[hi_r])
-                if hi_r == lo_r or hk == lk:
-                    out[p] = float(lk)
-                else:       # Spark Percentile linear interpolation (A.4)
-                    out[p] = (hi_r - pos) * float(lk) + (pos - lo_r) * float(hk)
-            else:
-                out[p] = key_to_float(values[lo_r])
-        return out, fallback is not None
-
-    def _select_sharded(self, queued):
-        """All order statistics of a column of a row-sharded table at once,
-        device-driven (sdp_select_init/hist/step): per radix round every
-        select's local digit histogram lands in one [Q, 2048] buffer, ONE
-        all-reduce sums them on the stream, and each select's decide kernel
-        picks the global digit.  Ranks hold different candidates but the same
-        state, so they stay in lockstep with no host round trip until the
-        results are read once.  The Q selects run max(rounds) rounds; a select
-        that has finished ignores the extra rounds (its state is done)."""
-        q = len(queued)
-        hist = self._u64(q * 2048, zero=True)
-        res = self._u64(q)
-        works, rounds = [], []
-        s = self._s()
-        for i, (r, arr, arr_n, ncap, kk, lo, hi) in enumerate(queued):
-            wb = sdp.sdp_select_kth_workspace_bytes(ncap)
-            work = self._bytes(wb)
-            sdp.sdp_select_init(int(kk), _u(lo), _u(hi), ptr(work), wb, ncap, ptr(hist[i * 2048:]), s)
-            works.append((work, wb))
-            rounds.append(sdp.sdp_select_rounds(_u(lo), _u(hi)))
-        for i, (r, arr, arr_n, ncap, kk, lo, hi) in enumerate(queued):
-            sdp.sdp_select_hist(ptr(arr), ptr(arr_n), ncap, 0, ptr(works[i][0]), works[i][1],
-                                ptr(hist[i * 2048:]), s)
-        for rd in range(max(rounds)):
-            # (each step's filter leaves the next round's local histogram in hist)
-            self.comm.allreduce_sum_(hist)
-            for i, (r, arr, arr_n, ncap, kk, lo, hi) in enumerate(queued):
-                if rd < rounds[i]:
-                    sdp.sdp_select_step(ptr(arr), ptr(arr_n), ncap, rd, int(rd == rounds[i] - 1),
-                                        ptr(works[i][0]), works[i][1], ptr(hist[i * 2048:]), ptr(res[i:]), s)
-        return res
-
-    def _compact(self, cand_info, w):
-        nseg, cap = cand_info['nseg'], cand_info['cap']
-        out = self._u64(max(1, nseg * cap))     # sized by the slot capacity: no readback of the counts
-        out_n = self._u64(1, zero=True)
-        base = cand_info['cand'][w * nseg * cap:]
-        sdp.sdp_compact_candidates(ptr(base), ptr(cand_info['counts'][w * nseg:]), nseg, cap,
-                                   ptr(self._u64(nseg)), ptr(out), ptr(out_n), self._s())
-        return out, out_n
-
-    def _all_keys(self, col):
-        out = self._u64(max(col.length, 1))
+    def _range_keys(self, col, a, b, cap):
+        """The na.drop keys of `col` in [a, b] (at most `cap` of them locally)."""
+        out = self._u64(max(int(cap), 1))
         out_n = self._u64(1, zero=True)
         cs = col.sdp()
-        sdp.sdp_column_keys(ctypes.byref(cs), ptr(out), ptr(out_n), self._s())
+        nat.annotate(_label(col, 'range_keys'), col_read_bytes(col))
+        sdp.sdp_column_keys_range(ctypes.byref(cs), _u(a), _u(b), ptr(out), ptr(out_n), self._s())
         return out, out_n
 
     def pass2(self, col, mean, edges, hi_t, lo_t):
@@ -492,7 +393,7 @@ class Engine:
         nat.annotate(_label(col), col_read_bytes(col))
         sdp.sdp_pass2(ctypes.byref(cs), float(mean), ptr(e), bins, int(mono), float(hi_t), float(lo_t), ptr(work),
                       work.numel(), ptr(res), ptr(hist), self._s())
-        if self.comm.world == 1:         # result struct and bins in one readback
+        if not self.comm.sharded:        # result struct and bins in one readback
             sz = ctypes.sizeof(nat.SdpPass2Result)
             raw = torch.cat([res[:sz], hist.view(torch.uint8)]).cpu().numpy()
             r = nat.SdpPass2Result.from_buffer_copy(raw[:sz].tobytes())
@@ -538,12 +439,13 @@ class Engine:
     # column's pass 2, each with ONE host readback (one collective set when
     # sharded) instead of one or more per column
     # ==========================================================================
-    def _queue_column_selects(self, col, p1, plan, cand_info, probs, compact, selects):
+    def _queue_column_selects(self, col, p1, plan, cand_info, probs, compact, selects, fallbacks):
         """Decide, for each rank a column needs (describe.py:203-208), whether a
-        window bound resolves it from pass-1's counts or a select must run (in
-        a window's compacted candidates, or -- missed window / slot overflow --
-        over all the column's keys).  Appends compaction and select tasks; the
-        returned state is finished by _finish_column_quantiles."""
+        window bound resolves it from pass-1's counts or a select must run in a
+        window's compacted candidates (appended to `compact` / `selects`).  A
+        rank no window resolves (missed window, overflowed slots) goes to
+        `fallbacks` as (rank, key range [a, b], first rank of the range, keys
+        in it).  The returned state is finished by _finish_column_quantiles."""
         n = p1['count']
         is_int = not col.is_float
         needed = {}
@@ -554,7 +456,7 @@ class Engine:
             else:
                 needed[p] = (None, spark_percentile_approx_rank(n, p) - 1, None)
         ranks = sorted({r for v in needed.values() for r in (v[1], v[2]) if r is not None})
-        values, dense, fallback = {}, {}, None
+        values, dense = {}, {}
         for r in ranks:
             key = None
             for w in range(plan.n_windows):
@@ -582,44 +484,28 @@ class Engine:
                     else:
                         key = hi
                     break
-            if key is None:                                    # window missed: exact fallback
-                if fallback is None:
-                    fallback = self._all_keys(col)
-                arr, arr_n = fallback
-                # (the last field sizes the workspace budget identically on every rank)
-                selects.append([r, arr, arr_n, arr.numel(), r, 0, EMPTY64, max(1, int(p1['n_valid']))])
+            if key is None:
+                fallbacks.append((r,) + self._rank_key_range(r, p1, plan))
                 key = 'queued'
             values[r] = key
-        return {'values': values, 'needed': needed, 'is_int': is_int, 'probs': probs, 'fallback': fallback,
+        return {'values': values, 'needed': needed, 'is_int': is_int, 'probs': probs, 'fallback': False,
                 'dense': dense}
 
     SELECT_BATCH_BYTES = 24 << 30          # select workspaces alive at once (flushed in groups)
+    BYTES_BATCH_BYTES = 40 << 30           # byte columns' (key, count) group outputs alive at once
 
-    def quantiles_batch(self, items, probs=PROBS):
-        """[(col, p1, plan, cand_info)] -> [(quantiles, fallback_used)] with
-        the candidate compactions of every window in two launches, the selects
-        of every column in ~2 launches per radix round (sdp_select_batch; one
-        all-reduce per round for ALL columns when sharded) and one readback."""
+    def _run_selects(self, selects, res):
+        """Queue every select of `selects` ([rank, keys, n_dev, n_cap, k, lo, hi,
+        budget_cap]); result j lands in res[j].  Groups whose workspaces fit
+        SELECT_BATCH_BYTES run as one sdp_select_batch (sharded: one stream-
+        ordered all-reduce of the digit histograms per radix round for the
+        whole group).  Returns the buffers that must outlive the readback."""
         s = self._s()
-        states, sel_owner, compact, selects = [], [], [], []
-        for i, (col, p1, plan, cand_info) in enumerate(items):
-            before = len(selects)
-            states.append(self._queue_column_selects(col, p1, plan, cand_info, probs, compact, selects))
-            sel_owner += [i] * (len(selects) - before)
         keep = []
-        if compact:
-            tasks = (nat.SdpCompactTask * len(compact))()
-            for j, (cand, cnt, nseg, slot, offw, out, out_n) in enumerate(compact):
-                tasks[j] = nat.SdpCompactTask(cand.data_ptr(), cnt.data_ptr(), nseg, slot, offw.data_ptr(),
-                                              out.data_ptr(), out_n.data_ptr())
-            d_tasks = self._h2d(np.frombuffer(bytearray(bytes(tasks)), dtype=np.uint8))
-            sdp.sdp_compact_batch(ptr(d_tasks), len(compact), max(c[2] for c in compact), s)
-            keep.append((d_tasks, compact))
-        res = self._u64(max(1, len(selects)))
-        world = self.comm.world
         j0 = 0
         while j0 < len(selects):
-            # a group of selects whose workspaces fit the budget (at least one)
+            # a group of selects whose workspaces fit the budget (at least one);
+            # budget_cap is the same on every rank, so is the grouping
             j1, tot = j0, 0
             while j1 < len(selects):
                 wb = int(sdp.sdp_select_kth_workspace_bytes(int(selects[j1][7])))
@@ -640,7 +526,7 @@ class Engine:
                 rounds = max(rounds, int(sdp.sdp_select_rounds(_u(lo), _u(hi))))
             d_tasks = self._h2d(np.frombuffer(bytearray(bytes(tasks)), dtype=np.uint8))
             hist = self._u64(q * 2048)
-            if world == 1:
+            if not self.comm.sharded:
                 sdp.sdp_select_batch(ptr(d_tasks), q, rounds, ptr(hist), s)
             else:
                 sdp.sdp_select_batch_init(ptr(d_tasks), q, ptr(hist), s)
@@ -649,15 +535,58 @@ class Engine:
                     sdp.sdp_select_batch_step(ptr(d_tasks), q, rd, int(rd == rounds - 1), ptr(hist), s)
             keep.append((d_tasks, work, hist))
             j0 = j1
+        return keep
+
+    def quantiles_batch(self, items, probs=PROBS):
+        """[(col, p1, plan, cand_info)] -> [(quantiles, fallback_used)] with
+        the candidate compactions of every window in two launches, the selects
+        of every column in ~2 launches per radix round (sdp_select_batch; one
+        all-reduce per round for ALL columns when sharded) and one readback.
+        Ranks no window resolves are then selected one key range at a time:
+        the range's keys are re-collected from the column (sized by pass 1's
+        exact count), selected and freed, so the fallback holds at most one
+        range (<= 24 B per row of it) instead of every column's keys."""
+        s = self._s()
+        states, sel_owner, compact, selects, fbs = [], [], [], [], []
+        for i, (col, p1, plan, cand_info) in enumerate(items):
+            before = len(selects)
+            fb = []
+            states.append(self._queue_column_selects(col, p1, plan, cand_info, probs, compact, selects, fb))
+            sel_owner += [i] * (len(selects) - before)
+            fbs.append(fb)
+        keep = []
+        if compact:
+            tasks = (nat.SdpCompactTask * len(compact))()
+            for j, (cand, cnt, nseg, slot, offw, out, out_n) in enumerate(compact):
+                tasks[j] = nat.SdpCompactTask(cand.data_ptr(), cnt.data_ptr(), nseg, slot, offw.data_ptr(),
+                                              out.data_ptr(), out_n.data_ptr())
+            d_tasks = self._h2d(np.frombuffer(bytearray(bytes(tasks)), dtype=np.uint8))
+            sdp.sdp_compact_batch(ptr(d_tasks), len(compact), max(c[2] for c in compact), s)
+            keep.append((d_tasks, compact))
+        res = self._u64(max(1, len(selects)))
+        keep += self._run_selects(selects, res)
         keys = self._host_u64(res) if selects else []          # the one readback
         del keep
-        out = []
-        for i, st in enumerate(states):
-            for j, owner in enumerate(sel_owner):
-                if owner == i:
-                    st['values'][selects[j][0]] = keys[j]
-            out.append(self._finish_column_quantiles(st))
-        return out
+        for j, owner in enumerate(sel_owner):
+            states[owner]['values'][selects[j][0]] = keys[j]
+        del selects, compact
+        for st in states:
+            st['dense'] = None
+        # fallback ranks, one key range at a time (the same sequence on every rank)
+        for i, (col, p1, plan, cand_info) in enumerate(items):
+            groups = {}
+            for r, a, b, base, cnt in fbs[i]:
+                groups.setdefault((a, b, base, cnt), []).append(r)
+            for (a, b, base, cnt), rs in groups.items():
+                arr, arr_n = self._range_keys(col, a, b, min(int(cnt), col.length))
+                sel = [[r, arr, arr_n, arr.numel(), r - base, a, b, max(1, int(cnt))] for r in rs]
+                res = self._u64(len(sel))
+                keep = self._run_selects(sel, res)
+                for r, v in zip(rs, self._host_u64(res)):
+                    states[i]['values'][r] = v
+                del keep, arr, arr_n, sel
+                states[i]['fallback'] = True
+        return [self._finish_column_quantiles(st) for st in states]
 
     @staticmethod
     def _finish_column_quantiles(st):
@@ -673,7 +602,7 @@ class Engine:
                     out[p] = (hi_r - pos) * float(lk) + (pos - lo_r) * float(hk)
             else:
                 out[p] = key_to_float(values[lo_r])
-        return out, st['fallback'] is not None
+        return out, st['fallback']
 
     def pass2_batch(self, items, count_ctx=None):
         """[(col, mean, edges, hi_t, lo_t)] -> [pass-2 dict] (see pass2), all
@@ -706,8 +635,6 @@ class Engine:
                                     ptr(work), work.numel(), ptr(res), ptr(hist),
                                     ctypes.byref(hv['struct']) if hv else None, ctx['b1'], ptr(ctx['h1']),
                                     ptr(ctx['hcnt']), ptr(ctx['stats']), s)
-                if self._counted is Engine._counted:
-                    self._counted = {}
                 self._counted[id(col)] = ctx
             else:
                 work = self._bytes(sdp.sdp_pass2_workspace_bytes(col.length, col.dtype, bins))
@@ -715,7 +642,7 @@ class Engine:
                 sdp.sdp_pass2(ctypes.byref(cs), float(mean), ptr(e), bins, int(mono), float(hi_t), float(lo_t),
                               ptr(work), work.numel(), ptr(res), ptr(hist), s)
             outs.append((res, hist, e, work))
-        if self.comm.world == 1:
+        if not self.comm.sharded:
             raw = torch.cat([t for res, hist, _, _ in outs for t in (res[:rsz], hist.view(torch.uint8))]).cpu().numpy()
             result, off = [], 0
             for (res, hist, _, _) in outs:
@@ -744,25 +671,45 @@ class Engine:
         """percentile_approx(c, p, accuracy) (describe.py:205-206) as Spark 2.x's
         ApproximatePercentile returns it when the column's rows form `partitions`
         contiguous Spark partitions merged in partition order (sdp_gk_quantiles;
-        oracle/gk.py restates the algorithm).  Single rank: a sharded table's
-        partitions would have to be merged across ranks in order."""
+        oracle/gk.py restates the algorithm).  On a row-sharded table rank r's
+        rows form partitions r*k .. r*k+k-1 (k = partitions / world) and the
+        digests are merged across ranks in partition order."""
+        return self.gk_quantiles_batch([col], probs, partitions, accuracy)[0]
+
+    def gk_quantiles_batch(self, cols, probs=PROBS, partitions=1, accuracy=10000):
+        """gk_quantiles of several columns: single rank, every column's GK
+        kernels queued back to back and ONE readback of all statuses and
+        results.  The GK build runs one workgroup per Spark partition with a
+        sequential compress scan, so few partitions over many rows leave the
+        GPU mostly idle (a correctness mode: see DESIGN.md)."""
         partitions = int(partitions)
-        if self.comm.world > 1:
-            return self._gk_quantiles_sharded(col, probs, partitions, accuracy)
+        if self.comm.sharded:
+            return [self._gk_quantiles_sharded(c, probs, partitions, accuracy) for c in cols]
+        if partitions < 64 and any(c.length > 10 ** 7 for c in cols):
+            import warnings
+            warnings.warn('quantile_mode="gk" with %d Spark partition(s) over %d rows: the GK build is one '
+                          'workgroup per partition; expect seconds per column (spark_partitions sets P)'
+                          % (partitions, max(c.length for c in cols)), RuntimeWarning, stacklevel=3)
         wb = sdp.sdp_gk_workspace_bytes(partitions)
-        work = self._bytes(wb)
         pr = self._h2d(np.asarray(probs, dtype=np.float64))
-        out = torch.empty(max(len(probs), 1), dtype=torch.float64, device=self.device)
-        status = self._u64(3, zero=True)
-        cs = col.sdp()
-        nat.annotate('gk', col_read_bytes(col))
-        sdp.sdp_gk_quantiles(ctypes.byref(cs), partitions, int(accuracy), ptr(pr), len(probs), ptr(work), wb,
-                             ptr(out), ptr(status), self._s())
-        st = status.cpu().numpy()
-        if st[0]:
-            raise RuntimeError('sdp_gk_quantiles: summary capacity exceeded (status %d)' % int(st[0]))
-        vals = out.cpu().numpy()
-        return {p: float(v) for p, v in zip(probs, vals)}
+        npb = max(len(probs), 1)
+        out = torch.empty(len(cols) * npb, dtype=torch.float64, device=self.device)
+        status = self._u64(3 * len(cols), zero=True)
+        work = self._bytes(wb)                 # reused: launches on one stream run in order
+        for i, col in enumerate(cols):
+            cs = col.sdp()
+            nat.annotate('gk', col_read_bytes(col))
+            sdp.sdp_gk_quantiles(ctypes.byref(cs), partitions, int(accuracy), ptr(pr), len(probs), ptr(work), wb,
+                                 ptr(out[i * npb:]), ptr(status[3 * i:]), self._s())
+        host = torch.cat([status.view(torch.float64), out]).cpu().numpy()
+        st = host[:3 * len(cols)].view(np.int64)
+        vals = host[3 * len(cols):]
+        res = []
+        for i in range(len(cols)):
+            if st[3 * i]:
+                raise RuntimeError('sdp_gk_quantiles: summary capacity exceeded (status %d)' % int(st[3 * i]))
+            res.append({p: float(v) for p, v in zip(probs, vals[i * npb:(i + 1) * npb])})
+        return res
 
     def _gk_quantiles_sharded(self, col, probs, partitions, accuracy):
         """gk_quantiles of a row-sharded column: rank r's rows form Spark
@@ -827,17 +774,24 @@ class Engine:
         when describe_1d reaches that column, as the reference would."""
         ks = ks or [2] * len(cols)
         live = [i for i, pk in enumerate(packs) if pk[0]['count'] > 0]
-        qres = self.quantiles_batch([(cols[i], packs[i][0], packs[i][1], packs[i][2]) for i in live], probs)
+        # quantile_mode='gk': float columns take Spark's percentile_approx
+        # element (also the q1/q3 of the outlier thresholds, as
+        # describe.py:212-223 uses them) and skip the exact window selects
+        gk_idx = [i for i in live if gk is not None and cols[i].is_float]
+        exact = [i for i in live if i not in set(gk_idx)]
+        qmap = dict(zip(exact, self.quantiles_batch([(cols[i], packs[i][0], packs[i][1], packs[i][2])
+                                                     for i in exact], probs)))
+        if gk_idx:
+            gq = self.gk_quantiles_batch([cols[i] for i in gk_idx], probs, gk.get('partitions', 1),
+                                         gk.get('accuracy', 10000))
+            qmap.update({i: (q, False) for i, q in zip(gk_idx, gq)})
         for i in live:                       # candidate slots are no longer needed
             packs[i][2]['cand'] = None
         stats = [None] * len(cols)
         p2_items, p2_idx = [], []
-        for i, (qs, fb) in zip(live, qres):
+        for i in live:
+            qs, fb = qmap[i]
             col, p1 = cols[i], packs[i][0]
-            if gk is not None and col.is_float:
-                # Spark's percentile_approx element (opt-in): also the q1/q3 of
-                # the outlier thresholds, as describe.py:212-223 uses them
-                qs = self.gk_quantiles(col, probs, gk.get('partitions', 1), gk.get('accuracy', 10000))
             mom = moments(p1, not col.is_float)
             st = NumericStats(count=p1['count'], n_valid=p1['n_valid'], n_nan=p1['n_nan'], n_zero=p1['n_zero'],
                               **mom)
@@ -859,14 +813,16 @@ class Engine:
             p2_idx.append(i)
             stats[i] = st
         # columns whose countDistinct takes the partitioning path: pass 2 also
-        # does their level-1 count (single rank; one column read fewer)
+        # does their level-1 count (one column read fewer, single rank or sharded)
         count_ctx = {}
-        if self.comm.world == 1:
-            for j, i in enumerate(p2_idx):
-                if i in group_cols:
-                    ctx = self._group_prepare(cols[i], False)
-                    if ctx is not None:
-                        count_ctx[j] = ctx
+        for j, i in enumerate(p2_idx):
+            if i in group_cols:
+                # sharded: group_sharded_batch's level-1 geometry (heavy keys
+                # pooled over the ranks, the same on every rank)
+                ctx = self._group_prepare_sharded(cols[i]) if self.comm.sharded else \
+                    self._group_prepare(cols[i], False)
+                if ctx is not None:
+                    count_ctx[j] = ctx
         for i, r2 in zip(p2_idx, self.pass2_batch(p2_items, count_ctx)):
             st = stats[i]
             st.mad = r2['abs_dev_sum']
@@ -888,14 +844,14 @@ class Engine:
         per column; results are identical to numeric_pass1 column by column."""
         if not cols:
             return []
-        world = self.comm.world
+        world, sharded = self.comm.world, self.comm.sharded
         ns = max(1, SAMPLE_TOTAL // world)
         s = self._s()
         samples = self._u64(len(cols) * ns)
         for i, col in enumerate(cols):
             cs = col.sdp()
             sdp.sdp_sample_keys(ctypes.byref(cs), ns, ptr(samples[i * ns:]), s)
-        if world > 1:
+        if sharded:
             # [cols, world * ns]: column i's pooled sample in rank order
             samples = torch.cat([p.view(len(cols), ns) for p in self.comm.allgather(samples)], dim=1).contiguous()
         pr = self._h2d(np.array(list(probs), dtype=np.float64))
@@ -908,21 +864,21 @@ class Engine:
         # like the first): fewer pass-1 candidates and cheaper selects
         ns2 = max(1, SAMPLE2_TOTAL // world)
         # (sharded: always, so every rank takes the same collective path)
-        if world > 1 or min(c.length for c in cols) > SAMPLE_TOTAL:
+        if sharded or min(c.length for c in cols) > SAMPLE_TOTAL:
             s2 = self._u64(len(cols) * ns2)
             for i, col in enumerate(cols):
                 cs = col.sdp()
                 sdp.sdp_sample_keys(ctypes.byref(cs), ns2, ptr(s2[i * ns2:]), s)
-            if world > 1:
+            if sharded:
                 s2 = torch.cat([p.view(len(cols), ns2) for p in self.comm.allgather(s2)], dim=1).contiguous()
             sdp.sdp_quantile_refine_batch(ptr(s2), ns2 * world, len(cols), ptr(pr), len(probs), ptr(plans_dev), s)
             ns3 = SAMPLE3_TOTAL // world
-            if ns3 > ns2 and (world > 1 or min(c.length for c in cols) > SAMPLE2_TOTAL):
+            if ns3 > ns2 and (sharded or min(c.length for c in cols) > SAMPLE2_TOTAL):
                 s3 = self._u64(len(cols) * ns3)
                 for i, col in enumerate(cols):
                     cs = col.sdp()
                     sdp.sdp_sample_keys(ctypes.byref(cs), ns3, ptr(s3[i * ns3:]), s)
-                if world > 1:
+                if sharded:
                     s3 = torch.cat([p.view(len(cols), ns3) for p in self.comm.allgather(s3)], dim=1).contiguous()
                 sdp.sdp_quantile_refine_batch(ptr(s3), ns3 * world, len(cols), ptr(pr), len(probs), ptr(plans_dev), s)
         # heavy-key samples of the columns the partitioning path will group
@@ -930,7 +886,7 @@ class Engine:
         # plans; the host finds the heavy keys while pass 1 runs
         # (sharded: every column, PART_SAMPLE / world rows per rank pooled in
         # rank order, the same keys on every rank -- group_sharded's gather)
-        hcols = [c for c in cols if world > 1 or c.length >= (1 << 16)]
+        hcols = [c for c in cols if sharded or c.length >= (1 << 16)]
         hn_each = PART_SAMPLE // world * world
         hs = None
         if hcols:
@@ -942,7 +898,7 @@ class Engine:
                     continue
                 cs = col.sdp()
                 sdp.sdp_part_sample(ctypes.byref(cs), None, nsr, ptr(hs[i * nsr:]), None, s)
-            if world > 1:
+            if sharded:
                 hs = torch.cat([p.view(len(hcols), nsr) for p in self.comm.allgather(hs)], dim=1).contiguous()
             sdp.sdp_sort_small_batch(ptr(hs), hn_each, len(hcols), s)
             raw = torch.cat([plans_dev, hs.view(-1).view(torch.uint8)]).cpu().numpy()
@@ -977,7 +933,7 @@ class Engine:
                 self._heavy_pre[id(col)] = self._heavy_struct(a[start], cnt)
                 if start.size >= 0.9 * a.size:
                     self._near_unique.add(id(col))
-        if world == 1:
+        if not sharded:
             raw = res_all.cpu().numpy().tobytes()
             merged = [merge_pass1_results([nat.SdpPass1Result.from_buffer_copy(raw[i * rsz:(i + 1) * rsz])])
                       for i in range(len(cols))]
@@ -1016,7 +972,7 @@ class Engine:
         outside the partitions (describe.py:251's hot groups).  gather=True
         (fixed keys of a sharded table): the samples of all ranks are pooled,
         so every rank picks the same heavy keys."""
-        if not isb and gather == (self.comm.world > 1) and self._heavy_pre and id(col) in self._heavy_pre:
+        if not isb and gather == self.comm.sharded and self._heavy_pre and id(col) in self._heavy_pre:
             return self._heavy_pre.pop(id(col))        # sampled with pass 1 (numeric_pass1_batch)
         smp = self._heavy_sample_launch(col, isb, gather)
         if smp['readback'] is not None:
@@ -1028,7 +984,7 @@ class Engine:
     def _heavy_sample_launch(self, col, isb, gather=False):
         """Queue the heavy-key sample of `col` (no readback)."""
         ns = min(PART_SAMPLE, max(col.length, 1))
-        if gather and self.comm.world > 1:
+        if gather and self.comm.sharded:
             ns = max(1, min(PART_SAMPLE // self.comm.world, col.length))   # pooled: PART_SAMPLE in all
         s = self._s()
         h = self._u64(ns)
@@ -1041,7 +997,7 @@ class Engine:
         else:
             keep = None
             sdp.sdp_part_sample(ctypes.byref(col.sdp()), None, ns, ptr(h), None, s)
-        if gather and self.comm.world > 1:
+        if gather and self.comm.sharded:
             h = torch.cat(self.comm.allgatherv(h))
         # sample hashes (and byte-key metas) leave the device in one piece
         readback = torch.cat([h, keep[2][:ns]]) if (isb and keep is not None) else None
@@ -1400,7 +1356,7 @@ class Engine:
         if not cols:
             return []
         s = self._s()
-        B1 = 10
+        B1 = self.SHARDED_B1
         nb1 = 1 << B1
         n_all = int(comm.allreduce_sum(torch.tensor([cols[0].length], dtype=torch.int64,
                                                      device=self.device)).item())
@@ -1410,19 +1366,15 @@ class Engine:
         lo = [(r * nb1) // world for r in range(world + 1)]
         ctxs = []
         for col in cols:                                  # level 1 counts of every column, no readback
-            n = col.length
-            hv = self._heavy_keys(col, False, gather=True)
-            ctx = {'col': col, 'n': n, 'cs': col.sdp(), 'hv': hv, 'stats': self._u64(68, zero=True),
-                   'hcnt': self._u64(max(hv['n'] if hv else 1, 1), zero=True), 'rb': col_read_bytes(col)}
-            ctx['hvref'] = ctypes.byref(hv['struct']) if hv else None
-            rpb = sdp.sdp_part_rows_per_block(max(n, 1), 0)
-            grid = max(1, -(-n // rpb))
-            h1 = torch.zeros(nb1 * grid, dtype=torch.int32, device=self.device)
-            if n:
-                nat.annotate(_label(col, 'count'), ctx['rb'])
-                sdp.sdp_part_rows(ctypes.byref(ctx['cs']), None, ctx['hvref'], B1, 0, ptr(h1), None, None,
-                                  ptr(ctx['hcnt']), ptr(ctx['stats']), s)
-            ctx['o1'] = self._scan(h1)
+            ctx = self._counted.pop(id(col), None)        # counted by pass 2 (sdp_pass2_count)
+            if ctx is None:
+                ctx = self._group_prepare_sharded(col)
+                if ctx['n']:
+                    nat.annotate(_label(col, 'count'), ctx['rb'])
+                    sdp.sdp_part_rows(ctypes.byref(ctx['cs']), None, ctx['hvref'], B1, 0, ptr(ctx['h1']), None,
+                                      None, ptr(ctx['hcnt']), ptr(ctx['stats']), s)
+            grid = ctx['grid']
+            ctx['o1'] = self._scan(ctx.pop('h1'))
             ctx['bsn_dev'] = torch.cat([ctx['o1'][0:nb1 * grid:grid], ctx['o1'][-1:]])
             ctxs.append(ctx)
         flat = torch.cat([c['bsn_dev'] for c in ctxs]).cpu().numpy().astype(np.int64)
@@ -1511,6 +1463,39 @@ class Engine:
                         'groups': groups, 'groups_local': groups, 'sharded': True})
         return out
 
+    SHARDED_B1 = 10            # level-1 hash bits of the sharded grouping (buckets owned by rank ranges)
+
+    def _group_prepare_sharded(self, col):
+        """Level-1 geometry and buffers of group_sharded_batch for one column
+        (the same as the single-rank count's, so sdp_pass2_count can fill it);
+        heavy keys from the samples pooled over every rank."""
+        n = col.length
+        hv = self._heavy_keys(col, False, gather=True)
+        rpb = sdp.sdp_part_rows_per_block(max(n, 1), 0)
+        grid = max(1, -(-n // rpb))
+        nb1 = 1 << self.SHARDED_B1
+        ctx = {'col': col, 'n': n, 'cs': col.sdp(), 'hv': hv, 'stats': self._u64(68, zero=True),
+               'hcnt': self._u64(max(hv['n'] if hv else 1, 1), zero=True), 'rb': col_read_bytes(col),
+               'b1': self.SHARDED_B1, 'grid': grid, 'sharded': True,
+               'h1': torch.zeros(nb1 * grid, dtype=torch.int32, device=self.device)}
+        ctx['hvref'] = ctypes.byref(hv['struct']) if hv else None
+        return ctx
+
+    def distinct_paths_sharded(self, cols, hints, bounds, n_all):
+        """'bitmap' | 'table' | 'group' per column: distinct_batch_sharded's
+        path choice (identical on every rank: it reads merged pass-1 values
+        and the global row count only)."""
+        out = []
+        for col, hint, bd in zip(cols, hints, bounds):
+            if (bd is not None and col.kind == 'fixed' and col.dtype in self.BITMAP_DTYPES
+                    and bd[1] - bd[0] + 1 <= nat.BITMAP_MAX_BITS):
+                out.append('bitmap')
+            elif hint is not None and hint * 4 <= max(n_all, 1):
+                out.append('table')
+            else:
+                out.append('group')
+        return out
+
     def distinct_batch_sharded(self, cols, hints, bounds):
         """distinct_batch on a row-sharded table (every rank calls it with the
         same columns; hints/bounds come from the merged pass 1): bitmaps for
@@ -1521,12 +1506,12 @@ class Engine:
                                                     device=self.device)).item()) if cols else 0
         out = [None] * len(cols)
         grp = []
-        for i, (col, hint, bd) in enumerate(zip(cols, hints, bounds)):
-            if (bd is not None and col.kind == 'fixed' and col.dtype in self.BITMAP_DTYPES
-                    and bd[1] - bd[0] + 1 <= nat.BITMAP_MAX_BITS):
+        for i, (col, pth) in enumerate(zip(cols, self.distinct_paths_sharded(cols, hints, bounds, n_all))):
+            bd = bounds[i]
+            if pth == 'bitmap':
                 out[i] = self.distinct_bitmap(col, bd[0], bd[1] - bd[0] + 1)
-            elif hint is not None and hint * 4 <= max(n_all, 1):
-                out[i] = self._distinct_fixed_table(col, False, hint)['groups']
+            elif pth == 'table':
+                out[i] = self._distinct_fixed_table(col, False, hints[i])['groups']
             else:
                 grp.append(i)
         for i, tab in zip(grp, self.group_sharded_batch([cols[i] for i in grp])):
@@ -1560,7 +1545,7 @@ class Engine:
         in [lo, lo + range_), range_ <= 2^20: LDS bitmaps (sdp_bitmap.hip).  Ranks
         all-gather their OR-ed bitmaps and re-reduce them."""
         out, bm, nw = self._distinct_bitmap_launch(col, lo, range_, keep_bitmap=True)
-        if self.comm.world > 1:
+        if self.comm.sharded:
             allb = torch.cat(self.comm.allgather(bm))
             out.zero_()
             sdp.sdp_bitmap_reduce(ptr(allb), self.comm.world, nw, None, ptr(out), self._s())
@@ -1574,14 +1559,14 @@ class Engine:
         ms); a global table sized by a small key range (<= rows / 4) stays
         cache-resident and wins there (23 vs 44 ms)."""
         n = col.length
-        if self.comm.world > 1:       # the path choice must agree on every rank: decide on the global rows
+        if self.comm.sharded:         # the path choice must agree on every rank: decide on the global rows
             n = int(self.comm.allreduce_sum(torch.tensor([n], dtype=torch.int64, device=self.device)).item())
         small_range = capacity_hint is not None and capacity_hint * 4 <= max(n, 1)
-        if self.comm.world == 1 and not small_range and col.length >= (1 << 16):
+        if not self.comm.sharded and not small_range and col.length >= (1 << 16):
             tab = self.group(col, with_counts, dense=with_counts)
             if tab is not None:
                 return tab
-        if self.comm.world > 1 and not with_counts and not small_range:
+        if self.comm.sharded and not with_counts and not small_range:
             tab = self.group_sharded(col)          # collective: every rank takes this branch
             if tab is not None:
                 return tab
@@ -1601,7 +1586,7 @@ class Engine:
         groups = st[0] + (1 if st[2] else 0)
         tab = {'slots': slots, 'counts': counts, 'capacity': cap, 'bytes': False, 'max_key_rows': st[2],
                'rows': st[1], 'groups': groups, 'groups_local': st[0], 'col': col}
-        if self.comm.world > 1 and not exchanged:
+        if self.comm.sharded and not exchanged:
             tab = self._exchange_fixed(tab, with_counts)
         return tab
 
@@ -1613,38 +1598,62 @@ class Engine:
         if col.length >= (1 << 16):
             tab = self.group(col, True, dense=True)          # no collective inside
             if tab is not None:
-                return self._exchange_bytes(tab) if self.comm.world > 1 else tab
+                return self._exchange_bytes(tab) if self.comm.sharded else tab
         return self.value_counts_bytes_table(col)
 
     def value_counts_bytes_batch(self, cols):
-        """value_counts_bytes of several byte columns on one rank with shared
-        readbacks: ONE readback of every column's heavy-key sample, then per
-        column the one-read records, the bucket-start readback and the
-        scatters/dedup, and ONE readback of every column's group statistics."""
+        """value_counts_bytes of several byte columns with shared readbacks:
+        ONE readback of every column's heavy-key sample, then per column the
+        one-read records, the bucket-start readback and the scatters/dedup,
+        and ONE readback of the group statistics of every column in flight
+        (flushed under BYTES_BATCH_BYTES).  The grouping is local to the rank;
+        on a sharded table each column's groups then take the owner exchange."""
         out = [None] * len(cols)
-        if self.comm.world > 1:
-            return [self.value_counts_bytes(c) for c in cols]
         big = [i for i, c in enumerate(cols) if c.length >= (1 << 16)]
         hvs = self._heavy_keys_batch([cols[i] for i in big])
         done = []
-        for i, hv in zip(big, hvs):
-            ctx = self._group_prepare(cols[i], True, hv=hv)
-            if ctx is None:
-                continue
-            self._group_count(ctx)
-            self._group_scan(ctx)
-            self._group_middle(ctx, ctx['bsn_dev'].cpu().numpy().astype(np.int64))
-            done.append((i, ctx))
-        if done:
+
+        def flush():
+            # one readback of the group statistics of every column in flight;
+            # the (key, count) outputs of each are compacted and then dropped
+            if not done:
+                return
             sizes = [ctx['stats_dev'].numel() for _, ctx in done]
             allst = self._host_u64(torch.cat([ctx['stats_dev'] for _, ctx in done]))
             off = 0
             for (i, ctx), m in zip(done, sizes):
                 out[i] = self._group_end(ctx, allst[off:off + m], True)
+                for key in ('out_key', 'out_cnt', 'starts', 'ngroups', 'stats_dev'):
+                    ctx.pop(key, None)
                 off += m
-        for i, c in enumerate(cols):                 # small columns, collisions, table overflow
+            done.clear()
+
+        held = 0
+        for i, hv in zip(big, hvs):
+            ctx = self._group_prepare(cols[i], True, hv=hv)
+            if ctx is None:
+                continue
+            # each column in flight keeps 16 B per record of (key, count)
+            # outputs until the shared readback: flush under a byte budget
+            need = 16 * cols[i].length
+            if done and held + need > self.BYTES_BATCH_BYTES:
+                flush()
+                held = 0
+            self._group_count(ctx)
+            self._group_scan(ctx)
+            self._group_middle(ctx, ctx['bsn_dev'].cpu().numpy().astype(np.int64))
+            done.append((i, ctx))
+            held += need
+        flush()
+        for i, c in enumerate(cols):
+            # small columns, collisions, table overflow: the global table (which
+            # exchanges itself when sharded); sharded partitioned groups go
+            # through the owner exchange -- one exchange per column, in column
+            # order, on every rank
             if out[i] is None:
                 out[i] = self.value_counts_bytes_table(c)
+            elif self.comm.sharded:
+                out[i] = self._exchange_bytes(out[i])
         return out
 
     def value_counts_bytes_table(self, col, row_counts=None, exchanged=False, capacity=None):
@@ -1658,7 +1667,7 @@ class Engine:
         st = self._host_u64(stats)
         tab = {'slots': slots, 'counts': counts, 'capacity': cap, 'bytes': True, 'rows': st[1], 'groups': st[0],
                'groups_local': st[0], 'col': col}
-        if self.comm.world > 1 and not exchanged:
+        if self.comm.sharded and not exchanged:
             tab = self._exchange_bytes(tab)
         return tab
 

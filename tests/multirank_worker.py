@@ -89,6 +89,11 @@ def main():
         'corr': datagen.corr_table(20_000),
         'legacy': datagen.legacy_table(),
     }
+    if 'c3' in (sys.argv[2].split(',') if len(sys.argv) > 2 else []):
+        import bench
+        # the bench generator at 4 M rows, made on the device (rank-independent: the
+        # whole table is built on every rank and sliced like the others)
+        tables['c3'] = bench.shard_to_arrow(bench.make_c3_shard(4_000_000, 0, 1, dev))
     only = sys.argv[2].split(',') if len(sys.argv) > 2 else None
     failures = 0
     for name, t in tables.items():
@@ -113,7 +118,11 @@ def main():
                 print('[%s] rank %d missing images for %s' % (name, rank, bad), flush=True)
         if rank == 0:
             import oracle
-            want = oracle.describe(t)
+            if t.num_rows > 1_000_000:
+                from oracle import fast
+                want = fast.describe(t)
+            else:
+                want = oracle.describe(t)
             try:
                 assert_describe_equal(got, want)
                 print('[%s] OK world=%d' % (name, world), flush=True)
@@ -125,6 +134,13 @@ def main():
     dist.barrier()
     dist.destroy_process_group()
     if rank == 0:
+        # the collectives the sharded path issued (SDP_REQUIRE_CALLS: each must have run)
+        print('[calls] backend=%s sharded=%s %s' % (comm.backend, comm.sharded, dict(comm.calls)), flush=True)
+        need = [c for c in os.environ.get('SDP_REQUIRE_CALLS', '').split(',') if c]
+        missing = [c for c in need if not comm.calls.get(c)]
+        if missing:
+            failures += 1
+            print('[calls] MISSING %s' % missing, flush=True)
         print('MULTIRANK %s failures=%d' % ('OK' if not failures else 'FAILED', failures), flush=True)
     if failures:
         sys.exit(1)

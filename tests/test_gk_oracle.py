@@ -63,3 +63,17 @@ def test_empty_partitions_are_skipped():
     a = gk.percentile_approx([[], [3.0, 1.0, 2.0], []], [0.5])
     b = gk.percentile_approx([[3.0, 1.0, 2.0]], [0.5])
     assert a == b
+
+
+def test_query_rank_saturates_like_scala_toint():
+    # QuantileSummaries.query: rank = math.ceil(q * count).toInt, which
+    # saturates at Int.MaxValue once q * count >= 2^31 (a row-sharded table of
+    # ~2.3e9 values at q = 0.95).  Interior samples at minRank 2^31 - 2 and
+    # 3e9 - 2 (target error 3): the saturated rank matches the first; the
+    # unbounded rank 2.85e9 matches none and falls through to the maximum.
+    count = 3 * 10 ** 9
+    m = gk.INT_MAX
+    sampled = [(0.0, 1, 0), (1.0, m - 1, 0), (2.0, count - m - 1, 0), (3.0, 1, 0)]
+    s = gk.Summary(1e-9, sampled, count)
+    assert s.query(0.95) == 1.0          # rank min(ceil(2.85e9), 2^31 - 1) = 2^31 - 1 = minRank of 1.0
+    assert s.query(0.5) == 3.0           # ceil(1.5e9) < 2^31 - 1 matches no interior sample: the maximum

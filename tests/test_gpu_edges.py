@@ -1,8 +1,9 @@
 """Edge paths of the GPU engine that the ordinary tables never reach:
 
-* the quantile window-miss and candidate-slot-overflow fallbacks
-  (engine._quantiles_launch -> exact whole-column select), forced by the
-  SDP_DEBUG_QUANTILE knob, against the oracle;
+* the quantile window-miss and candidate-slot-overflow fallbacks (the
+  missed rank's key range re-collected by sdp_column_keys_range, then an
+  exact select), forced by the SDP_DEBUG_QUANTILE knob, against the oracle
+  (test_gpu_scale_1e9.py repeats the forced miss at 1e9 rows);
 * determinism: two describe() runs of one table are bitwise
   equal in every output;
 * a duck-typed Spark DataFrame (toArrow / limit().toPandas()) through
