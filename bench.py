@@ -408,7 +408,18 @@ def shard_to_arrow(shard):
     return pa.table(arrays)
 
 
-CPU_WORKERS = 16          # the GPU box's CPU share (OMP_NUM_THREADS there); one column per process
+def cpu_share():
+    """(cores the baseline uses, what the host reports): the box gives this job
+    a 16-CPU share (OMP_NUM_THREADS=16 there) while os.cpu_count() reports the
+    whole machine; the affinity mask bounds both."""
+    visible = os.cpu_count() or 1
+    try:
+        allowed = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        allowed = visible
+    share = int(os.environ.get('OMP_NUM_THREADS', '16') or 16)
+    return max(1, min(allowed, share)), {'os_cpu_count': visible, 'affinity_cpus': allowed,
+                                         'omp_num_threads': os.environ.get('OMP_NUM_THREADS')}
 
 
 def cpu_baseline(sample_rows, device):
@@ -428,6 +439,7 @@ def cpu_baseline(sample_rows, device):
     fast.describe(table)
     dt = time.perf_counter() - t0
     return {'value': round(sample_rows / dt, 1), 'unit': 'rows/s', 'cores': workers, 'kind': 'port',
+            'host_cpus': cpu_share()[1],
             'sample': '%d rows x 16 cols of the same C3 generator; oracle/fast.py vectorised numpy/Arrow '
                       'restatement, one column per process on %d processes (CPU restatement, not reference Spark: '
                       'no pyspark/JVM in the image), %.1f s' % (sample_rows, workers, dt)}
@@ -487,16 +499,27 @@ def main():
         # the CPU baseline's worker processes, likewise spawned before any GPU call
         sys.path.insert(0, ROOT)
         from oracle import fast
-        fast.start_pool(min(CPU_WORKERS, os.cpu_count() or 1))
+        fast.start_pool(cpu_share()[0])
     local = int(os.environ.get('LOCAL_RANK', '0'))
     # (local % devices: a gloo rehearsal may put several ranks on one GPU)
     local = local % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     device = torch.device('cuda', local)
     comm = None
-    if world > 1:
+    # SDP_FORCE_SHARDED=1 at one rank: the sharded code paths over a one-rank
+    # RCCL group (per-round collectives, owner exchanges), for measuring their
+    # cost on one GPU; the JSON line says so in config.parallelism
+    force_sharded = os.environ.get('SDP_FORCE_SHARDED', '0') == '1'
+    if world > 1 or force_sharded:
         import torch.distributed as dist
         os.environ.setdefault('MASTER_ADDR', '127.0.0.1')
+        if 'MASTER_PORT' not in os.environ:
+            import socket
+            with socket.socket() as sk:
+                sk.bind(('127.0.0.1', 0))
+                os.environ['MASTER_PORT'] = str(sk.getsockname()[1])
+        os.environ.setdefault('RANK', str(rank))
+        os.environ.setdefault('WORLD_SIZE', str(world))
         backend = os.environ.get('SDP_DIST_BACKEND', 'nccl')      # nccl = RCCL over xGMI
         if backend == 'nccl':
             dist.init_process_group('nccl', device_id=device)
@@ -584,7 +607,8 @@ def main():
         'ms_per_step': round(1e3 * elapsed / args.steps, 2), 'higher_is_better': True, 'scaling': 'strong',
         'vs_baseline': None, 'dtype': 'f64', 'data': 'synthetic (torch, seeded, generated in HBM)',
         'config': {'workload': workload, 'rows': args.rows, 'columns': ncols,
-                   'parallelism': 'row-shard x%d' % world, 'plots': not args.no_plots,
+                   'parallelism': 'row-shard x%d%s' % (world, ' (sharded paths forced)' if force_sharded else ''),
+                   'plots': not args.no_plots,
                    'column_workers': column_workers_used},
         'roofline': rl,
         'per_kernel': per_kernel,

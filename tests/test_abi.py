@@ -82,6 +82,10 @@ def test_part_argument_checks_without_gpu():
     with pytest.raises(_native.NativeError, match='scan_u32'):
         _native.sdp.sdp_scan_u32(None, 0, None, None, 0, None)
     assert _native.sdp.sdp_part_rows_per_block(10 ** 9, 0) % 4096 == 0
+    # an empty shard (a rank with no rows) still gets a positive block size: the
+    # launchers divide by it
+    assert _native.sdp.sdp_part_rows_per_block(0, 0) > 0 and _native.sdp.sdp_part_rows_per_block(0, 1) > 0
+    assert _native.sdp.sdp_pass2_count_workspace_bytes(0, 10) > 0
     assert _native.sdp.sdp_part_bucket_target(1, 1) == 2048
     with pytest.raises(_native.NativeError, match='part_rows_records'):
         _native.sdp.sdp_part_rows_records(None, None, 4, None, None, None, None, None, None)

@@ -70,6 +70,7 @@ def test_c5_wide_pearson_2e5():
     w = want_raw['corr'].to_numpy()
     assert g.shape == (512, 512)
     assert np.allclose(g, w, rtol=1e-9, atol=1e-12)
-    # wide tables keep candidate-slot memory bounded (engine.CAND_FULL_BUDGET)
+    # wide tables keep candidate-slot memory bounded (engine.CAND_FULL_BUDGET:
+    # 1 GiB of room-for-every-row slots per pass-1 batch, sample-sized beyond)
     table_bytes = 200_000 * 512 * 4
-    assert torch.cuda.max_memory_allocated() < 3 * table_bytes + (3 << 30)
+    assert torch.cuda.max_memory_allocated() < 3 * table_bytes + (7 << 29)
