@@ -289,6 +289,13 @@ int sdp_column_keys(const sdp_column *col, uint64_t *d_out, uint64_t *d_out_n,
 int sdp_column_keys_range(const sdp_column *col, uint64_t lo_key, uint64_t hi_key,
                           uint64_t *d_out, uint64_t *d_out_n, void *stream);
 
+/* countDistinct of a column whose na.drop keys are non-decreasing in row
+ * order (describe.py:143 for ids / timestamps / pre-sorted data): d_out[4] =
+ * {distinct (1 + key changes between consecutive valid rows), violation
+ * (a decrease, or a null run too long to walk: group the column instead),
+ * first valid key, last valid key (UINT64_MAX when none)}; one read. */
+int sdp_sorted_distinct(const sdp_column *col, uint64_t *d_out, void *stream);
+
 /* Fused pass 2: mad, histogram over host-built CASE edges, outlier counts. */
 int sdp_pass2(const sdp_column *col, double mean, const double *d_edges,
               int32_t bins, int32_t edges_monotone, double hi_t, double lo_t,

@@ -1018,6 +1018,83 @@ __global__ void column_keys_kernel(sdp_column col, uint64_t lo, uint64_t hi, uin
     }
 }
 
+// ---- countDistinct of a sorted column -------------------------------------------
+// A column whose na.drop keys are non-decreasing in row order (ids, timestamps,
+// pre-sorted data) has distinct = 1 + #(key changes between consecutive valid
+// rows) -- one streaming read instead of the partitioning pipeline.  Each
+// element compares its key with the previous valid row's (a walk back over
+// nulls, normally one cached load); any decrease sets the violation flag and
+// the caller takes the grouping path.  out: [0] distinct (the first valid row
+// counts 1), [1] violation, [2] first valid row, [3] last valid row (indices,
+// turned into keys by sorted_distinct_final_kernel).
+constexpr int SD_T = 256;
+constexpr int SD_E = 4;                 // consecutive elements per thread per step
+constexpr int SD_WALK = 256;            // rows walked back over nulls at most
+
+template <typename T>
+__device__ __forceinline__ bool sd_fetch(const sdp_column &c, int64_t i, uint64_t &k) {
+    if (!valid_bit(c.d_validity, c.validity_bit_offset, i)) return false;
+    const T x = ((const T *)c.d_values)[i];
+    k = Elem<T>::key(x);                // NaN: one canonical key; -0.0 == +0.0
+    return true;
+}
+
+template <typename T>
+__global__ void __launch_bounds__(SD_T) sorted_distinct_kernel(sdp_column col, uint64_t *out) {
+    const int64_t n = col.length;
+    const int64_t ngroups = (n + SD_E - 1) / SD_E;
+    const int64_t stride = (int64_t)gridDim.x * SD_T;
+    uint64_t d = 0;
+    bool viol = false;
+    int64_t first = INT64_MAX, last = -1;
+    for (int64_t gi = (int64_t)blockIdx.x * SD_T + threadIdx.x; gi < ngroups; gi += stride) {
+        const int64_t i0 = gi * SD_E;
+        uint64_t prev = 0;
+        bool have = false;
+        // the previous valid row before this group (one cached load unless
+        // nulls); a null run longer than SD_WALK gives up (violation: the
+        // caller groups the column instead), so a mostly-null column costs
+        // O(n SD_WALK), never O(n^2)
+        int64_t j = i0 - 1;
+        for (int w = 0; j >= 0 && w < SD_WALK; --j, ++w)
+            if (sd_fetch<T>(col, j, prev)) { have = true; break; }
+        if (!have && j >= 0) viol = true;
+#pragma unroll
+        for (int e = 0; e < SD_E; ++e) {
+            const int64_t i = i0 + e;
+            uint64_t k;
+            if (i < n && sd_fetch<T>(col, i, k)) {
+                d += (!have || k != prev);
+                viol |= have && k < prev;
+                if (!have) first = i;
+                last = i;
+                prev = k;
+                have = true;
+            }
+        }
+    }
+    d = wave_sum_u64(d);
+    const bool any_viol = __any(viol);
+    const int64_t fmin = wave_min_i64(first), lmax = wave_max_i64(last);
+    if (lane_id() == 0) {
+        if (d) atomicAdd((unsigned long long *)&out[0], (unsigned long long)d);
+        if (any_viol) atomicOr((unsigned long long *)&out[1], 1ull);
+        if (fmin != INT64_MAX) atomicMin((long long *)&out[2], (long long)fmin);
+        if (lmax >= 0) atomicMax((long long *)&out[3], (long long)lmax);
+    }
+}
+__global__ void sorted_distinct_init_kernel(uint64_t *out) {
+    out[0] = 0; out[1] = 0; out[2] = (uint64_t)INT64_MAX; out[3] = (uint64_t)(int64_t)-1;
+}
+template <typename T>
+__global__ void sorted_distinct_final_kernel(sdp_column col, uint64_t *out) {
+    const int64_t f = (int64_t)out[2], l = (int64_t)out[3];
+    uint64_t k = EMPTY64;
+    out[2] = (l >= 0 && sd_fetch<T>(col, f, k)) ? k : EMPTY64;
+    k = EMPTY64;
+    out[3] = (l >= 0 && sd_fetch<T>(col, l, k)) ? k : EMPTY64;
+}
+
 // ============================================================================
 // pass 2: mad + histogram + outliers
 // ============================================================================
@@ -1896,6 +1973,20 @@ extern "C" int sdp_column_keys_range(const sdp_column *col, uint64_t lo_key, uin
     SDP_DISPATCH_NUMERIC(col->dtype,
         hipLaunchKernelGGL(column_keys_kernel<T>, dim3(1024), dim3(256), 0, s, *col, lo_key, hi_key, d_out, d_out_n));
     return check_launch("column_keys_kernel");
+}
+
+extern "C" int sdp_sorted_distinct(const sdp_column *col, uint64_t *d_out, void *stream) {
+    int rc = check_col(col, "sdp_sorted_distinct");
+    if (rc) return rc;
+    if (d_out == nullptr) return set_error(SDP_EINVAL, "sdp_sorted_distinct: output");
+    hipStream_t s = (hipStream_t)stream;
+    hipLaunchKernelGGL(sorted_distinct_init_kernel, dim3(1), dim3(1), 0, s, d_out);
+    const int64_t groups = (col->length + SD_E - 1) / SD_E;
+    const int grid = (int)std::min<int64_t>(std::max<int64_t>((groups + SD_T - 1) / SD_T, 1), 8192);
+    SDP_DISPATCH_NUMERIC(col->dtype,
+        hipLaunchKernelGGL(sorted_distinct_kernel<T>, dim3(grid), dim3(SD_T), 0, s, *col, d_out);
+        hipLaunchKernelGGL(sorted_distinct_final_kernel<T>, dim3(1), dim3(1), 0, s, *col, d_out));
+    return check_launch("sorted_distinct_kernel");
 }
 
 extern "C" int sdp_column_keys(const sdp_column *col, uint64_t *d_out, uint64_t *d_out_n, void *stream) {

@@ -1055,86 +1055,9 @@ __device__ __forceinline__ uint32_t wave_insert_regs(uint64_t *T, uint64_t (&hq)
     return fresh;
 }
 
-// The same inserts with WV_M probes in flight per lane: the lane's WV_Q
-// records form WV_M static sub-queues of WV_Q / WV_M, each with its own
-// current record, and every step issues one table access per live sub-queue
-// before waiting on any of them.  The wave's LDS round trips per batch drop
-// from ~(sum of probes of the lane's records) to ~(that / WV_M) + the tail,
-// which is what bounds this latency-bound kernel (2 waves per SIMD: 16 KB of
-// table per wave).  Sub-queues advance by shifting 5 registers, never by a
-// dynamic register index (which would spill the queue to scratch).
-constexpr int WV_M = 4;
-constexpr int WV_S = WV_Q / WV_M;
-static_assert(WV_Q % WV_M == 0, "sub-queues must split the batch evenly");
-
-template <bool LIMIT, bool DIRECT>
-__device__ __forceinline__ uint32_t wave_insert_mlp(uint64_t *T, uint64_t (&hq)[WV_Q], int64_t rb, int64_t hi,
-                                                    int lane, bool &full) {
-    const int64_t rem = hi - rb - lane;
-    const int left = rem <= 0 ? 0 : (int)min((int64_t)WV_Q, (rem + WAVE - 1) / WAVE);
-    uint64_t x[WV_M];
-    uint32_t pos[WV_M];
-    int cnt[WV_M], probes[WV_M];
-    uint32_t fresh = 0;
-#pragma unroll
-    for (int j = 0; j < WV_M; ++j) {
-        // record q of the lane's batch is valid for q < left; sub-queue j holds q = j*WV_S ..
-        cnt[j] = min(max(left - j * WV_S, 0), WV_S);
-        x[j] = hq[j * WV_S];
-        pos[j] = (uint32_t)x[j] & (WV_SLOTS - 1);
-        probes[j] = 0;
-    }
-    auto advance = [&](int j) {
-        // next record of sub-queue j into slot j (static shifts of WV_S registers)
-#pragma unroll
-        for (int k = 0; k < WV_S - 1; ++k) hq[j * WV_S + k] = hq[j * WV_S + k + 1];
-        --cnt[j];
-        x[j] = hq[j * WV_S];
-        pos[j] = (uint32_t)x[j] & (WV_SLOTS - 1);
-        probes[j] = 0;
-    };
-    while (true) {
-        bool any = false;
-#pragma unroll
-        for (int j = 0; j < WV_M; ++j) any |= cnt[j] > 0;
-        if (!any) break;
-        uint64_t cur[WV_M];
-        if (DIRECT) {
-#pragma unroll
-            for (int j = 0; j < WV_M; ++j)
-                cur[j] = cnt[j] > 0 ? atomicCAS((unsigned long long *)&T[pos[j]], (unsigned long long)EMPTY64,
-                                                (unsigned long long)x[j])
-                                    : x[j];
-        } else {
-#pragma unroll
-            for (int j = 0; j < WV_M; ++j) cur[j] = cnt[j] > 0 ? T[pos[j]] : x[j];
-#pragma unroll
-            for (int j = 0; j < WV_M; ++j)
-                if (cnt[j] > 0 && cur[j] == EMPTY64)
-                    cur[j] = atomicCAS((unsigned long long *)&T[pos[j]], (unsigned long long)EMPTY64,
-                                       (unsigned long long)x[j]);
-        }
-#pragma unroll
-        for (int j = 0; j < WV_M; ++j) {
-            if (cnt[j] <= 0) continue;
-            if (cur[j] == EMPTY64 || cur[j] == x[j]) {
-                fresh += cur[j] == EMPTY64;
-                advance(j);
-            } else {
-                pos[j] = (pos[j] + 1) & (WV_SLOTS - 1);
-                if (LIMIT && ++probes[j] >= WV_SLOTS / 2) {
-                    full = true;
-                    advance(j);
-                }
-            }
-        }
-    }
-    return fresh;
-}
-
 // The first batch of the wave's next bucket is loaded before the current bucket
 // is inserted, so its memory latency overlaps the LDS probing.
-template <bool DIRECT, bool MLP>
+template <bool DIRECT>
 __global__ void __launch_bounds__(WV_W * WAVE) part_dedup_u64_wave_kernel(const uint64_t *in_h,
                                                                           const uint64_t *starts,
                                                                           int64_t nbuckets, uint64_t *stats) {
@@ -1168,13 +1091,11 @@ __global__ void __launch_bounds__(WV_W * WAVE) part_dedup_u64_wave_kernel(const 
             __builtin_amdgcn_wave_barrier();
             uint32_t fresh = 0;
             if (hi - lo <= WV_BATCH) {
-                fresh = MLP ? wave_insert_mlp<false, DIRECT>(T, cur, lo, hi, lane, full)
-                            : wave_insert_regs<false, DIRECT>(T, cur, lo, hi, lane, full);
+                fresh = wave_insert_regs<false, DIRECT>(T, cur, lo, hi, lane, full);
             } else {
                 for (int64_t rb = lo; rb < hi; rb += WV_BATCH) {
                     if (rb != lo) wave_load_batch(cur, in_h, rb, hi, lane);
-                    fresh += MLP ? wave_insert_mlp<true, DIRECT>(T, cur, rb, hi, lane, full)
-                                 : wave_insert_regs<true, DIRECT>(T, cur, rb, hi, lane, full);
+                    fresh += wave_insert_regs<true, DIRECT>(T, cur, rb, hi, lane, full);
                 }
             }
             groups += fresh;
@@ -1669,24 +1590,12 @@ int sdp_part_dedup(const sdp_records *in, int32_t is_bytes, const sdp_bytes_colu
                            nullptr, nullptr, nullptr, d_stats);
     } else {
         const int wgrid = grid_of((nbuckets + WV_W - 1) / WV_W, 256 * 16);
-        // SDP_DEDUP_MLP=0: one probe in flight per lane (the round-2 kernel, for A/B runs)
-        const char *e = getenv("SDP_DEDUP_MLP");
-        const bool mlp = !(e && e[0] == '0');
-        if (with_counts & 4) {          // near-unique keys: claim with one CAS, no read first
-            if (mlp)
-                hipLaunchKernelGGL((part_dedup_u64_wave_kernel<true, true>), dim3(wgrid), dim3(WV_W * WAVE), 0, s,
-                                   in->d_k0, d_starts, nbuckets, d_stats);
-            else
-                hipLaunchKernelGGL((part_dedup_u64_wave_kernel<true, false>), dim3(wgrid), dim3(WV_W * WAVE), 0, s,
-                                   in->d_k0, d_starts, nbuckets, d_stats);
-        } else {
-            if (mlp)
-                hipLaunchKernelGGL((part_dedup_u64_wave_kernel<false, true>), dim3(wgrid), dim3(WV_W * WAVE), 0, s,
-                                   in->d_k0, d_starts, nbuckets, d_stats);
-            else
-                hipLaunchKernelGGL((part_dedup_u64_wave_kernel<false, false>), dim3(wgrid), dim3(WV_W * WAVE), 0, s,
-                                   in->d_k0, d_starts, nbuckets, d_stats);
-        }
+        if (with_counts & 4)            // near-unique keys: claim with one CAS, no read first
+            hipLaunchKernelGGL(part_dedup_u64_wave_kernel<true>, dim3(wgrid), dim3(WV_W * WAVE), 0, s, in->d_k0,
+                               d_starts, nbuckets, d_stats);
+        else
+            hipLaunchKernelGGL(part_dedup_u64_wave_kernel<false>, dim3(wgrid), dim3(WV_W * WAVE), 0, s, in->d_k0,
+                               d_starts, nbuckets, d_stats);
     }
     return check_launch("part_dedup");
 }

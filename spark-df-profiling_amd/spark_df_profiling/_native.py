@@ -133,6 +133,7 @@ _SIGNATURES = {
     'sdp_select_step': (ctypes.c_int, [_P, _P, _I64, _I32, _I32, _P, _I64, _P, _P, _P]),
     'sdp_column_keys': (ctypes.c_int, [_COL, _P, _P, _P]),
     'sdp_column_keys_range': (ctypes.c_int, [_COL, _U64, _U64, _P, _P, _P]),
+    'sdp_sorted_distinct': (ctypes.c_int, [_COL, _P, _P]),
     'sdp_select_batch': (ctypes.c_int, [_P, _I32, _I32, _P, _P]),
     'sdp_select_batch_init': (ctypes.c_int, [_P, _I32, _P, _P]),
     'sdp_select_batch_step': (ctypes.c_int, [_P, _I32, _I32, _I32, _P, _P]),

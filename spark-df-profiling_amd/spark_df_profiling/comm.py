@@ -50,11 +50,25 @@ class LocalComm:
         assert len(send_counts) == 1 and list(send_counts) == list(recv_counts)
         return send
 
+    def alltoallv_known_async(self, send, send_counts, recv_counts):
+        return self.alltoallv_known(send, send_counts, recv_counts), _DONE
+
+    def alltoall_counts(self, rows):
+        return [list(r) for r in rows]
+
     def allgather_object(self, obj):
         return [obj]
 
     def barrier(self):
         pass
+
+
+class _Done:
+    def wait(self):
+        pass
+
+
+_DONE = _Done()
 
 
 class TorchComm:
@@ -140,6 +154,33 @@ class TorchComm:
         self.dist.all_to_all_single(out, x, output_split_sizes=list(recv_counts),
                                     input_split_sizes=list(send_counts), group=self.group)
         return out.to(dev)
+
+    def alltoallv_known_async(self, send, send_counts, recv_counts):
+        """Start alltoallv_known: returns (out, work); `out` holds the result
+        after work.wait().  RCCL: the collective runs on its own stream and
+        wait() only orders the current stream after it (no host wait), so the
+        caller can queue independent kernels meanwhile; `send` must stay
+        referenced until then.  gloo: done at once."""
+        if self.cpu:
+            return self.alltoallv_known(send, send_counts, recv_counts), _DONE
+        self.calls['alltoallv_known'] += 1
+        out = torch.empty(sum(recv_counts), dtype=send.dtype, device=send.device)
+        work = self.dist.all_to_all_single(out, send.contiguous(), output_split_sizes=list(recv_counts),
+                                           input_split_sizes=list(send_counts), group=self.group, async_op=True)
+        return out, work
+
+    def alltoall_counts(self, rows):
+        """rows: k lists of `world` ints (row j, entry r = what this rank sends
+        rank r) -> k lists of `world` ints (entry r = what rank r sends this
+        rank): every count of an exchange in ONE all-to-all and one readback."""
+        self.calls['alltoall_counts'] += 1
+        k = len(rows)
+        dev = torch.device('cpu') if self.cpu else torch.device('cuda', torch.cuda.current_device())
+        send = torch.tensor(rows, dtype=torch.int64).t().contiguous().to(dev)     # [world, k]
+        recv = torch.empty_like(send)
+        self.dist.all_to_all_single(recv, send, group=self.group)
+        r = recv.cpu().tolist()
+        return [[r[src][j] for src in range(self.world)] for j in range(k)]
 
     def allgather_object(self, obj):
         self.calls['allgather_object'] += 1

@@ -349,9 +349,11 @@ def describe(df, bins=10, corr_reject=0.9, **kwargs):
         bounds = [(p1['imin'], p1['imax']) if p1['count'] else None for p1 in p1s]
         # columns whose countDistinct partitions by hash: pass 2 also counts
         # their level-1 buckets (one column read fewer)
+        # (a column found sorted in pass 1 already has its count: sdp_sorted_distinct)
+        known = [p1.get('sorted_distinct') for p1 in p1s]
         paths = engine.distinct_paths_sharded(num_cols, hints, bounds, n) if sharded else \
             engine.distinct_paths(num_cols, hints, bounds)
-        group_cols = {i for i, pth in enumerate(paths) if pth == 'group'}
+        group_cols = {i for i, pth in enumerate(paths) if pth == 'group' and known[i] is None}
         stats = engine.numeric_stats_batch(num_cols, packs, bins, [k_vals.get(c.name, 2) for c in num_cols],
                                            group_cols=group_cols, gk=gk)
         for col, pack, st in zip(num_cols, packs, stats):
@@ -364,8 +366,8 @@ def describe(df, bins=10, corr_reject=0.9, **kwargs):
                     early_plots[col.name] = _submit_plot(st)
         # every NUM column's countDistinct with shared readbacks (and, sharded,
         # shared collectives)
-        dist = engine.distinct_batch(num_cols, hints, bounds) if not sharded else \
-            engine.distinct_batch_sharded(num_cols, hints, bounds)
+        dist = engine.distinct_batch(num_cols, hints, bounds, known) if not sharded else \
+            engine.distinct_batch_sharded(num_cols, hints, bounds, known)
         for col, d in zip(num_cols, dist):
             bundles[col.name]['distinct_pre'] = d
         # every string/binary/decimal column's value counts with shared

@@ -54,13 +54,15 @@ def exchange_fixed_groups(engine, tab, with_counts):
     world = comm.world
     keys, cnt = _table_groups(engine, tab)
     owner = _owner_u64(keys, world)
-    order = torch.argsort(owner, stable=True)
+    order = _owner_order(owner, world)
     keys = keys[order]
-    send = torch.bincount(owner, minlength=world).tolist()
-    rkeys = comm.alltoallv(keys.contiguous(), send)
+    per = torch.zeros(world, dtype=torch.int64, device=engine.device).scatter_add_(0, owner, torch.ones_like(owner))
+    send = per.tolist()
+    recv = comm.alltoall_counts([send])[0]
+    rkeys = comm.alltoallv_known(keys.contiguous(), send, recv)
     rcnt = None
     if with_counts:
-        rcnt = comm.alltoallv(cnt[order].contiguous(), send)
+        rcnt = comm.alltoallv_known(cnt[order].contiguous(), send, recv)
     # owner table over the received keys (they are already order-preserving
     # u64 keys: a U64 column hashes them unchanged)
     from .columns import DeviceColumn
@@ -79,16 +81,32 @@ def exchange_fixed_groups(engine, tab, with_counts):
     return local
 
 
+def _owner_order(owner, world):
+    """Stable order of the groups by owner rank: a radix sort of 1- or 2-byte
+    keys (one or two passes) instead of an int64 argsort."""
+    key = owner.to(torch.uint8 if world <= 256 else torch.int16)
+    return torch.sort(key, stable=True)[1]
+
+
 def exchange_bytes_groups(engine, tab):
+    """Re-partition a rank's byte-key groups by key hash: each group's
+    (length, count) and its key bytes go to the owner rank, which re-aggregates
+    them in a global table.  Host round trips: one readback of the per-owner
+    group and byte counts, one all-to-all of every count of the exchange, the
+    owner table's statistics, one all-reduce of the totals."""
     comm = engine.comm
     world = comm.world
     col = tab['col']
-    slots, cnt = _table_groups(engine, tab)
+    if tab.get('dense'):
+        # partitioned groups are already packed: every entry is a group
+        m = int(tab['groups_local'])
+        slots, cnt = tab['slots'][:m], tab['counts'][:m]
+    else:
+        slots, cnt = _table_groups(engine, tab)
     rows = (slots & MASK40) - 1
     owner = ((slots >> 40) & 0xFFFFFF) % world
-    order = torch.argsort(owner, stable=True)
+    order = _owner_order(owner, world)
     rows, cnt, owner = rows[order], cnt[order], owner[order]
-    send = torch.bincount(owner, minlength=world).tolist()
     if col.fixed_width:
         starts = rows * col.fixed_width
         lens = torch.full_like(rows, col.fixed_width)
@@ -96,21 +114,25 @@ def exchange_bytes_groups(engine, tab):
         o = col.offsets.to(torch.int64)
         starts = o[rows]
         lens = o[rows + 1] - starts
+    # groups and key bytes per owner, summed on the device and read back once
+    # (a host list of every group's length would cost seconds at 1e8 labels)
+    per = torch.zeros((2, world), dtype=torch.int64, device=engine.device)
+    per[0].scatter_add_(0, owner, torch.ones_like(owner))
+    per[1].scatter_add_(0, owner, lens)
+    send_groups, send_bytes = per.tolist()
+    tot = sum(send_bytes)
     # key bytes of every group, owner-major, packed by one native gather
-    # (no per-byte index array: C4's 5e8 labels would need 8 B per key byte)
     offs = torch.cumsum(lens, 0) - lens
-    tot = int((offs[-1] + lens[-1]).item()) if lens.numel() else 0
     payload = torch.empty(max(tot, 1), dtype=torch.uint8, device=engine.device)[:tot]
     if tot:
-        starts = starts.contiguous()
-        sdp.sdp_gather_bytes(ptr(col.data), ptr(starts), ptr(lens.contiguous()), ptr(offs), lens.numel(),
+        sdp.sdp_gather_bytes(ptr(col.data), ptr(starts.contiguous()), ptr(lens.contiguous()), ptr(offs), lens.numel(),
                              ptr(payload), engine._s())
-    # bytes per owner summed on the device (a host list of every group's
-    # length would cost seconds at tens of millions of groups)
-    byte_send = torch.zeros(world, dtype=torch.int64, device=engine.device).scatter_add_(0, owner, lens).tolist()
-    rlens = comm.alltoallv(lens.contiguous(), send)
-    rcnt = comm.alltoallv(cnt.contiguous(), send)
-    rbytes = comm.alltoallv(payload.contiguous(), byte_send)
+    recv_groups, recv_bytes = comm.alltoall_counts([send_groups, send_bytes])
+    # (length, count) pairs in one exchange, the key bytes in a second
+    meta = torch.stack([lens, cnt], 1).contiguous().view(-1)
+    rmeta = comm.alltoallv_known(meta, [2 * g for g in send_groups], [2 * g for g in recv_groups]).view(-1, 2)
+    rbytes = comm.alltoallv_known(payload.contiguous(), send_bytes, recv_bytes)
+    rlens, rcnt = rmeta[:, 0].contiguous(), rmeta[:, 1].contiguous()
     from .columns import DeviceColumn
     n = int(rlens.numel())
     rc = DeviceColumn('_exchange', col.spark_type, n, 'bytes', decimal_scale=col.decimal_scale)

@@ -858,6 +858,11 @@ class Engine:
         isf = self._h2d(np.array([int(c.is_float) for c in cols], dtype=np.int32))
         psz = ctypes.sizeof(nat.SdpQPlan)
         plans_dev = self._bytes(len(cols) * psz)
+        # columns whose sampled keys (evenly spaced rows, in row order: pooled
+        # over the ranks in rank order) never decrease may be sorted (ids,
+        # timestamps): their countDistinct is verified by one streaming pass
+        # (sdp_sorted_distinct) instead of the partitioning pipeline
+        mono = self._sample_nondecreasing(samples.view(len(cols), ns * world))
         sdp.sdp_quantile_plan_batch(ptr(samples), ns * world, len(cols), ptr(pr), len(probs), ptr(isf),
                                     ptr(plans_dev), s)
         # narrower windows from a second, 8x larger sample (pooled across ranks
@@ -901,9 +906,11 @@ class Engine:
             if sharded:
                 hs = torch.cat([p.view(len(hcols), nsr) for p in self.comm.allgather(hs)], dim=1).contiguous()
             sdp.sdp_sort_small_batch(ptr(hs), hn_each, len(hcols), s)
-            raw = torch.cat([plans_dev, hs.view(-1).view(torch.uint8)]).cpu().numpy()
+            raw = torch.cat([plans_dev, hs.view(-1).view(torch.uint8), mono]).cpu().numpy()
         else:
-            raw = plans_dev.cpu().numpy()
+            raw = torch.cat([plans_dev, mono]).cpu().numpy()
+        mono_h = raw[-len(cols):].astype(bool)
+        raw = raw[:-len(cols)]
         plans = [nat.SdpQPlan.from_buffer_copy(raw[i * psz:(i + 1) * psz].tobytes()) for i in range(len(cols))]
         if DEBUG_QUANTILE == 'miss':
             for i, p in enumerate(plans):
@@ -917,6 +924,14 @@ class Engine:
         budget = [CAND_FULL_BUDGET]
         for i, col in enumerate(cols):
             infos.append(self._pass1_launch(col, plans_dev[i * psz:], plans[i], res_all[i * rsz:], budget))
+        # (sharded: the flag comes from the pooled sample, the same on every rank)
+        sorted_idx = [i for i, c in enumerate(cols)
+                      if mono_h[i] and c.kind == 'fixed' and (sharded or c.length >= SORTED_MIN_ROWS)]
+        sd = self._u64(4 * max(1, len(sorted_idx)))
+        for j, i in enumerate(sorted_idx):
+            cs = cols[i].sdp()
+            nat.annotate(_label(cols[i], 'sorted'), col_read_bytes(cols[i]))
+            sdp.sdp_sorted_distinct(ctypes.byref(cs), ptr(sd[4 * j:]), s)
         if hcols:
             if self._heavy_pre is None:
                 self._heavy_pre = {}
@@ -933,15 +948,29 @@ class Engine:
                 self._heavy_pre[id(col)] = self._heavy_struct(a[start], cnt)
                 if start.size >= 0.9 * a.size:
                     self._near_unique.add(id(col))
+        both = torch.cat([res_all, sd.view(torch.uint8)])      # pass-1 results + sorted checks: one readback
         if not sharded:
-            raw = res_all.cpu().numpy().tobytes()
-            merged = [merge_pass1_results([nat.SdpPass1Result.from_buffer_copy(raw[i * rsz:(i + 1) * rsz])])
-                      for i in range(len(cols))]
+            raws = [both.cpu().numpy().tobytes()]
         else:
-            ranks = [g.cpu().numpy().tobytes() for g in self.comm.allgather(res_all)]
-            merged = [merge_pass1_results([nat.SdpPass1Result.from_buffer_copy(r[i * rsz:(i + 1) * rsz])
-                                           for r in ranks]) for i in range(len(cols))]
+            raws = [g.cpu().numpy().tobytes() for g in self.comm.allgather(both)]
+        merged = [merge_pass1_results([nat.SdpPass1Result.from_buffer_copy(r[i * rsz:(i + 1) * rsz]) for r in raws])
+                  for i in range(len(cols))]
+        off = len(cols) * rsz
+        for j, i in enumerate(sorted_idx):
+            parts = [np.frombuffer(r[off + 32 * j: off + 32 * j + 32], dtype=np.uint64) for r in raws]
+            merged[i]['sorted_distinct'] = merge_sorted_distinct(parts)
         return [(merged[i], plans[i], infos[i]) for i in range(len(cols))]
+
+    @staticmethod
+    def _sample_nondecreasing(samp):
+        """[cols, m] sampled keys in row order (UINT64_MAX = null/NaN row) ->
+        uint8 [cols]: 1 where the valid keys never decrease (at least 2)."""
+        valid = samp != -1
+        x = samp ^ (-(1 << 63))                      # unsigned key order as signed order
+        x = torch.where(valid, x, torch.full_like(x, -(1 << 63)))
+        run = torch.cummax(x, dim=1).values
+        down = (valid & (x < run)).any(dim=1)
+        return (~down & (valid.sum(dim=1) >= 2)).to(torch.uint8)
 
     def minmax_pass(self, col):
         """count / min / max of a date or timestamp column (describe.py:233)."""
@@ -1309,17 +1338,17 @@ class Engine:
                 out.append('table')
         return out
 
-    def distinct_batch(self, cols, hints, bounds):
+    def distinct_batch(self, cols, hints, bounds, known=None):
         """countDistinct of several NUM/DATE columns (describe.py:143) with
         the path choice of describe._distinct_count / distinct_fixed per column
         and the host readbacks shared: LDS bitmaps for small integral ranges
         (one readback for all), hash partitioning for the rest (group_batch).
         `bounds[i]` = (imin, imax) for integral columns with values, else None.
         Single rank only; returns [distinct count]."""
-        out = [None] * len(cols)
+        out = list(known) if known is not None else [None] * len(cols)     # sorted columns: counted
         paths = self.distinct_paths(cols, hints, bounds)
-        bm = [i for i, pth in enumerate(paths) if pth == 'bitmap']
-        grp = [i for i, pth in enumerate(paths) if pth == 'group']
+        bm = [i for i, pth in enumerate(paths) if pth == 'bitmap' and out[i] is None]
+        grp = [i for i, pth in enumerate(paths) if pth == 'group' and out[i] is None]
         if bm:
             outs = [self._distinct_bitmap_launch(cols[i], bounds[i][0], bounds[i][1] - bounds[i][0] + 1) for i in bm]
             for i, v in zip(bm, self._host_u64(torch.cat(outs))):
@@ -1383,6 +1412,59 @@ class Engine:
         all_sizes = torch.stack(comm.allgather(sizes)).cpu().numpy().reshape(world, len(ctxs), nb1)
         my0, my1 = lo[rank], lo[rank + 1]
         nmy = my1 - my0
+
+        def owner_stage(ci, ctx, recv, S, part_tot):
+            """Level 2 + LDS de-duplication of the records this rank owns."""
+            col, stats = ctx['col'], ctx['stats']
+            nrecv = int(recv.numel())
+            if not nrecv:
+                return
+            # received layout: source-rank-major, my buckets in order inside each
+            # part; chunks of <= PART_CHUNK records, ordered (bucket, source, chunk)
+            part_base = np.concatenate([[0], np.cumsum(part_tot)[:-1]]).astype(np.int64)
+            st0 = part_base[:, None] + np.concatenate([np.zeros((world, 1), np.int64),
+                                                      np.cumsum(S, axis=1)[:, :-1]], axis=1)
+            cnt = -(-S // PART_CHUNK)                                   # chunks per (source, bucket)
+            cb, csrc = cnt.T.reshape(-1), np.tile(np.arange(world), nmy)
+            bi_of = np.repeat(np.arange(nmy), world)
+            rep_b, rep_src = np.repeat(bi_of, cb), np.repeat(csrc, cb)
+            first = np.concatenate([[0], np.cumsum(cb)[:-1]])
+            jj = np.arange(int(cb.sum()), dtype=np.int64) - np.repeat(first, cb)
+            seg_start = st0[rep_src, rep_b] + jj * PART_CHUNK
+            seg_end = np.minimum(st0[rep_src, rep_b] + S[rep_src, rep_b], seg_start + PART_CHUNK)
+            nch = np.bincount(rep_b, minlength=nmy).astype(np.int64)
+            k0 = np.concatenate([[0], np.cumsum(nch)[:-1]]).astype(np.int64)
+            K = int(nch.sum())
+            j = np.arange(K, dtype=np.int64) - k0[rep_b]
+            ch = np.empty((K, 4), dtype=np.int64)
+            ch[:, 0], ch[:, 1] = seg_start, seg_end
+            ch[:, 2] = nb2 * k0[rep_b] + j
+            ch[:, 3] = nch[rep_b]
+            chunks = self._h2d(ch)
+            rin = nat.SdpRecords(recv.data_ptr(), None, None)
+            h2 = torch.empty(nb2 * K, dtype=torch.int32, device=self.device)
+            nat.annotate('u64/count', nrecv * 8)
+            sdp.sdp_part_recs(ctypes.byref(rin), 0, ptr(chunks), K, B1, b2, 0, ptr(h2), None, None, s)
+            o2 = self._scan(h2)
+            rf, keepf = self._records(nrecv, False)
+            nat.annotate('u64/scatter', 2 * nrecv * 8)
+            sdp.sdp_part_recs(ctypes.byref(rin), 0, ptr(chunks), K, B1, b2, 1, None, ptr(o2),
+                              ctypes.byref(rf), s)
+            del h2
+            sidx = (nb2 * k0[:, None] + np.arange(nb2)[None, :] * nch[:, None]).reshape(-1)
+            sidx = np.append(sidx, nb2 * K)
+            starts = o2[self._h2d(sidx)].contiguous()
+            ngroups = torch.zeros(nmy * nb2, dtype=torch.int32, device=self.device)
+            nat.annotate('u64', nrecv * 8)
+            sdp.sdp_part_dedup(ctypes.byref(rf), 0, None, ptr(starts), nmy * nb2,
+                               4 if id(col) in self._near_unique else 0, None, None, ptr(ngroups),
+                               ptr(stats), s)
+            del keepf, rf
+
+        # pipelined: column i's all-to-all runs on the collective stream while
+        # column i-1's owner stage runs on the compute stream (every rank
+        # issues the exchanges in column order)
+        pending = None
         for ci, (ctx, bs) in enumerate(zip(ctxs, bss)):
             col, stats = ctx['col'], ctx['stats']
             nrec = int(bs[-1])
@@ -1395,51 +1477,20 @@ class Engine:
             send = [int(bs[lo[r + 1]] - bs[lo[r]]) for r in range(world)]
             S = all_sizes[:, ci, my0:my1]                                   # [world, nmy]
             part_tot = S.sum(axis=1)
-            recv = comm.alltoallv_known(keep1[0][:nrec], send, [int(x) for x in part_tot])
+            recv, work = comm.alltoallv_known_async(keep1[0][:nrec], send, [int(x) for x in part_tot])
+            if pending is not None:
+                p_ci, p_ctx, p_recv, p_work, p_S, p_tot, p_keep = pending
+                p_work.wait()
+                del p_keep                     # the send buffer outlives its collective
+                owner_stage(p_ci, p_ctx, p_recv, p_S, p_tot)
+            pending = (ci, ctx, recv, work, S, part_tot, (keep1, r1))
             del keep1, r1
-            nrecv = int(recv.numel())
-            if nrecv:
-                # received layout: source-rank-major, my buckets in order inside each
-                # part; chunks of <= PART_CHUNK records, ordered (bucket, source, chunk)
-                part_base = np.concatenate([[0], np.cumsum(part_tot)[:-1]]).astype(np.int64)
-                st0 = part_base[:, None] + np.concatenate([np.zeros((world, 1), np.int64),
-                                                          np.cumsum(S, axis=1)[:, :-1]], axis=1)
-                cnt = -(-S // PART_CHUNK)                                   # chunks per (source, bucket)
-                cb, csrc = cnt.T.reshape(-1), np.tile(np.arange(world), nmy)
-                bi_of = np.repeat(np.arange(nmy), world)
-                rep_b, rep_src = np.repeat(bi_of, cb), np.repeat(csrc, cb)
-                first = np.concatenate([[0], np.cumsum(cb)[:-1]])
-                jj = np.arange(int(cb.sum()), dtype=np.int64) - np.repeat(first, cb)
-                seg_start = st0[rep_src, rep_b] + jj * PART_CHUNK
-                seg_end = np.minimum(st0[rep_src, rep_b] + S[rep_src, rep_b], seg_start + PART_CHUNK)
-                nch = np.bincount(rep_b, minlength=nmy).astype(np.int64)
-                k0 = np.concatenate([[0], np.cumsum(nch)[:-1]]).astype(np.int64)
-                K = int(nch.sum())
-                j = np.arange(K, dtype=np.int64) - k0[rep_b]
-                ch = np.empty((K, 4), dtype=np.int64)
-                ch[:, 0], ch[:, 1] = seg_start, seg_end
-                ch[:, 2] = nb2 * k0[rep_b] + j
-                ch[:, 3] = nch[rep_b]
-                chunks = self._h2d(ch)
-                rin = nat.SdpRecords(recv.data_ptr(), None, None)
-                h2 = torch.empty(nb2 * K, dtype=torch.int32, device=self.device)
-                nat.annotate('u64/count', nrecv * 8)
-                sdp.sdp_part_recs(ctypes.byref(rin), 0, ptr(chunks), K, B1, b2, 0, ptr(h2), None, None, s)
-                o2 = self._scan(h2)
-                rf, keepf = self._records(nrecv, False)
-                nat.annotate('u64/scatter', 2 * nrecv * 8)
-                sdp.sdp_part_recs(ctypes.byref(rin), 0, ptr(chunks), K, B1, b2, 1, None, ptr(o2),
-                                  ctypes.byref(rf), s)
-                del recv, h2
-                sidx = (nb2 * k0[:, None] + np.arange(nb2)[None, :] * nch[:, None]).reshape(-1)
-                sidx = np.append(sidx, nb2 * K)
-                starts = o2[self._h2d(sidx)].contiguous()
-                ngroups = torch.zeros(nmy * nb2, dtype=torch.int32, device=self.device)
-                nat.annotate('u64', nrecv * 8)
-                sdp.sdp_part_dedup(ctypes.byref(rf), 0, None, ptr(starts), nmy * nb2,
-                                   4 if id(col) in self._near_unique else 0, None, None, ptr(ngroups),
-                                   ptr(stats), s)
-                del keepf, rf
+        if pending is not None:
+            p_ci, p_ctx, p_recv, p_work, p_S, p_tot, p_keep = pending
+            p_work.wait()
+            del p_keep
+            owner_stage(p_ci, p_ctx, p_recv, p_S, p_tot)
+            pending = None
         # every column's group statistics in one all-reduce and one readback
         parts, spans = [], []
         for ctx in ctxs:
@@ -1496,7 +1547,7 @@ class Engine:
                 out.append('group')
         return out
 
-    def distinct_batch_sharded(self, cols, hints, bounds):
+    def distinct_batch_sharded(self, cols, hints, bounds, known=None):
         """distinct_batch on a row-sharded table (every rank calls it with the
         same columns; hints/bounds come from the merged pass 1): bitmaps for
         small integral ranges, the global-table exchange for small key ranges,
@@ -1504,10 +1555,12 @@ class Engine:
         comm = self.comm
         n_all = int(comm.allreduce_sum(torch.tensor([cols[0].length if cols else 0], dtype=torch.int64,
                                                     device=self.device)).item()) if cols else 0
-        out = [None] * len(cols)
+        out = list(known) if known is not None else [None] * len(cols)     # sorted columns: counted
         grp = []
         for i, (col, pth) in enumerate(zip(cols, self.distinct_paths_sharded(cols, hints, bounds, n_all))):
             bd = bounds[i]
+            if out[i] is not None:
+                continue
             if pth == 'bitmap':
                 out[i] = self.distinct_bitmap(col, bd[0], bd[1] - bd[0] + 1)
             elif pth == 'table':
@@ -1936,6 +1989,30 @@ def _merge_special(res, extra, k, tab):
 def _slot_key_for_sort(tab, slot):
     cached = tab.get('_slotval', {}).get(slot)
     return _u(cached) if cached is not None else _u(tab['slots'][slot].item())
+
+
+SORTED_MIN_ROWS = 1 << 16      # single rank: smaller columns group quickly anyway
+
+
+def merge_sorted_distinct(parts):
+    """Rank-order merge of sdp_sorted_distinct outputs [distinct, violation,
+    first key, last key] -> the column's distinct count, or None when it is not
+    sorted (a rank saw a decrease, or a rank's first key is below the last key
+    of the ranks before it).  Equal keys across a rank boundary are one value."""
+    total, last = 0, None
+    for d, viol, first, lastk in (tuple(int(v) for v in p) for p in parts):
+        if viol:
+            return None
+        if d == 0:
+            continue                                   # a rank with no valid rows
+        total += d
+        if last is not None:
+            if first < last:
+                return None
+            if first == last:
+                total -= 1
+        last = lastk
+    return total
 
 
 def merge_pass1_results(parts):

@@ -52,7 +52,7 @@ def pytest_sessionstart(session):
            # rounds, all_to_all_single on device tensors, the owner exchanges)
            'SDP_FORCE_SHARDED=1 SDP_REQUIRE_CALLS=allreduce_sum_,alltoallv_known,allgather,allgather_object ' +
            run.format(t=300, py=sys.executable, np=1, port=_free_port(), w=worker, be='nccl',
-                      only='demo,numeric,numeric_big,categorical,categorical_big,dates,corr,legacy,gk,c3'))
+                      only='demo,numeric,numeric_big,categorical,categorical_big,dates,corr,legacy,sorted,gk,c3'))
     env = dict(os.environ, SDP_PLOT_WORKERS='0', HSA_ENABLE_IPC_MODE_LEGACY='0')
     log = open(MULTIRANK_LOG, 'w')
     _MULTIRANK['proc'] = subprocess.Popen(['bash', '-c', cmd], cwd=ROOT, env=env, stdout=log,

@@ -232,3 +232,34 @@ def c5_table(n, ncols=512, seed=C_SEED + 5, factors=4):
     for j in range(ncols):
         cols['c%03d' % j] = pa.array((F @ L[:, j] + g.standard_normal(n)).astype(np.float32))
     return pa.table(cols)
+
+
+def sorted_table(n, seed=41):
+    """Columns sorted in row order (ids, timestamps, pre-sorted data) and
+    near-misses, for the sorted-column countDistinct path (sdp_sorted_distinct):
+    strictly increasing ids with nulls, non-decreasing values with duplicates,
+    sorted doubles with -0.0/+0.0 and NaN at the end, one swapped pair deep
+    inside, a null run longer than the kernel's walk, a descending column."""
+    g = rng(seed)
+    ids = np.arange(n, dtype=np.int64) * 3 + 7
+    dup = np.sort(g.integers(0, max(2, n // 10), n)).astype(np.int64)
+    f = np.sort(g.standard_normal(n))
+    f[n // 3: n // 3 + 50] = 0.0
+    f[n // 3: n // 3 + 25] = -0.0
+    f[-(n // 100):] = np.nan                              # NaN sorts last (countDistinct: one value)
+    f[(np.arange(n) > n // 3 + 50) & (np.arange(n) < n // 3 + 60)] = f[n // 3 + 60]   # a small tie run
+    almost = np.arange(n, dtype=np.int64)
+    almost[n // 2], almost[n // 2 + 1] = almost[n // 2 + 1], almost[n // 2]
+    runs = np.arange(n, dtype=np.float64)
+    rmask = np.zeros(n, dtype=bool)
+    rmask[n // 4: n // 4 + 1000] = True                   # a null run longer than the walk (256)
+    return pa.table({
+        'ids': pa.array(ids, mask=_mask(g, n, 0.05)),
+        'dup': pa.array(dup, mask=_mask(g, n, 0.03)),
+        'fsort': pa.array(f, mask=_mask(g, n, 0.02)),
+        'f32sort': pa.array(np.sort(g.random(n)).astype(np.float32)),
+        'almost': pa.array(almost),
+        'nullrun': pa.array(runs, mask=rmask),
+        'desc': pa.array(np.arange(n, dtype=np.int64)[::-1].copy()),
+        'num': pa.array(g.standard_normal(n)),
+    })

@@ -88,6 +88,8 @@ def main():
         'dates': datagen.date_table(20_000),
         'corr': datagen.corr_table(20_000),
         'legacy': datagen.legacy_table(),
+        # sorted columns across rank boundaries (equal keys on both sides of a boundary)
+        'sorted': datagen.sorted_table(200_003),
     }
     if 'c3' in (sys.argv[2].split(',') if len(sys.argv) > 2 else []):
         import bench

@@ -24,6 +24,6 @@ def test_two_rank_sharded_describe():
     assert rc == 0, log[-6000:]
     runs = [l for l in log.splitlines() if l.startswith('MULTIRANK ')]
     assert runs == ['MULTIRANK OK failures=0'] * 3, log[-6000:]
-    assert log.count('OK world=2') >= 10, log[-6000:]
-    assert log.count('OK world=1') >= 10, log[-6000:]          # 9 tables + gk on the forced-sharded nccl rank
+    assert log.count('OK world=2') >= 11, log[-6000:]
+    assert log.count('OK world=1') >= 11, log[-6000:]          # 10 tables + gk on the forced-sharded nccl rank
     assert '[calls] backend=nccl sharded=True' in log, log[-6000:]

@@ -143,3 +143,32 @@ def test_spark_to_arrow_duck_types():
     got = spark_to_arrow(S2())
     assert got.column('s').to_pylist() == ['x', None, 'z']
     assert got.column('a').to_pylist()[:2] == [1.0, 2.0]
+
+
+def test_sample_nondecreasing_flags():
+    import torch
+    from spark_df_profiling.engine import Engine
+    E = -1                                            # UINT64_MAX: a null / NaN sample row
+    big = (1 << 63) + 5                               # keys above 2^63 (positive floats' keys)
+    rows = [[1, 2, 2, E, 3, 9],                       # non-decreasing with a null
+            [1, 3, 2, 4, 5, 6],                       # one decrease
+            [E, E, 7, E, E, E],                       # one valid key: not a candidate
+            [5, big - (1 << 64), E, big + 1 - (1 << 64), E, E],   # across the sign bit, unsigned order
+            [big - (1 << 64), 5, 6, 7, 8, 9]]         # big key first: decreasing in unsigned order
+    t = torch.tensor(rows, dtype=torch.int64)
+    assert Engine._sample_nondecreasing(t).tolist() == [1, 0, 0, 1, 0]
+
+
+def test_merge_sorted_distinct_rank_order():
+    import numpy as np
+    from spark_df_profiling.engine import merge_sorted_distinct
+    E = np.uint64(2 ** 64 - 1)
+    p = lambda d, v, f, l: np.array([d, v, f, l], dtype=np.uint64)
+    assert merge_sorted_distinct([p(5, 0, 10, 20)]) == 5
+    # rank boundary with an equal key: one value, counted once
+    assert merge_sorted_distinct([p(5, 0, 10, 20), p(3, 0, 20, 30)]) == 7
+    assert merge_sorted_distinct([p(5, 0, 10, 20), p(3, 0, 21, 30)]) == 8
+    # an empty rank in between is skipped; a decrease across ranks is not sorted
+    assert merge_sorted_distinct([p(5, 0, 10, 20), p(0, 0, E, E), p(1, 0, 20, 20)]) == 5
+    assert merge_sorted_distinct([p(5, 0, 10, 20), p(3, 0, 19, 30)]) is None
+    assert merge_sorted_distinct([p(5, 1, 10, 20)]) is None
