@@ -127,6 +127,11 @@ int64_t sdp_pass2_workspace_bytes(int64_t length, int32_t dtype, int32_t bins);
 int sdp_sample_keys(const sdp_column *col, int32_t n_sample, uint64_t *d_sample,
                     void *stream);
 
+/* sdp_sample_keys of n_cols columns in one launch: d_cols is a DEVICE array of
+ * column structs (any numeric dtypes); column c's sample at d_sample + c * n_sample. */
+int sdp_sample_keys_batch(const sdp_column *d_cols, int32_t n_cols, int32_t n_sample,
+                          uint64_t *d_sample, void *stream);
+
 /* Sort a key sample (<= 16384 keys) and choose one value window per target
  * probability around its sample rank, merged where windows overlap.  Replaces
  * the five `percentile`/`percentile_approx` jobs of describe.py:203-208 (the

@@ -81,6 +81,38 @@ __global__ void sample_keys_kernel(sdp_column col, int32_t ns, uint64_t *out) {
     out[j] = k;
 }
 
+// every column's sample in one launch (blockIdx.y = column; the dtype is read
+// per column, so the tables may mix dtypes): column c's keys at out + c * ns
+template <typename T>
+__device__ __forceinline__ uint64_t sample_key_at(const sdp_column &col, int64_t i) {
+    const T x = ((const T *)col.d_values)[i];
+    const double xd = Elem<T>::d(x);
+    return xd == xd ? Elem<T>::key(x) : EMPTY64;
+}
+__global__ void sample_keys_batch_kernel(const sdp_column *cols, int32_t ns, uint64_t *out) {
+    const int j = blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= ns) return;
+    const sdp_column col = cols[blockIdx.y];
+    const int64_t n = col.length;
+    const int64_t i = (int64_t)(((double)j + 0.5) * (double)n / (double)ns);
+    uint64_t k = EMPTY64;
+    if (i < n && valid_bit(col.d_validity, col.validity_bit_offset, i)) {
+        switch (col.dtype) {
+        case SDP_I8: k = sample_key_at<int8_t>(col, i); break;
+        case SDP_I16: k = sample_key_at<int16_t>(col, i); break;
+        case SDP_I32: k = sample_key_at<int32_t>(col, i); break;
+        case SDP_I64: k = sample_key_at<int64_t>(col, i); break;
+        case SDP_U8: k = sample_key_at<uint8_t>(col, i); break;
+        case SDP_U16: k = sample_key_at<uint16_t>(col, i); break;
+        case SDP_U32: k = sample_key_at<uint32_t>(col, i); break;
+        case SDP_F32: k = sample_key_at<float>(col, i); break;
+        case SDP_F64: k = sample_key_at<double>(col, i); break;
+        default: break;
+        }
+    }
+    out[(int64_t)blockIdx.y * ns + j] = k;
+}
+
 // LDS bitonic sort of `n` keys (n <= SORT_MAX); pads with EMPTY64.
 __device__ void block_sort_keys(uint64_t *s, int n) {
     int P = 2;
@@ -1494,6 +1526,15 @@ extern "C" int sdp_sample_keys(const sdp_column *col, int32_t n_sample, uint64_t
     SDP_DISPATCH_NUMERIC(col->dtype,
         hipLaunchKernelGGL(sample_keys_kernel<T>, dim3(blocks), dim3(256), 0, s, *col, n_sample, d_sample));
     return check_launch("sample_keys_kernel");
+}
+
+extern "C" int sdp_sample_keys_batch(const sdp_column *d_cols, int32_t n_cols, int32_t n_sample, uint64_t *d_sample,
+                                     void *stream) {
+    if (d_cols == nullptr || n_cols < 1 || n_cols > 65535 || n_sample < 1 || n_sample > (1 << 22))
+        return set_error(SDP_EINVAL, "sdp_sample_keys_batch: n_cols %d n_sample %d", n_cols, n_sample);
+    hipLaunchKernelGGL(sample_keys_batch_kernel, dim3((n_sample + 255) / 256, n_cols), dim3(256), 0,
+                       (hipStream_t)stream, d_cols, n_sample, d_sample);
+    return check_launch("sample_keys_batch_kernel");
 }
 
 extern "C" int sdp_quantile_plan(uint64_t *d_sample, int32_t n_sample, const double *d_probs, int32_t n_probs,

@@ -116,6 +116,7 @@ _SIGNATURES = {
     'sdp_pass2_workspace_bytes': (_I64, [_I64, _I32, _I32]),
     'sdp_pass1_grid': (_I32, [_I64, _I32]),
     'sdp_sample_keys': (ctypes.c_int, [_COL, _I32, _P, _P]),
+    'sdp_sample_keys_batch': (ctypes.c_int, [_P, _I32, _I32, _P, _P]),
     'sdp_quantile_plan': (ctypes.c_int, [_P, _I32, _P, _I32, _I32, _P, _P]),
     'sdp_quantile_plan_batch': (ctypes.c_int, [_P, _I32, _I32, _P, _I32, _P, _P, _P]),
     'sdp_quantile_refine_batch': (ctypes.c_int, [_P, _I32, _I32, _P, _I32, _P, _P]),

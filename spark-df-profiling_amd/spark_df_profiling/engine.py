@@ -847,10 +847,11 @@ class Engine:
         world, sharded = self.comm.world, self.comm.sharded
         ns = max(1, SAMPLE_TOTAL // world)
         s = self._s()
+        # every column's struct on the device once: the three sample rounds
+        # are one launch each for the whole table
+        d_cols = self._h2d(np.frombuffer(bytearray(b''.join(bytes(c.sdp()) for c in cols)), dtype=np.uint8))
         samples = self._u64(len(cols) * ns)
-        for i, col in enumerate(cols):
-            cs = col.sdp()
-            sdp.sdp_sample_keys(ctypes.byref(cs), ns, ptr(samples[i * ns:]), s)
+        sdp.sdp_sample_keys_batch(ptr(d_cols), len(cols), ns, ptr(samples), s)
         if sharded:
             # [cols, world * ns]: column i's pooled sample in rank order
             samples = torch.cat([p.view(len(cols), ns) for p in self.comm.allgather(samples)], dim=1).contiguous()
@@ -871,18 +872,14 @@ class Engine:
         # (sharded: always, so every rank takes the same collective path)
         if sharded or min(c.length for c in cols) > SAMPLE_TOTAL:
             s2 = self._u64(len(cols) * ns2)
-            for i, col in enumerate(cols):
-                cs = col.sdp()
-                sdp.sdp_sample_keys(ctypes.byref(cs), ns2, ptr(s2[i * ns2:]), s)
+            sdp.sdp_sample_keys_batch(ptr(d_cols), len(cols), ns2, ptr(s2), s)
             if sharded:
                 s2 = torch.cat([p.view(len(cols), ns2) for p in self.comm.allgather(s2)], dim=1).contiguous()
             sdp.sdp_quantile_refine_batch(ptr(s2), ns2 * world, len(cols), ptr(pr), len(probs), ptr(plans_dev), s)
             ns3 = SAMPLE3_TOTAL // world
             if ns3 > ns2 and (sharded or min(c.length for c in cols) > SAMPLE2_TOTAL):
                 s3 = self._u64(len(cols) * ns3)
-                for i, col in enumerate(cols):
-                    cs = col.sdp()
-                    sdp.sdp_sample_keys(ctypes.byref(cs), ns3, ptr(s3[i * ns3:]), s)
+                sdp.sdp_sample_keys_batch(ptr(d_cols), len(cols), ns3, ptr(s3), s)
                 if sharded:
                     s3 = torch.cat([p.view(len(cols), ns3) for p in self.comm.allgather(s3)], dim=1).contiguous()
                 sdp.sdp_quantile_refine_batch(ptr(s3), ns3 * world, len(cols), ptr(pr), len(probs), ptr(plans_dev), s)

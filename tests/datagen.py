@@ -244,10 +244,12 @@ def sorted_table(n, seed=41):
     ids = np.arange(n, dtype=np.int64) * 3 + 7
     dup = np.sort(g.integers(0, max(2, n // 10), n)).astype(np.int64)
     f = np.sort(g.standard_normal(n))
-    f[n // 3: n // 3 + 50] = 0.0
-    f[n // 3: n // 3 + 25] = -0.0
+    z = int(np.searchsorted(f, 0.0))                      # -0.0 then +0.0 where the values cross zero
+    f[z - 25:z] = -0.0
+    f[z:z + 25] = 0.0
+    h = n // 2
+    f[h:h + 10] = f[h + 10]                               # a small tie run
     f[-(n // 100):] = np.nan                              # NaN sorts last (countDistinct: one value)
-    f[(np.arange(n) > n // 3 + 50) & (np.arange(n) < n // 3 + 60)] = f[n // 3 + 60]   # a small tie run
     almost = np.arange(n, dtype=np.int64)
     almost[n // 2], almost[n // 2 + 1] = almost[n // 2 + 1], almost[n // 2]
     runs = np.arange(n, dtype=np.float64)
