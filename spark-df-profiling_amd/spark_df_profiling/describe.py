@@ -133,13 +133,15 @@ def describe_1d(engine: Engine, col: DeviceColumn, nrows, bins, k, freq, bundle)
         if distinct is None:
             distinct = _distinct_count(engine, col, p1, _distinct_hint(p1, spark_t))
     elif spark_t in DATE_TYPES:
-        p1 = engine.minmax_pass(col)
+        p1 = bundle.pop('minmax_pre', None) or engine.minmax_pass(col)
         bundle['minmax'] = p1
         count = p1['count']
-        hint = p1['n_valid']
-        if p1['count']:
-            hint = min(hint, p1['imax'] - p1['imin'] + 1)
-        distinct = _distinct_count(engine, col, p1, hint)
+        distinct = bundle.pop('distinct_pre', None)
+        if distinct is None:
+            hint = p1['n_valid']
+            if p1['count']:
+                hint = min(hint, p1['imax'] - p1['imin'] + 1)
+            distinct = _distinct_count(engine, col, p1, hint)
     elif col.kind == 'fixed':                      # boolean, decimal(20,0) from uint64
         tab = engine.distinct_fixed(col, with_counts=True)
         distinct, count = tab['groups'], tab['rows']
@@ -205,6 +207,11 @@ def _is_numeric(col):
     return col.kind != 'null' and not nested and (st in INT_TYPES or st in ('float', 'double'))
 
 
+def _is_date(col):
+    """describe_date_1d's columns (describe.py:162, :232): fixed-width date/timestamp."""
+    return col.kind == 'fixed' and col.spark_type in DATE_TYPES
+
+
 def _is_byte_keyed(col):
     """describe_1d's string/binary/decimal branch (value counts on byte keys)."""
     st = col.spark_type
@@ -257,7 +264,9 @@ def _date_series(engine, col, p1, distinct, freq):
 def _categorical_series(engine, col, tab, count, bundle):
     """describe_categorical_1d (describe.py:250-271).  Groups ordered by count
     desc then key asc (the reference's orderBy leaves ties unspecified)."""
-    pairs = engine.global_topk(tab, col, TOPK)
+    pairs = bundle.pop('topk_pre', None)
+    if pairs is None:
+        pairs = engine.global_topk(tab, col, TOPK)
     values = [v for v, _ in pairs]
     counts = [int(c) for _, c in pairs]
     bundle['topk'] = pairs
@@ -343,7 +352,12 @@ def describe(df, bins=10, corr_reject=0.9, **kwargs):
         # then every column's order statistics and pass 2 (two more) -- the
         # per-column loop below only counts distincts and assembles
         num_cols = [c for c in table.columns if _is_numeric(c)]
-        packs = engine.numeric_pass1_batch(num_cols)
+        # date / timestamp columns: min/max in the numeric pass-1 launches and readback
+        date_cols = [c for c in table.columns if _is_date(c)]
+        packs, date_p1 = engine.numeric_pass1_batch(num_cols, minmax_cols=date_cols) if date_cols else \
+            (engine.numeric_pass1_batch(num_cols), [])
+        for col, p1 in zip(date_cols, date_p1):
+            bundles[col.name]['minmax_pre'] = p1
         p1s = [pk[0] for pk in packs]
         hints = [_distinct_hint(p1, c.spark_type) for c, p1 in zip(num_cols, p1s)]
         bounds = [(p1['imin'], p1['imax']) if p1['count'] else None for p1 in p1s]
@@ -366,15 +380,27 @@ def describe(df, bins=10, corr_reject=0.9, **kwargs):
                     early_plots[col.name] = _submit_plot(st)
         # every NUM column's countDistinct with shared readbacks (and, sharded,
         # shared collectives)
-        dist = engine.distinct_batch(num_cols, hints, bounds, known) if not sharded else \
-            engine.distinct_batch_sharded(num_cols, hints, bounds, known)
-        for col, d in zip(num_cols, dist):
+        # (date columns join the batch: their distinct hint is the day range)
+        dcols = num_cols + date_cols
+        dhints = hints + [min(p1['n_valid'], p1['imax'] - p1['imin'] + 1) if p1['count'] else p1['n_valid']
+                          for p1 in date_p1]
+        dbounds = bounds + [(p1['imin'], p1['imax']) if p1['count'] else None for p1 in date_p1]
+        dknown = known + [None] * len(date_cols)
+        dist = engine.distinct_batch(dcols, dhints, dbounds, dknown) if not sharded else \
+            engine.distinct_batch_sharded(dcols, dhints, dbounds, dknown)
+        for col, d in zip(dcols, dist):
             bundles[col.name]['distinct_pre'] = d
         # every string/binary/decimal column's value counts with shared
         # readbacks (sharded: then each column's owner exchange, in column order)
         byte_cols = [c for c in table.columns if _is_byte_keyed(c)]
+        cat_items = []
         for col, tab in zip(byte_cols, engine.value_counts_bytes_batch(byte_cols)):
             bundles[col.name]['tab_pre'] = tab
+            if 1 < tab['groups'] != n:                 # CAT (describe.py:163-168): its top-50 is needed
+                cat_items.append((col, tab))
+        # every CAT column's top-50 and their values with shared readbacks
+        for (col, tab), pairs in zip(cat_items, engine.global_topk_batch([(t, c) for c, t in cat_items], TOPK)):
+            bundles[col.name]['topk_pre'] = pairs
     if workers > 1:
         done = _describe_concurrent(engine, table.columns, one, workers)
     else:

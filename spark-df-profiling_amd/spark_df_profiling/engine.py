@@ -836,12 +836,17 @@ class Engine:
         local, cand_info = self.pass1(col, plan_dev, plan)
         return self.merge_pass1(local), plan, cand_info
 
-    def numeric_pass1_batch(self, cols, probs=PROBS):
+    def numeric_pass1_batch(self, cols, probs=PROBS, minmax_cols=()):
         """numeric_pass1 of several columns with the GPU work queued back to
         back: every column's sample + quantile plan, ONE readback of the plans,
         every column's pass 1, ONE readback (one all-gather on a sharded table)
         of the results.  Two host round trips for the whole table instead of two
-        per column; results are identical to numeric_pass1 column by column."""
+        per column; results are identical to numeric_pass1 column by column.
+        `minmax_cols` (date / timestamp columns, describe.py:233) take pass 1
+        without quantile windows in the same launches and readback; with them
+        the return value is (packs, [their merged pass-1 results])."""
+        if minmax_cols:
+            return self._pass1_batch_with_minmax(cols, probs, minmax_cols)
         if not cols:
             return []
         world, sharded = self.comm.world, self.comm.sharded
@@ -945,11 +950,17 @@ class Engine:
                 self._heavy_pre[id(col)] = self._heavy_struct(a[start], cnt)
                 if start.size >= 0.9 * a.size:
                     self._near_unique.add(id(col))
-        both = torch.cat([res_all, sd.view(torch.uint8)])      # pass-1 results + sorted checks: one readback
+        # pass-1 results + sorted checks (+ the date columns' pass 1): one readback
+        extra = self._extra_readback
+        both = torch.cat([res_all, sd.view(torch.uint8)] + ([extra] if extra is not None else []))
         if not sharded:
             raws = [both.cpu().numpy().tobytes()]
         else:
             raws = [g.cpu().numpy().tobytes() for g in self.comm.allgather(both)]
+        if extra is not None:
+            tail = len(cols) * rsz + sd.numel() * 8
+            self._extra_raws = [r[tail:] for r in raws]
+            raws = [r[:tail] for r in raws]
         merged = [merge_pass1_results([nat.SdpPass1Result.from_buffer_copy(r[i * rsz:(i + 1) * rsz]) for r in raws])
                   for i in range(len(cols))]
         off = len(cols) * rsz
@@ -957,6 +968,31 @@ class Engine:
             parts = [np.frombuffer(r[off + 32 * j: off + 32 * j + 32], dtype=np.uint64) for r in raws]
             merged[i]['sorted_distinct'] = merge_sorted_distinct(parts)
         return [(merged[i], plans[i], infos[i]) for i in range(len(cols))]
+
+    def _pass1_batch_with_minmax(self, cols, probs, minmax_cols):
+        """numeric_pass1_batch plus windowless pass 1 of `minmax_cols`, whose
+        results ride the numeric columns' readback (or its all-gather)."""
+        rsz = ctypes.sizeof(nat.SdpPass1Result)
+        m = len(minmax_cols)
+        res = self._bytes(m * rsz)
+        plan_dev, plan = self.empty_plan()
+        for i, col in enumerate(minmax_cols):
+            self._pass1_launch(col, plan_dev, plan, res[i * rsz:])
+        self._extra_readback = res
+        try:
+            packs = self.numeric_pass1_batch(cols, probs) if cols else []
+        finally:
+            self._extra_readback = None
+        raws = self._extra_raws if cols else None
+        if raws is None:                                   # no numeric columns: read back alone
+            raws = [res.cpu().numpy().tobytes()] if not self.comm.sharded else \
+                [g.cpu().numpy().tobytes() for g in self.comm.allgather(res)]
+        mm = [merge_pass1_results([nat.SdpPass1Result.from_buffer_copy(r[i * rsz:(i + 1) * rsz]) for r in raws])
+              for i in range(m)]
+        return packs, mm
+
+    _extra_readback = None
+    _extra_raws = None
 
     @staticmethod
     def _sample_nondecreasing(samp):
@@ -1809,6 +1845,95 @@ class Engine:
             res += self._smallest_keys_among(select(T, T, n_eq), r_t, tab, sort_take)
         return _merge_special(res, extra, k, tab)
 
+    def topk_batch(self, tabs, k=TOPK):
+        """topk() of several tables with shared readbacks: ONE readback of the
+        log2 count histograms of every table with more than k groups, ONE of
+        every table's sorted top groups.  A table whose threshold bucket holds
+        more than GSORT_MAX groups (heavy ties) takes topk() on its own."""
+        s = self._s()
+        out = [None] * len(tabs)
+        info = []
+        for tab in tabs:
+            isb = tab['bytes']
+            info.append({'flags': int(isb) | (2 if tab.get('dense') else 0),
+                         'groups': tab['groups_local'] if 'groups_local' in tab else tab['groups'],
+                         'bcol': tab['col'].sdp_bytes() if isb else None})
+        hists = []
+        for i, (tab, inf) in enumerate(zip(tabs, info)):
+            if inf['groups'] > k:
+                hist = self._u64(64, zero=True)
+                sdp.sdp_table_count_log2_hist(ptr(tab['slots']), ptr(tab['counts']), tab['capacity'], inf['flags'],
+                                              ptr(hist), s)
+                hists.append((i, hist))
+        hh = {}
+        if hists:
+            flat = np.array(self._host_u64(torch.cat([h for _, h in hists])), dtype=np.int64)
+            hh = {i: flat[64 * j:64 * (j + 1)] for j, (i, _) in enumerate(hists)}
+        pend = []
+        for i, (tab, inf) in enumerate(zip(tabs, info)):
+            slots, counts, cap = tab['slots'], tab['counts'], tab['capacity']
+            if inf['groups'] <= k:
+                cmin, limit = 1, max(inf['groups'], 1)
+            else:
+                h = hh[i]
+                cum, b = 0, 63
+                while b >= 0:
+                    cum += int(h[b])
+                    if cum >= k:
+                        break
+                    b -= 1
+                b = max(b, 0)
+                if cum > GSORT_MAX:
+                    out[i] = self.topk(tab, k)
+                    continue
+                cmin, limit = 1 << b, cum
+            sel = self._u64(max(limit, 1))
+            on = self._u64(1, zero=True)
+            sdp.sdp_table_select(ptr(slots), ptr(counts), cap, inf['flags'], cmin, U64, ptr(sel), ptr(on), limit, s)
+            bref = ctypes.byref(inf['bcol']) if inf['bcol'] is not None else None
+            sdp.sdp_sort_groups(ptr(sel), ptr(on), ptr(slots), ptr(counts), bref, s)
+            t = max(1, min(k, sel.numel()))
+            live = torch.arange(t, device=self.device) < on[0]
+            idx_d = torch.where(live, sel[:t], torch.zeros_like(sel[:t]))
+            pend.append((i, t, torch.cat([on[:1], idx_d, counts[idx_d], slots[idx_d]])))
+        if pend:
+            flat = self._host_u64(torch.cat([p for _, _, p in pend]))
+            off = 0
+            for i, t, p in pend:
+                got = flat[off:off + p.numel()]
+                off += p.numel()
+                tab = tabs[i]
+                m = min(got[0], k)
+                idx, cnt, val = got[1:1 + m], got[1 + t:1 + t + m], got[1 + 2 * t:1 + 2 * t + m]
+                tab.setdefault('_slotval', {}).update(zip(idx, val))
+                special = (not tab['bytes']) and tab.get('max_key_rows', 0)
+                out[i] = _merge_special(list(zip(idx, cnt)), [(None, special)] if special else [], k, tab)
+        return out
+
+    def global_topk_batch(self, items, k=TOPK):
+        """global_topk of several (tab, col) pairs: the top groups of all tables
+        with shared readbacks, then the byte values of all of them in two
+        readbacks (bounds, bytes); each column's rank merge in column order."""
+        tops = self.topk_batch([tab for tab, _ in items], k)
+        byte_req = []
+        values = [None] * len(items)
+        for j, ((tab, col), top) in enumerate(zip(items, tops)):
+            slots = [sl for sl, _ in top]
+            if tab['bytes']:
+                cache = tab.get('_slotval', {})
+                rows = [(cache[sl] & ((1 << 40) - 1)) - 1 for sl in slots]
+                byte_req.append((j, tab.get('src_col', col), rows, col))
+            else:
+                values[j] = self.group_values(tab, slots, col)
+        for (j, _, _, _), vals in zip(byte_req, self.row_bytes_values_batch([r[1:] for r in byte_req])):
+            values[j] = vals
+        from .distributed import merge_topk
+        out = []
+        for (tab, col), top, vals in zip(items, tops, values):
+            pairs = [(v, int(c)) for v, (_, c) in zip(vals, top)]
+            out.append(merge_topk(self.comm, pairs, k))
+        return out
+
     def _smallest_keys_among(self, sel_pack, r, tab, sort_take):
         """The r groups with the smallest keys among a large set of equal counts."""
         sel, n_dev = sel_pack
@@ -1917,6 +2042,43 @@ class Engine:
         elif col.dtype == nat.U16:
             v = v.view(np.uint16)
         return [host_value(x, col) for x in v.tolist()]
+
+    def row_bytes_values_batch(self, reqs):
+        """row_bytes_values of several (src, rows, col) requests: ONE readback
+        of every row's byte bounds, ONE of all their bytes."""
+        out = [[] for _ in reqs]
+        live = [(j, src, rows, col) for j, (src, rows, col) in enumerate(reqs) if rows]
+        if not live:
+            return out
+        bounds = []
+        for j, src, rows, col in live:
+            if src.fixed_width:
+                w = src.fixed_width
+                st = torch.tensor([r * w for r in rows], dtype=torch.int64)
+                bounds.append(torch.cat([st, st + w]).to(self.device))
+            else:
+                ri = torch.tensor(rows, dtype=torch.int64, device=self.device)
+                o = src.offsets
+                bounds.append(torch.cat([o[ri], o[ri + 1]]).to(torch.int64))
+        se = torch.cat(bounds).cpu().tolist()                    # one readback of every bound
+        off, gathers, spans = 0, [], []
+        for (j, src, rows, col) in live:
+            m = len(rows)
+            starts, ends = se[off:off + m], se[off + m:off + 2 * m]
+            off += 2 * m
+            pos = np.concatenate([np.arange(a, b, dtype=np.int64) for a, b in zip(starts, ends)])
+            if pos.size:
+                gathers.append(src.data[torch.from_numpy(pos).to(self.device)])
+            spans.append((j, col, starts, ends, int(pos.size)))
+        flat = torch.cat(gathers).cpu().numpy().tobytes() if gathers else b''   # one readback of all bytes
+        p = 0
+        for j, col, starts, ends, _ in spans:
+            vals = []
+            for a, b in zip(starts, ends):
+                vals.append(bytes_value(flat[p:p + (b - a)], col))
+                p += b - a
+            out[j] = vals
+        return out
 
     def row_bytes_values(self, src: DeviceColumn, rows, col: DeviceColumn):
         if not rows:
