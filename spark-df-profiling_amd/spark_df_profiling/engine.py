@@ -1715,21 +1715,38 @@ class Engine:
             done.clear()
 
         held = 0
+        counted = []
+
+        def middles():
+            # ONE readback of the level-1 bucket starts of every counted column
+            if not counted:
+                return
+            flat = torch.cat([ctx['bsn_dev'] for _, ctx in counted]).cpu().numpy().astype(np.int64)
+            off = 0
+            for i, ctx in counted:
+                m = ctx['bsn_dev'].numel()
+                self._group_middle(ctx, flat[off:off + m])
+                off += m
+                done.append((i, ctx))
+            counted.clear()
+
         for i, hv in zip(big, hvs):
             ctx = self._group_prepare(cols[i], True, hv=hv)
             if ctx is None:
                 continue
-            # each column in flight keeps 16 B per record of (key, count)
-            # outputs until the shared readback: flush under a byte budget
-            need = 16 * cols[i].length
-            if done and held + need > self.BYTES_BATCH_BYTES:
+            # a column in flight holds its one-read records (24 B per row) until
+            # its middle stage, then 16 B per record of (key, count) outputs
+            # until the shared statistics readback: both under a byte budget
+            need = 40 * cols[i].length
+            if (counted or done) and held + need > self.BYTES_BATCH_BYTES:
+                middles()
                 flush()
                 held = 0
             self._group_count(ctx)
             self._group_scan(ctx)
-            self._group_middle(ctx, ctx['bsn_dev'].cpu().numpy().astype(np.int64))
-            done.append((i, ctx))
+            counted.append((i, ctx))
             held += need
+        middles()
         flush()
         for i, c in enumerate(cols):
             # small columns, collisions, table overflow: the global table (which
