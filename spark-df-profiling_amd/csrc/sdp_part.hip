@@ -1118,6 +1118,175 @@ __global__ void __launch_bounds__(WV_W * WAVE) part_dedup_u64_wave_kernel(const 
     }
 }
 
+// Two-phase wave dedup (round 3; SDP_DEDUP_V2=0 selects the kernel above).
+// The register-queue loop above pays a dependent LDS round trip plus a shift of
+// its 20-record queue (40 VGPR moves) for every probe: PMC showed ~1300 VALU and
+// ~700 SALU instructions per ~1 K-record bucket against ~80 LDS instructions
+// (profiles/r03h_pmc_group_f64_norm.csv).
+//   Phase A: every record of the batch tries its home slot once.  A lane's
+//   WV_Q home CASes (reads, then CASes of the empty ones, for repeated keys)
+//   do not depend on each other, so they issue back to back and the LDS
+//   pipelines them.  A record whose home holds a different key is appended to
+//   a wave-private LDS list (ballot + mbcnt; about a quarter of the records at
+//   the final load of one half).
+//   Phase B: lane l takes list entries l, l + 64, ... and probes linearly from
+//   home + 1 (the next entry is read while the current one probes).
+// Correctness: a slot is written once, so a deferred key's home still holds the
+// other key in phase B and every copy of a key walks the same probe sequence;
+// the table is the same linear-probing table as above, filled in another order.
+// A batch with more collisions than the list holds re-reads the extra records
+// from global memory (L2) in phase B (never seen on the bench columns).
+constexpr int WV2_OVF = 448;                    // list entries per wave (3.5 KB; 2 workgroups per CU)
+// MODE 0: read, then CAS an empty slot (repeated keys: reads broadcast);
+// MODE 1: CAS at once (near-unique keys).  (An atomic-free form -- the table is
+// wave-private and lanes run in lockstep, so read / store-if-empty / read-back
+// settles same-instruction conflicts, groups = occupied slots at the end -- was
+// measured slower: f64 4.51 -> 5.23, f32 2.31 -> 2.69 ms per 1e9 records,
+// profiles/r03n_dedup_modes_ab.log.)
+template <int MODE, bool LIMIT>
+__device__ __forceinline__ uint32_t wave2_probe(uint64_t *T, uint64_t x, bool &full) {
+    uint32_t pos = ((uint32_t)x + 1u) & (WV_SLOTS - 1);
+    for (int probes = 1;; ++probes) {
+        uint64_t cur;
+        if (MODE == 1) {
+            cur = atomicCAS((unsigned long long *)&T[pos], (unsigned long long)EMPTY64, (unsigned long long)x);
+        } else {
+            cur = T[pos];
+            if (cur == EMPTY64)
+                cur = atomicCAS((unsigned long long *)&T[pos], (unsigned long long)EMPTY64, (unsigned long long)x);
+        }
+        if (cur == EMPTY64) return 1u;
+        if (cur == x) return 0u;
+        pos = (pos + 1) & (WV_SLOTS - 1);
+        if (LIMIT && probes >= WV_SLOTS / 2) { full = true; return 0u; }
+    }
+}
+// one batch (records rb + q * 64 + lane, q < WV_Q, below hi) -> new groups of this lane
+template <int MODE, bool LIMIT>
+__device__ __forceinline__ uint32_t wave2_insert(uint64_t *T, uint64_t *O, const uint64_t (&hq)[WV_Q],
+                                                 const uint64_t *in_h, int64_t rb, int64_t hi, int lane,
+                                                 bool &full) {
+    const int64_t rem = hi - rb - lane;
+    const int left = rem <= 0 ? 0 : (int)min((int64_t)WV_Q, (rem + WAVE - 1) / WAVE);
+    uint64_t cur[WV_Q];
+#pragma unroll
+    for (int q = 0; q < WV_Q; ++q) {
+        const uint64_t x = hq[q];
+        uint64_t c = 0;
+        if (q < left) {
+            uint64_t *p = &T[(uint32_t)x & (WV_SLOTS - 1)];
+            c = MODE == 1 ? (uint64_t)atomicCAS((unsigned long long *)p, (unsigned long long)EMPTY64,
+                                                (unsigned long long)x)
+                          : *p;
+        }
+        cur[q] = c;
+    }
+    if (MODE == 0) {
+#pragma unroll
+        for (int q = 0; q < WV_Q; ++q)
+            if (q < left && cur[q] == EMPTY64)
+                cur[q] = atomicCAS((unsigned long long *)&T[(uint32_t)hq[q] & (WV_SLOTS - 1)],
+                                   (unsigned long long)EMPTY64, (unsigned long long)hq[q]);
+    }
+    uint32_t fresh = 0, late = 0, nov = 0;
+#pragma unroll
+    for (int q = 0; q < WV_Q; ++q) {
+        const bool v = q < left;
+        fresh += (v && cur[q] == EMPTY64) ? 1u : 0u;
+        const bool coll = v && cur[q] != EMPTY64 && cur[q] != hq[q];
+        const uint64_t m = __ballot(coll);
+        if (m) {                                             // wave-uniform
+            const uint32_t slot = nov + (uint32_t)lane_rank(m);
+            if (coll) {
+                if (slot < (uint32_t)WV2_OVF) O[slot] = hq[q];
+                else late |= 1u << q;
+            }
+            nov += (uint32_t)__popcll(m);
+        }
+    }
+    if (nov == 0) return fresh;
+    nov = min(nov, (uint32_t)WV2_OVF);
+    __builtin_amdgcn_wave_barrier();
+    // phase B: lane-local walk of the list, the next entry read while probing
+    uint32_t j = lane;
+    uint64_t nx = j < nov ? O[j] : 0;
+    while (j < nov) {
+        const uint64_t x = nx;
+        j += WAVE;
+        nx = j < nov ? O[j] : 0;
+        fresh += wave2_probe<MODE, LIMIT>(T, x, full);
+    }
+    while (late) {                                           // list overflow: re-read from L2
+        const int q = __builtin_ctz(late);
+        late &= late - 1;
+        fresh += wave2_probe<MODE, LIMIT>(T, in_h[rb + (int64_t)q * WAVE + lane], full);
+    }
+    __builtin_amdgcn_wave_barrier();
+    return fresh;
+}
+template <int MODE>
+__global__ void __launch_bounds__(WV_W * WAVE) part_dedup_u64_wave2_kernel(const uint64_t *in_h,
+                                                                           const uint64_t *starts,
+                                                                           int64_t nbuckets, uint64_t *stats) {
+    __shared__ uint64_t tab[WV_W][WV_SLOTS];
+    __shared__ uint64_t lst[WV_W][WV2_OVF];
+    const int lane = lane_id(), w = threadIdx.x / WAVE;
+    uint64_t *T = tab[w];
+    uint64_t *O = lst[w];
+    uint64_t groups = 0;
+    bool full = false;
+    const int64_t stride = (int64_t)gridDim.x * WV_W;
+    int64_t f = (int64_t)blockIdx.x * WV_W + w;
+    int64_t lo = 0, hi = 0;
+    uint64_t hq[WV_Q];
+    if (f < nbuckets) {
+        lo = starts[f];
+        hi = starts[f + 1];
+        wave_load_batch(hq, in_h, lo, hi, lane);
+    }
+    uint64_t hn[WV_Q];
+    auto step = [&](uint64_t (&cur)[WV_Q], uint64_t (&nxt)[WV_Q]) {
+        const int64_t fn = f + stride;
+        int64_t lo_n = 0, hi_n = 0;
+        if (fn < nbuckets) {
+            lo_n = starts[fn];
+            hi_n = starts[fn + 1];
+            wave_load_batch(nxt, in_h, lo_n, hi_n, lane);
+        }
+        if (lo != hi) {
+            ulonglong2 *T2 = (ulonglong2 *)T;
+#pragma unroll
+            for (int k = 0; k < WV_SLOTS / (2 * WAVE); ++k) T2[k * WAVE + lane] = make_ulonglong2(EMPTY64, EMPTY64);
+            __builtin_amdgcn_wave_barrier();
+            uint32_t fresh = 0;
+            if (hi - lo <= WV_BATCH) {
+                fresh = wave2_insert<MODE, false>(T, O, cur, in_h, lo, hi, lane, full);
+            } else {
+                for (int64_t rb = lo; rb < hi; rb += WV_BATCH) {
+                    if (rb != lo) wave_load_batch(cur, in_h, rb, hi, lane);
+                    fresh += wave2_insert<MODE, true>(T, O, cur, in_h, rb, hi, lane, full);
+                }
+            }
+            groups += fresh;
+            __builtin_amdgcn_wave_barrier();
+        }
+        lo = lo_n;
+        hi = hi_n;
+        f = fn;
+    };
+    while (f < nbuckets) {
+        step(hq, hn);
+        if (f >= nbuckets) break;
+        step(hn, hq);
+    }
+    groups = wave_sum_u64(groups);
+    const bool any_full = __any(full);
+    if (lane == 0) {
+        if (groups) atomicAdd((unsigned long long *)&stats[4 + (blockIdx.x & 63)], (unsigned long long)groups);
+        if (any_full) atomicOr((unsigned long long *)&stats[3], 1ull);
+    }
+}
+
 // Byte keys, in rounds of DT * 4 records held in registers:
 //   1. claim a slot per distinct hash (CAS on h)        2. the claimant writes
 //   its record into the slot    3. everyone compares bytes and counts.
@@ -1590,7 +1759,15 @@ int sdp_part_dedup(const sdp_records *in, int32_t is_bytes, const sdp_bytes_colu
                            nullptr, nullptr, nullptr, d_stats);
     } else {
         const int wgrid = grid_of((nbuckets + WV_W - 1) / WV_W, 256 * 16);
-        if (with_counts & 4)            // near-unique keys: claim with one CAS, no read first
+        const char *e = getenv("SDP_DEDUP_V2");
+        const bool v2 = e == nullptr || e[0] != '0';          // SDP_DEDUP_V2=0: the register-queue kernel
+        if (v2 && (with_counts & 4))
+            hipLaunchKernelGGL(part_dedup_u64_wave2_kernel<1>, dim3(wgrid), dim3(WV_W * WAVE), 0, s, in->d_k0,
+                               d_starts, nbuckets, d_stats);
+        else if (v2)
+            hipLaunchKernelGGL(part_dedup_u64_wave2_kernel<0>, dim3(wgrid), dim3(WV_W * WAVE), 0, s, in->d_k0,
+                               d_starts, nbuckets, d_stats);
+        else if (with_counts & 4)       // near-unique keys: claim with one CAS, no read first
             hipLaunchKernelGGL(part_dedup_u64_wave_kernel<true>, dim3(wgrid), dim3(WV_W * WAVE), 0, s, in->d_k0,
                                d_starts, nbuckets, d_stats);
         else

@@ -89,71 +89,97 @@ def _owner_order(owner, world):
 
 
 def exchange_bytes_groups(engine, tab):
-    """Re-partition a rank's byte-key groups by key hash: each group's
-    (length, count) and its key bytes go to the owner rank, which re-aggregates
-    them in a global table.  Host round trips: one readback of the per-owner
-    group and byte counts, one all-to-all of every count of the exchange, the
-    owner table's statistics, one all-reduce of the totals."""
+    """exchange_bytes_groups_batch of one rank-local table."""
+    return exchange_bytes_groups_batch(engine, [tab])[0]
+
+
+def exchange_bytes_groups_batch(engine, tabs):
+    """Re-partition every rank's byte-key groups of several columns by key
+    hash: each group's (length, count) and its key bytes go to the owner rank,
+    which re-aggregates them in a global table.  The columns share their host
+    round trips: ONE readback of every column's per-owner group and byte
+    counts, ONE all-to-all of every count of every exchange, ONE readback of
+    every owner table's statistics, ONE all-reduce of the totals (round 2 paid
+    these four per column)."""
     comm = engine.comm
     world = comm.world
-    col = tab['col']
-    if tab.get('dense'):
-        # partitioned groups are already packed: every entry is a group
-        m = int(tab['groups_local'])
-        slots, cnt = tab['slots'][:m], tab['counts'][:m]
-    else:
-        slots, cnt = _table_groups(engine, tab)
-    rows = (slots & MASK40) - 1
-    owner = ((slots >> 40) & 0xFFFFFF) % world
-    order = _owner_order(owner, world)
-    rows, cnt, owner = rows[order], cnt[order], owner[order]
-    if col.fixed_width:
-        starts = rows * col.fixed_width
-        lens = torch.full_like(rows, col.fixed_width)
-    else:
-        o = col.offsets.to(torch.int64)
-        starts = o[rows]
-        lens = o[rows + 1] - starts
-    # groups and key bytes per owner, summed on the device and read back once
-    # (a host list of every group's length would cost seconds at 1e8 labels)
-    per = torch.zeros((2, world), dtype=torch.int64, device=engine.device)
-    per[0].scatter_add_(0, owner, torch.ones_like(owner))
-    per[1].scatter_add_(0, owner, lens)
-    send_groups, send_bytes = per.tolist()
-    tot = sum(send_bytes)
-    # key bytes of every group, owner-major, packed by one native gather
-    offs = torch.cumsum(lens, 0) - lens
-    payload = torch.empty(max(tot, 1), dtype=torch.uint8, device=engine.device)[:tot]
-    if tot:
-        sdp.sdp_gather_bytes(ptr(col.data), ptr(starts.contiguous()), ptr(lens.contiguous()), ptr(offs), lens.numel(),
-                             ptr(payload), engine._s())
-    recv_groups, recv_bytes = comm.alltoall_counts([send_groups, send_bytes])
-    # (length, count) pairs in one exchange, the key bytes in a second
-    meta = torch.stack([lens, cnt], 1).contiguous().view(-1)
-    rmeta = comm.alltoallv_known(meta, [2 * g for g in send_groups], [2 * g for g in recv_groups]).view(-1, 2)
-    rbytes = comm.alltoallv_known(payload.contiguous(), send_bytes, recv_bytes)
-    rlens, rcnt = rmeta[:, 0].contiguous(), rmeta[:, 1].contiguous()
-    from .columns import DeviceColumn
-    n = int(rlens.numel())
-    rc = DeviceColumn('_exchange', col.spark_type, n, 'bytes', decimal_scale=col.decimal_scale)
-    offs = torch.zeros(n + 1, dtype=torch.int64, device=engine.device)
-    if n:
-        torch.cumsum(rlens, 0, out=offs[1:])
-    rc.offsets = offs
-    rc.offset_width = 8
-    data = torch.zeros(int(rbytes.numel()) + 16, dtype=torch.uint8, device=engine.device)
-    data[:rbytes.numel()] = rbytes
-    rc.data = data
-    local = engine.value_counts_bytes_table(rc, row_counts=rcnt, exchanged=True)
-    local['src_col'] = rc
-    local['col'] = rc
-    side = torch.tensor([tab['rows'], local['groups']], dtype=torch.int64, device=engine.device)
-    t = comm.allreduce_sum(side).tolist()
-    local['groups_local'] = local['groups']
-    local['groups'] = int(t[1])
-    local['rows'] = int(t[0])
-    local['sharded'] = True
-    return local
+    if not tabs:
+        return []
+    preps, pers = [], []
+    for tab in tabs:
+        col = tab['col']
+        if tab.get('dense'):
+            # partitioned groups are already packed: every entry is a group
+            m = int(tab['groups_local'])
+            slots, cnt = tab['slots'][:m], tab['counts'][:m]
+        else:
+            slots, cnt = _table_groups(engine, tab)
+        rows = (slots & MASK40) - 1
+        owner = ((slots >> 40) & 0xFFFFFF) % world
+        order = _owner_order(owner, world)
+        rows, cnt, owner = rows[order], cnt[order], owner[order]
+        if col.fixed_width:
+            starts = rows * col.fixed_width
+            lens = torch.full_like(rows, col.fixed_width)
+        else:
+            o = col.offsets.to(torch.int64)
+            starts = o[rows]
+            lens = o[rows + 1] - starts
+        # groups and key bytes per owner, summed on the device (a host list of
+        # every group's length would cost seconds at 1e8 labels)
+        per = torch.zeros((2, world), dtype=torch.int64, device=engine.device)
+        per[0].scatter_add_(0, owner, torch.ones_like(owner))
+        per[1].scatter_add_(0, owner, lens)
+        pers.append(per)
+        preps.append((tab, col, starts, lens, cnt))
+    allper = torch.stack(pers).cpu().tolist()                     # [column][groups | bytes][owner]
+    payloads = []
+    for (tab, col, starts, lens, cnt), (send_groups, send_bytes) in zip(preps, allper):
+        # key bytes of every group, owner-major, packed by one native gather
+        tot = sum(send_bytes)
+        offs = torch.cumsum(lens, 0) - lens
+        payload = torch.empty(max(tot, 1), dtype=torch.uint8, device=engine.device)[:tot]
+        if tot:
+            sdp.sdp_gather_bytes(ptr(col.data), ptr(starts.contiguous()), ptr(lens.contiguous()), ptr(offs),
+                                 lens.numel(), ptr(payload), engine._s())
+        payloads.append(payload)
+    recv = comm.alltoall_counts([row for pr in allper for row in pr])
+    launched = []
+    for j, ((tab, col, starts, lens, cnt), (send_groups, send_bytes), payload) in enumerate(zip(preps, allper,
+                                                                                               payloads)):
+        recv_groups, recv_bytes = recv[2 * j], recv[2 * j + 1]
+        # (length, count) pairs in one exchange, the key bytes in a second
+        meta = torch.stack([lens, cnt], 1).contiguous().view(-1)
+        rmeta = comm.alltoallv_known(meta, [2 * g for g in send_groups], [2 * g for g in recv_groups]).view(-1, 2)
+        rbytes = comm.alltoallv_known(payload.contiguous(), send_bytes, recv_bytes)
+        rlens, rcnt = rmeta[:, 0].contiguous(), rmeta[:, 1].contiguous()
+        from .columns import DeviceColumn
+        n = int(rlens.numel())
+        rc = DeviceColumn('_exchange', col.spark_type, n, 'bytes', decimal_scale=col.decimal_scale)
+        offs = torch.zeros(n + 1, dtype=torch.int64, device=engine.device)
+        if n:
+            torch.cumsum(rlens, 0, out=offs[1:])
+        rc.offsets = offs
+        rc.offset_width = 8
+        data = torch.zeros(int(rbytes.numel()) + 16, dtype=torch.uint8, device=engine.device)
+        data[:rbytes.numel()] = rbytes
+        rc.data = data
+        launched.append((tab, rc, engine.bytes_table_launch(rc, row_counts=rcnt)))
+    st = engine._host_u64(torch.cat([lt[2]['stats'] for lt in launched]))
+    locals_, sides = [], []
+    for j, (tab, rc, pend) in enumerate(launched):
+        local = engine.bytes_table_finish(pend, st[4 * j:4 * j + 4], rc)
+        local['src_col'] = rc
+        local['col'] = rc
+        locals_.append(local)
+        sides += [tab['rows'], local['groups']]
+    t = comm.allreduce_sum(torch.tensor(sides, dtype=torch.int64, device=engine.device)).tolist()
+    for j, local in enumerate(locals_):
+        local['groups_local'] = local['groups']
+        local['groups'] = int(t[2 * j + 1])
+        local['rows'] = int(t[2 * j])
+        local['sharded'] = True
+    return locals_
 
 
 def merge_topk(comm, pairs, k):

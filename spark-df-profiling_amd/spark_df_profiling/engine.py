@@ -1748,31 +1748,44 @@ class Engine:
             held += need
         middles()
         flush()
+        xch = []
         for i, c in enumerate(cols):
-            # small columns, collisions, table overflow: the global table (which
-            # exchanges itself when sharded); sharded partitioned groups go
-            # through the owner exchange -- one exchange per column, in column
-            # order, on every rank
+            # small columns, collisions, table overflow: the global table; when
+            # sharded every column's local groups (either path: the choice is
+            # rank-local) go through ONE batched owner exchange, in column order
             if out[i] is None:
-                out[i] = self.value_counts_bytes_table(c)
-            elif self.comm.sharded:
-                out[i] = self._exchange_bytes(out[i])
+                out[i] = self.value_counts_bytes_table(c, exchanged=True)
+            if self.comm.sharded:
+                xch.append(i)
+        if xch:
+            from .distributed import exchange_bytes_groups_batch
+            for i, tab in zip(xch, exchange_bytes_groups_batch(self, [out[i] for i in xch])):
+                out[i] = tab
         return out
 
     def value_counts_bytes_table(self, col, row_counts=None, exchanged=False, capacity=None):
         """Global open-addressing byte-key table (fallback / multi-rank path)."""
+        pend = self.bytes_table_launch(col, row_counts, capacity)
+        tab = self.bytes_table_finish(pend, self._host_u64(pend['stats']), col)
+        if self.comm.sharded and not exchanged:
+            tab = self._exchange_bytes(tab)
+        return tab
+
+    def bytes_table_launch(self, col, row_counts=None, capacity=None):
+        """The global byte-key table of `col`, queued (no readback)."""
         cap = capacity if capacity is not None else _next_pow2(2 * max(col.length, 1))
         slots, counts = self._table(cap, True, True)
         stats = self._u64(4, zero=True)
         bc = col.sdp_bytes()
         nat.annotate(_label(col), col_read_bytes(col))
         sdp.sdp_hash_bytes(ctypes.byref(bc), ptr(row_counts), ptr(slots), ptr(counts), cap, ptr(stats), self._s())
-        st = self._host_u64(stats)
-        tab = {'slots': slots, 'counts': counts, 'capacity': cap, 'bytes': True, 'rows': st[1], 'groups': st[0],
-               'groups_local': st[0], 'col': col}
-        if self.comm.sharded and not exchanged:
-            tab = self._exchange_bytes(tab)
-        return tab
+        return {'slots': slots, 'counts': counts, 'capacity': cap, 'stats': stats}
+
+    @staticmethod
+    def bytes_table_finish(pend, st, col):
+        """bytes_table_launch's tab from the host copy `st` of its statistics."""
+        return {'slots': pend['slots'], 'counts': pend['counts'], 'capacity': pend['capacity'], 'bytes': True,
+                'rows': st[1], 'groups': st[0], 'groups_local': st[0], 'col': col}
 
     # -- top-k by (count desc, key asc) ------------------------------------------
     def topk(self, tab, k=TOPK):

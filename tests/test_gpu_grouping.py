@@ -143,3 +143,48 @@ def test_describe_large_categorical():
     got = describe(t, plots=False)
     want, _ = oracle.profile_raw(t)
     assert_describe_equal(got, want)
+
+
+def _dedup_buckets(buckets, flags):
+    """sdp_part_dedup (distinct only) over hand-made final buckets of u64 hashes."""
+    import ctypes
+    import torch
+    from spark_df_profiling import _native as nat
+    from spark_df_profiling._native import sdp, ptr
+    h = np.concatenate(buckets).astype(np.uint64)
+    starts = np.concatenate([[0], np.cumsum([len(b) for b in buckets])]).astype(np.int64)
+    dev = torch.device('cuda', 0)
+    d_h = torch.from_numpy(h.view(np.int64)).to(dev)
+    d_s = torch.from_numpy(starts).to(dev)
+    stats = torch.zeros(68, dtype=torch.int64, device=dev)
+    rin = nat.SdpRecords(d_h.data_ptr(), None, None)
+    rc = sdp.sdp_part_dedup(ctypes.byref(rin), 0, None, ptr(d_s), len(buckets), flags, None, None, None, ptr(stats),
+                            nat.stream_handle())
+    assert rc == 0
+    st = stats.cpu().numpy()
+    return int(st[4:68].sum()), int(st[3])
+
+
+@pytest.mark.parametrize('v2', ['0', '1'])
+@pytest.mark.parametrize('direct', [0, 4])
+def test_wave_dedup_kernels(v2, direct, monkeypatch):
+    """Both wave dedup kernels (SDP_DEDUP_V2) on crafted final buckets: single and
+    multi-batch buckets, duplicates, keys sharing one home slot (collision list
+    and its overflow past 448 entries), empty buckets."""
+    monkeypatch.setenv('SDP_DEDUP_V2', v2)
+    g = datagen.rng(7)
+    b = []
+    for _ in range(300):                                   # ordinary buckets with repeats
+        m = int(g.integers(0, 1200))
+        u = g.integers(0, 2 ** 63, max(1, m // 2), dtype=np.uint64)
+        b.append(u[g.integers(0, len(u), m)] if m else np.zeros(0, np.uint64))
+    same_home = (g.integers(0, 2 ** 52, 900, dtype=np.uint64) << np.uint64(11)) | np.uint64(77)
+    b.append(np.repeat(same_home[:300], 2))                # 300 keys, one home slot
+    b.append(same_home)                                    # 900 keys, one home: list overflow
+    big = g.integers(0, 2 ** 63, 1500, dtype=np.uint64)
+    b.append(big[g.integers(0, 1500, 6000)])               # multi-batch bucket (probe limit path)
+    b.append(np.zeros(0, np.uint64))
+    groups, full = _dedup_buckets(b, direct)
+    want = sum(len(np.unique(x)) for x in b)
+    assert full == 0
+    assert groups == want
