@@ -439,13 +439,15 @@ class Engine:
     # column's pass 2, each with ONE host readback (one collective set when
     # sharded) instead of one or more per column
     # ==========================================================================
-    def _queue_column_selects(self, col, p1, plan, cand_info, probs, compact, selects, fallbacks):
+    def _queue_column_selects(self, ci, col, p1, plan, cand_info, probs, dense_req, selects, fallbacks):
         """Decide, for each rank a column needs (describe.py:203-208), whether a
         window bound resolves it from pass-1's counts or a select must run in a
-        window's compacted candidates (appended to `compact` / `selects`).  A
-        rank no window resolves (missed window, overflowed slots) goes to
-        `fallbacks` as (rank, key range [a, b], first rank of the range, keys
-        in it).  The returned state is finished by _finish_column_quantiles."""
+        window's compacted candidates (the window is appended to `dense_req` as
+        (column, window, dense capacity, cand_info) and the select to `selects`
+        as [rank, ('dense', request), None, cap, k, lo, hi, cap]).  A rank no
+        window resolves (missed window, overflowed slots) goes to `fallbacks`
+        as (rank, key range [a, b], first rank of the range, keys in it).  The
+        returned state is finished by _finish_column_quantiles."""
         n = p1['count']
         is_int = not col.is_float
         needed = {}
@@ -457,29 +459,26 @@ class Engine:
                 needed[p] = (None, spark_percentile_approx_rank(n, p) - 1, None)
         ranks = sorted({r for v in needed.values() for r in (v[1], v[2]) if r is not None})
         values, dense = {}, {}
+        w_eq_lo, w_in, w_gt, w_eq_hi = p1['w_eq_lo'], p1['w_in'], p1['w_gt'], p1['w_eq_hi']
         for r in ranks:
             key = None
             for w in range(plan.n_windows):
-                size = p1['w_eq_lo'][w] + p1['w_in'][w] + p1['w_eq_hi'][w]
-                below = n - p1['w_gt'][w] - size
+                size = w_eq_lo[w] + w_in[w] + w_eq_hi[w]
+                below = n - w_gt[w] - size
                 if below <= r < below + size:
                     rr = r - below
                     lo, hi = plan.lo[w], plan.hi[w]
-                    if rr < p1['w_eq_lo'][w]:
+                    if rr < w_eq_lo[w]:
                         key = lo
-                    elif rr < p1['w_eq_lo'][w] + p1['w_in'][w]:
+                    elif rr < w_eq_lo[w] + w_in[w]:
                         if (p1['w_overflow'] >> w) & 1:
                             break
                         if w not in dense:
                             # dense copy sized by the window's (global) inside count
-                            cap = max(1, int(p1['w_in'][w]))
-                            out, out_n = self._u64(cap), self._u64(1, zero=True)
-                            nseg, slot = cand_info['nseg'], cand_info['cap']
-                            compact.append((cand_info['cand'][w * nseg * slot:], cand_info['counts'][w * nseg:],
-                                            nseg, slot, self._u64(nseg), out, out_n))
-                            dense[w] = (out, out_n, cap)
-                        out, out_n, cap = dense[w]
-                        selects.append([r, out, out_n, cap, rr - p1['w_eq_lo'][w], lo, hi, cap])
+                            dense[w] = len(dense_req)
+                            dense_req.append((ci, w, max(1, int(w_in[w])), cand_info))
+                        cap = dense_req[dense[w]][2]
+                        selects.append([r, ('dense', dense[w]), None, cap, rr - w_eq_lo[w], lo, hi, cap])
                         key = 'queued'
                     else:
                         key = hi
@@ -488,43 +487,63 @@ class Engine:
                 fallbacks.append((r,) + self._rank_key_range(r, p1, plan))
                 key = 'queued'
             values[r] = key
-        return {'values': values, 'needed': needed, 'is_int': is_int, 'probs': probs, 'fallback': False,
-                'dense': dense}
+        return {'values': values, 'needed': needed, 'is_int': is_int, 'probs': probs, 'fallback': False}
 
     SELECT_BATCH_BYTES = 24 << 30          # select workspaces alive at once (flushed in groups)
     BYTES_BATCH_BYTES = 40 << 30           # byte columns' (key, count) group outputs alive at once
+    _sel_ws0 = None
+
+    @classmethod
+    def _select_ws(cls, n_cap):
+        """sdp_select_kth_workspace_bytes(n_cap) (sdp_numeric.hip: 256-byte
+        aligned state, histogram, two counters, two key buffers) without a
+        foreign call per select."""
+        if cls._sel_ws0 is None:
+            cls._sel_ws0 = int(sdp.sdp_select_kth_workspace_bytes(1)) - 512
+        return cls._sel_ws0 + 2 * ((8 * max(int(n_cap), 1) + 255) // 256 * 256)
+
+    @staticmethod
+    def _select_rounds(lo, hi):
+        x = _u(lo) ^ _u(hi)
+        return (x.bit_length() - 1) // 11 + 1 if x else 1      # sdp_select_rounds
 
     def _run_selects(self, selects, res):
-        """Queue every select of `selects` ([rank, keys, n_dev, n_cap, k, lo, hi,
-        budget_cap]); result j lands in res[j].  Groups whose workspaces fit
-        SELECT_BATCH_BYTES run as one sdp_select_batch (sharded: one stream-
-        ordered all-reduce of the digit histograms per radix round for the
-        whole group).  Returns the buffers that must outlive the readback."""
+        """Queue every select of `selects` ([rank, keys pointer, count pointer,
+        n_cap, k, lo, hi, budget_cap]); result j lands in res[j].  Groups whose
+        workspaces fit SELECT_BATCH_BYTES run as one sdp_select_batch (sharded:
+        one stream-ordered all-reduce of the digit histograms per radix round
+        for the whole group).  Returns the buffers that must outlive the
+        readback."""
         s = self._s()
         keep = []
         j0 = 0
+        ws = [self._select_ws(x[7]) for x in selects]
+        wsa = [(w + 255) // 256 * 256 for w in ws]
         while j0 < len(selects):
             # a group of selects whose workspaces fit the budget (at least one);
             # budget_cap is the same on every rank, so is the grouping
             j1, tot = j0, 0
             while j1 < len(selects):
-                wb = int(sdp.sdp_select_kth_workspace_bytes(int(selects[j1][7])))
-                if j1 > j0 and tot + wb > self.SELECT_BATCH_BYTES:
+                if j1 > j0 and tot + ws[j1] > self.SELECT_BATCH_BYTES:
                     break
-                tot += (wb + 255) // 256 * 256
+                tot += wsa[j1]
                 j1 += 1
             q = j1 - j0
-            tot = sum((int(sdp.sdp_select_kth_workspace_bytes(int(x[3]))) + 255) // 256 * 256 for x in selects[j0:j1])
-            work = self._bytes(tot)
-            tasks = (nat.SdpSelectTask * q)()
-            off, rounds = 0, 1
-            for t, (r, arr, arr_n, ncap, kk, lo, hi, _) in enumerate(selects[j0:j1]):
-                wb = int(sdp.sdp_select_kth_workspace_bytes(int(ncap)))
-                tasks[t] = nat.SdpSelectTask(arr.data_ptr(), arr_n.data_ptr(), int(ncap), int(kk), _u(lo), _u(hi),
-                                             work.data_ptr() + off, res.data_ptr() + 8 * (j0 + t))
-                off += (wb + 255) // 256 * 256
-                rounds = max(rounds, int(sdp.sdp_select_rounds(_u(lo), _u(hi))))
-            d_tasks = self._h2d(np.frombuffer(bytearray(bytes(tasks)), dtype=np.uint8))
+            sizes = [self._select_ws(x[3]) for x in selects[j0:j1]]
+            offs = np.concatenate([[0], np.cumsum([(w + 255) // 256 * 256 for w in sizes])]).astype(np.uint64)
+            work = self._bytes(int(offs[-1]))
+            t = np.zeros((q, 8), dtype=np.uint64)           # SdpSelectTask rows
+            grp = selects[j0:j1]
+            t[:, 0] = [x[1] for x in grp]
+            t[:, 1] = [x[2] for x in grp]
+            t[:, 2] = [int(x[3]) for x in grp]
+            t[:, 3] = [int(x[4]) for x in grp]
+            t[:, 4] = [_u(x[5]) for x in grp]
+            t[:, 5] = [_u(x[6]) for x in grp]
+            t[:, 6] = np.uint64(work.data_ptr()) + offs[:-1]
+            t[:, 7] = np.uint64(res.data_ptr()) + np.uint64(8) * np.arange(j0, j1, dtype=np.uint64)
+            rounds = max(self._select_rounds(x[5], x[6]) for x in grp)
+            d_tasks = self._h2d(t.view(np.uint8).reshape(-1))
             hist = self._u64(q * 2048)
             if not self.comm.sharded:
                 sdp.sdp_select_batch(ptr(d_tasks), q, rounds, ptr(hist), s)
@@ -542,36 +561,53 @@ class Engine:
         the candidate compactions of every window in two launches, the selects
         of every column in ~2 launches per radix round (sdp_select_batch; one
         all-reduce per round for ALL columns when sharded) and one readback.
-        Ranks no window resolves are then selected one key range at a time:
-        the range's keys are re-collected from the column (sized by pass 1's
-        exact count), selected and freed, so the fallback holds at most one
-        range (<= 24 B per row of it) instead of every column's keys."""
+        The dense candidate copies of all windows share one allocation and
+        every task table is built as one numpy array (wide tables: 512 columns
+        x 5 windows).  Ranks no window resolves are then selected one key
+        range at a time: the range's keys are re-collected from the column
+        (sized by pass 1's exact count), selected and freed, so the fallback
+        holds at most one range (<= 24 B per row of it) instead of every
+        column's keys."""
         s = self._s()
-        states, sel_owner, compact, selects, fbs = [], [], [], [], []
+        states, sel_owner, dense_req, selects, fbs = [], [], [], [], []
         for i, (col, p1, plan, cand_info) in enumerate(items):
             before = len(selects)
             fb = []
-            states.append(self._queue_column_selects(col, p1, plan, cand_info, probs, compact, selects, fb))
+            states.append(self._queue_column_selects(i, col, p1, plan, cand_info, probs, dense_req, selects, fb))
             sel_owner += [i] * (len(selects) - before)
             fbs.append(fb)
         keep = []
-        if compact:
-            tasks = (nat.SdpCompactTask * len(compact))()
-            for j, (cand, cnt, nseg, slot, offw, out, out_n) in enumerate(compact):
-                tasks[j] = nat.SdpCompactTask(cand.data_ptr(), cnt.data_ptr(), nseg, slot, offw.data_ptr(),
-                                              out.data_ptr(), out_n.data_ptr())
-            d_tasks = self._h2d(np.frombuffer(bytearray(bytes(tasks)), dtype=np.uint8))
-            sdp.sdp_compact_batch(ptr(d_tasks), len(compact), max(c[2] for c in compact), s)
-            keep.append((d_tasks, compact))
+        if dense_req:
+            m = len(dense_req)
+            caps = np.array([d[2] for d in dense_req], dtype=np.uint64)
+            coff = np.concatenate([[0], np.cumsum(caps)]).astype(np.uint64)
+            nsegs = np.array([d[3]['nseg'] for d in dense_req], dtype=np.uint64)
+            noff = np.concatenate([[0], np.cumsum(nsegs)]).astype(np.uint64)
+            dbuf = self._u64(int(coff[-1]))
+            dn = self._u64(m, zero=True)
+            offw = self._u64(int(noff[-1]))
+            t = np.zeros((m, 7), dtype=np.uint64)           # SdpCompactTask rows
+            t[:, 0] = [d[3]['cand'].data_ptr() + 8 * d[1] * d[3]['nseg'] * d[3]['cap'] for d in dense_req]
+            t[:, 1] = [d[3]['counts'].data_ptr() + 4 * d[1] * d[3]['nseg'] for d in dense_req]
+            t[:, 2] = nsegs
+            t[:, 3] = [d[3]['cap'] for d in dense_req]
+            t[:, 4] = np.uint64(offw.data_ptr()) + np.uint64(8) * noff[:-1]
+            t[:, 5] = np.uint64(dbuf.data_ptr()) + np.uint64(8) * coff[:-1]
+            t[:, 6] = np.uint64(dn.data_ptr()) + np.uint64(8) * np.arange(m, dtype=np.uint64)
+            d_tasks = self._h2d(t.view(np.uint8).reshape(-1))
+            sdp.sdp_compact_batch(ptr(d_tasks), m, int(nsegs.max()), s)
+            keep.append((d_tasks, dbuf, dn, offw))
+            for x in selects:                                 # ('dense', j) -> the j-th dense copy
+                j = x[1][1]
+                x[1] = dbuf.data_ptr() + 8 * int(coff[j])
+                x[2] = dn.data_ptr() + 8 * j
         res = self._u64(max(1, len(selects)))
         keep += self._run_selects(selects, res)
         keys = self._host_u64(res) if selects else []          # the one readback
         del keep
         for j, owner in enumerate(sel_owner):
             states[owner]['values'][selects[j][0]] = keys[j]
-        del selects, compact
-        for st in states:
-            st['dense'] = None
+        del selects
         # fallback ranks, one key range at a time (the same sequence on every rank)
         for i, (col, p1, plan, cand_info) in enumerate(items):
             groups = {}
@@ -579,7 +615,8 @@ class Engine:
                 groups.setdefault((a, b, base, cnt), []).append(r)
             for (a, b, base, cnt), rs in groups.items():
                 arr, arr_n = self._range_keys(col, a, b, min(int(cnt), col.length))
-                sel = [[r, arr, arr_n, arr.numel(), r - base, a, b, max(1, int(cnt))] for r in rs]
+                sel = [[r, arr.data_ptr(), arr_n.data_ptr(), arr.numel(), r - base, a, b, max(1, int(cnt))]
+                       for r in rs]
                 res = self._u64(len(sel))
                 keep = self._run_selects(sel, res)
                 for r, v in zip(rs, self._host_u64(res)):

@@ -172,3 +172,19 @@ def test_merge_sorted_distinct_rank_order():
     assert merge_sorted_distinct([p(5, 0, 10, 20), p(0, 0, E, E), p(1, 0, 20, 20)]) == 5
     assert merge_sorted_distinct([p(5, 0, 10, 20), p(3, 0, 19, 30)]) is None
     assert merge_sorted_distinct([p(5, 1, 10, 20)]) is None
+
+
+def test_select_sizing_mirrors_the_library():
+    """quantiles_batch sizes select workspaces and radix rounds on the host
+    (Engine._select_ws / _select_rounds); they must equal the C ABI's
+    sdp_select_kth_workspace_bytes / sdp_select_rounds (no GPU needed)."""
+    import random
+    from spark_df_profiling.engine import Engine
+    from spark_df_profiling._native import sdp
+    for n in [0, 1, 2, 31, 32, 33, 1000, 12345678, 10 ** 9]:
+        assert Engine._select_ws(n) == sdp.sdp_select_kth_workspace_bytes(n), n
+    rnd = random.Random(3)
+    for _ in range(2000):
+        lo = rnd.getrandbits(64)
+        hi = rnd.getrandbits(rnd.randint(0, 64))
+        assert Engine._select_rounds(lo, hi) == sdp.sdp_select_rounds(lo, hi)

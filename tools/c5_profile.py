@@ -21,6 +21,13 @@ dev = torch.device('cuda', 0)
 t = bench.make_c5_shard(rows, 0, 1, dev, ncols=ncols)
 describe(t, plots=False)
 torch.cuda.synchronize()
+walls = []
+for _ in range(3):
+    t0 = time.perf_counter()
+    describe(t, plots=False)
+    torch.cuda.synchronize()
+    walls.append((time.perf_counter() - t0) * 1e3)
+print('steps (ms):', ' '.join('%.1f' % w for w in walls))
 rec = nat.start_recording()
 t0 = time.perf_counter()
 describe(t, plots=False)
