@@ -354,8 +354,10 @@ def describe(df, bins=10, corr_reject=0.9, **kwargs):
         num_cols = [c for c in table.columns if _is_numeric(c)]
         # date / timestamp columns: min/max in the numeric pass-1 launches and readback
         date_cols = [c for c in table.columns if _is_date(c)]
-        packs, date_p1 = engine.numeric_pass1_batch(num_cols, minmax_cols=date_cols) if date_cols else \
-            (engine.numeric_pass1_batch(num_cols), [])
+        # byte columns: their heavy-key samples ride the same readback
+        byte_cols = [c for c in table.columns if _is_byte_keyed(c)]
+        packs, date_p1 = engine.numeric_pass1_batch(num_cols, minmax_cols=date_cols, byte_cols=byte_cols) \
+            if date_cols else (engine.numeric_pass1_batch(num_cols, byte_cols=byte_cols), [])
         for col, p1 in zip(date_cols, date_p1):
             bundles[col.name]['minmax_pre'] = p1
         p1s = [pk[0] for pk in packs]
@@ -392,7 +394,6 @@ def describe(df, bins=10, corr_reject=0.9, **kwargs):
             bundles[col.name]['distinct_pre'] = d
         # every string/binary/decimal column's value counts with shared
         # readbacks (sharded: then each column's owner exchange, in column order)
-        byte_cols = [c for c in table.columns if _is_byte_keyed(c)]
         cat_items = []
         for col, tab in zip(byte_cols, engine.value_counts_bytes_batch(byte_cols)):
             bundles[col.name]['tab_pre'] = tab

@@ -185,6 +185,7 @@ class Engine:
         self._heavy_pre = None          # id(col) -> heavy keys sampled with pass 1
         self._near_unique = set()       # id(col) of columns >= 90 % distinct in that sample
         self._counted = {}              # id(col) -> group context whose level-1 count pass 2 did
+        self._heavy_bytes_pre = {}      # id(col) -> byte column's heavy keys, sampled with pass 1
 
     # -- small helpers ----------------------------------------------------------
 
@@ -873,7 +874,7 @@ class Engine:
         local, cand_info = self.pass1(col, plan_dev, plan)
         return self.merge_pass1(local), plan, cand_info
 
-    def numeric_pass1_batch(self, cols, probs=PROBS, minmax_cols=()):
+    def numeric_pass1_batch(self, cols, probs=PROBS, minmax_cols=(), byte_cols=()):
         """numeric_pass1 of several columns with the GPU work queued back to
         back: every column's sample + quantile plan, ONE readback of the plans,
         every column's pass 1, ONE readback (one all-gather on a sharded table)
@@ -883,7 +884,7 @@ class Engine:
         without quantile windows in the same launches and readback; with them
         the return value is (packs, [their merged pass-1 results])."""
         if minmax_cols:
-            return self._pass1_batch_with_minmax(cols, probs, minmax_cols)
+            return self._pass1_batch_with_minmax(cols, probs, minmax_cols, byte_cols)
         if not cols:
             return []
         world, sharded = self.comm.world, self.comm.sharded
@@ -945,11 +946,16 @@ class Engine:
             if sharded:
                 hs = torch.cat([p.view(len(hcols), nsr) for p in self.comm.allgather(hs)], dim=1).contiguous()
             sdp.sdp_sort_small_batch(ptr(hs), hn_each, len(hcols), s)
-            raw = torch.cat([plans_dev, hs.view(-1).view(torch.uint8), mono]).cpu().numpy()
-        else:
-            raw = torch.cat([plans_dev, mono]).cpu().numpy()
+        # the heavy-key samples of the byte columns (value_counts_bytes_batch)
+        # ride the same readback; their host work runs while pass 1 does
+        bsm = [self._heavy_sample_launch(c, True) for c in byte_cols if c.length >= (1 << 16)]
+        bparts = [sm['readback'] if sm['readback'] is not None else sm['h'] for sm in bsm]
+        bview = [p.view(torch.uint8) for p in bparts]
+        nb_bytes = sum(p.numel() for p in bview)
+        raw = torch.cat([plans_dev] + ([hs.view(-1).view(torch.uint8)] if hcols else []) + bview + [mono]).cpu().numpy()
         mono_h = raw[-len(cols):].astype(bool)
-        raw = raw[:-len(cols)]
+        braw = raw[len(raw) - len(cols) - nb_bytes:len(raw) - len(cols)]
+        raw = raw[:len(raw) - len(cols) - nb_bytes]
         plans = [nat.SdpQPlan.from_buffer_copy(raw[i * psz:(i + 1) * psz].tobytes()) for i in range(len(cols))]
         if DEBUG_QUANTILE == 'miss':
             for i, p in enumerate(plans):
@@ -971,6 +977,11 @@ class Engine:
             cs = cols[i].sdp()
             nat.annotate(_label(cols[i], 'sorted'), col_read_bytes(cols[i]))
             sdp.sdp_sorted_distinct(ctypes.byref(cs), ptr(sd[4 * j:]), s)
+        if bsm:                                   # (pass 1 is running meanwhile)
+            flat, off = braw.view(np.uint64), 0
+            for c, sm, p in zip([c for c in byte_cols if c.length >= (1 << 16)], bsm, bparts):
+                self._heavy_bytes_pre[id(c)] = self._heavy_keys_finish(sm, flat[off:off + p.numel()])
+                off += p.numel()
         if hcols:
             if self._heavy_pre is None:
                 self._heavy_pre = {}
@@ -1006,7 +1017,7 @@ class Engine:
             merged[i]['sorted_distinct'] = merge_sorted_distinct(parts)
         return [(merged[i], plans[i], infos[i]) for i in range(len(cols))]
 
-    def _pass1_batch_with_minmax(self, cols, probs, minmax_cols):
+    def _pass1_batch_with_minmax(self, cols, probs, minmax_cols, byte_cols=()):
         """numeric_pass1_batch plus windowless pass 1 of `minmax_cols`, whose
         results ride the numeric columns' readback (or its all-gather)."""
         rsz = ctypes.sizeof(nat.SdpPass1Result)
@@ -1017,7 +1028,7 @@ class Engine:
             self._pass1_launch(col, plan_dev, plan, res[i * rsz:])
         self._extra_readback = res
         try:
-            packs = self.numeric_pass1_batch(cols, probs) if cols else []
+            packs = self.numeric_pass1_batch(cols, probs, byte_cols=byte_cols) if cols else []
         finally:
             self._extra_readback = None
         raws = self._extra_raws if cols else None
@@ -1733,7 +1744,11 @@ class Engine:
         on a sharded table each column's groups then take the owner exchange."""
         out = [None] * len(cols)
         big = [i for i, c in enumerate(cols) if c.length >= (1 << 16)]
-        hvs = self._heavy_keys_batch([cols[i] for i in big])
+        pre = self._heavy_bytes_pre
+        if all(id(cols[i]) in pre for i in big):           # sampled with pass 1
+            hvs = [pre.pop(id(cols[i])) for i in big]
+        else:
+            hvs = self._heavy_keys_batch([cols[i] for i in big])
         done = []
 
         def flush():
