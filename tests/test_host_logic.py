@@ -188,3 +188,4 @@ def test_select_sizing_mirrors_the_library():
         lo = rnd.getrandbits(64)
         hi = rnd.getrandbits(rnd.randint(0, 64))
         assert Engine._select_rounds(lo, hi) == sdp.sdp_select_rounds(lo, hi)
+
