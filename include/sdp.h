@@ -197,6 +197,29 @@ int sdp_pass1(const sdp_column *col, const sdp_qplan *d_plan, void *d_work,
 /* Grid size sdp_pass1 uses for `length` rows (host-only). */
 int32_t sdp_pass1_grid(int64_t length, int32_t dtype);
 
+/* One column of sdp_pass1_batch: sdp_pass1's arguments, with the workspace
+ * holding `grid` (= sdp_pass1_grid of the column) block partials. */
+typedef struct sdp_pass1_task {
+    sdp_column         col;
+    const sdp_qplan   *d_plan;
+    void              *d_work;
+    uint64_t          *d_cand;
+    uint32_t          *d_cand_counts;
+    int64_t            slot_capacity;
+    sdp_pass1_result  *d_result;
+    int32_t            grid;
+    int32_t            _pad;
+} sdp_pass1_task;
+
+/* sdp_pass1 of `ntasks` columns of ONE dtype and one window mode (flags,
+ * slot_capacity > 0 or == 0 for all) in two launches (grid: max_grid x ntasks
+ * blocks, then one merge block per column) -- wide tables (SURVEY.md §8d C5:
+ * 512 columns) pay two launches instead of two per column.  d_tasks lives in
+ * device memory.  Replaces the per-column aggregate jobs of describe.py:193-220
+ * exactly as sdp_pass1 does. */
+int sdp_pass1_batch(const sdp_pass1_task *d_tasks, int32_t ntasks, int32_t dtype, int32_t windowed,
+                    int32_t flags, int32_t max_grid, void *stream);
+
 /* Gather `nseg` segments of `slot_capacity` u64 slots (segment s holds
  * d_cand_counts[s] entries) into a dense array, in segment order;
  * *d_out_count receives the total.  d_offsets_work: nseg u64 of workspace.

@@ -477,10 +477,12 @@ __device__ __forceinline__ void p1_fold(P1Thread &st) {
     st.t1 = st.t3 = 0.0;
 }
 
-template <typename T, bool WIN, bool INCL = false>
-__global__ void __launch_bounds__(P1_BLOCK, 4) pass1_kernel(sdp_column col, const sdp_qplan *plan,
-                                                         P1Partial *partials, uint64_t *cand,
-                                                         uint32_t *cand_counts, int64_t cap) {
+// pass 1 of one column by block bx of a G-block grid (the batched launch runs
+// several columns' grids side by side, blockIdx.y = column)
+template <typename T, bool WIN, bool INCL>
+__device__ __forceinline__ void pass1_body(const sdp_column &col, const sdp_qplan *plan, P1Partial *partials,
+                                           uint64_t *cand, uint32_t *cand_counts, int64_t cap, const int G,
+                                           const int bx) {
     constexpr int VPT = Vec16<T>::N;
 
     P1Ctx cx;
@@ -489,7 +491,7 @@ __global__ void __launch_bounds__(P1_BLOCK, 4) pass1_kernel(sdp_column col, cons
     for (int w = 0; w < SDP_MAX_WINDOWS; ++w) {
         cx.lo[w] = w < cx.nw ? plan->lo[w] : EMPTY64;
         cx.hi[w] = w < cx.nw ? plan->hi[w] : (INCL ? EMPTY64 - 1 : EMPTY64);
-        const int64_t seg = ((int64_t)w * gridDim.x + blockIdx.x) * P1_WPB + (threadIdx.x / WAVE);
+        const int64_t seg = ((int64_t)w * G + bx) * P1_WPB + (threadIdx.x / WAVE);
         cx.seg[w] = cand + seg * cap;
     }
     cx.K = plan->shift;
@@ -531,22 +533,22 @@ __global__ void __launch_bounds__(P1_BLOCK, 4) pass1_kernel(sdp_column col, cons
         }
         p1_fold(st);
     };
-    int64_t tile = blockIdx.x;
+    int64_t tile = bx;
     if (tile < ntiles) {
         load(ta, tile);
         while (true) {
-            load(tb, tile + gridDim.x);         // past the last tile: clamped, zero bits, never worked on
+            load(tb, tile + G);         // past the last tile: clamped, zero bits, never worked on
             work(ta);
-            tile += gridDim.x;
+            tile += G;
             if (tile >= ntiles) break;
-            load(ta, tile + gridDim.x);
+            load(ta, tile + G);
             work(tb);
-            tile += gridDim.x;
+            tile += G;
             if (tile >= ntiles) break;
         }
     }
     // tail elements (n % VPT) by the first wave of block 0
-    if (blockIdx.x == 0 && threadIdx.x < WAVE) {
+    if (bx == 0 && threadIdx.x < WAVE) {
         const int64_t i = nvec * VPT + threadIdx.x;
         const bool inb = i < n;
         T x = inb ? ((const T *)col.d_values)[i] : (T)0;
@@ -594,13 +596,13 @@ __global__ void __launch_bounds__(P1_BLOCK, 4) pass1_kernel(sdp_column col, cons
                 s_u[wid][4 + w] = g; s_u[wid][4 + W_ + w] = e1; s_u[wid][4 + 2 * W_ + w] = e2;
                 s_u[wid][4 + 3 * W_ + w] = st.wcur[w];
                 if (w < cx.nw)
-                    cand_counts[((int64_t)w * gridDim.x + blockIdx.x) * P1_WPB + wid] =
+                    cand_counts[((int64_t)w * G + bx) * P1_WPB + wid] =
                         (int64_t)st.wcur[w] < cap ? st.wcur[w] : (uint32_t)cap;
             }
         }
     }
     __syncthreads();
-    P1Partial *out = partials + blockIdx.x;
+    P1Partial *out = partials + bx;
     const int t = threadIdx.x;
     constexpr int NW = P1_BLOCK / WAVE;
     if (t < NU) {
@@ -635,6 +637,21 @@ __global__ void __launch_bounds__(P1_BLOCK, 4) pass1_kernel(sdp_column col, cons
     }
 }
 
+template <typename T, bool WIN, bool INCL = false>
+__global__ void __launch_bounds__(P1_BLOCK, 4) pass1_kernel(sdp_column col, const sdp_qplan *plan,
+                                                         P1Partial *partials, uint64_t *cand,
+                                                         uint32_t *cand_counts, int64_t cap) {
+    pass1_body<T, WIN, INCL>(col, plan, partials, cand, cand_counts, cap, (int)gridDim.x, (int)blockIdx.x);
+}
+// several columns of one dtype and window mode in one launch: blockIdx.y = task
+template <typename T, bool WIN, bool INCL = false>
+__global__ void __launch_bounds__(P1_BLOCK, 4) pass1_batch_kernel(const sdp_pass1_task *tasks) {
+    const sdp_pass1_task &tk = tasks[blockIdx.y];
+    if ((int)blockIdx.x >= tk.grid) return;
+    pass1_body<T, WIN, INCL>(tk.col, tk.d_plan, (P1Partial *)tk.d_work, tk.d_cand, tk.d_cand_counts,
+                             tk.slot_capacity, tk.grid, (int)blockIdx.x);
+}
+
 // Deterministic merge of the block partials: every field is reduced by the
 // whole workgroup (strided partial sums, then a fixed-order tree in LDS).
 constexpr int MERGE_T = 256;
@@ -663,8 +680,18 @@ __device__ __forceinline__ V block_reduce(V v, V *sm, Op op) {
     return v;
 }
 
+__device__ __forceinline__ void pass1_merge_body(const P1Partial *partials, int grid, const sdp_qplan *plan,
+                                                 sdp_pass1_result *out);
 __global__ void __launch_bounds__(MERGE_T) pass1_merge_kernel(const P1Partial *partials, int grid,
                                                               const sdp_qplan *plan, sdp_pass1_result *out) {
+    pass1_merge_body(partials, grid, plan, out);
+}
+__global__ void __launch_bounds__(MERGE_T) pass1_merge_batch_kernel(const sdp_pass1_task *tasks) {
+    const sdp_pass1_task &tk = tasks[blockIdx.x];
+    pass1_merge_body((const P1Partial *)tk.d_work, tk.grid, tk.d_plan, tk.d_result);
+}
+__device__ __forceinline__ void pass1_merge_body(const P1Partial *partials, int grid, const sdp_qplan *plan,
+                                                 sdp_pass1_result *out) {
     __shared__ double sh[MERGE_T], sl[MERGE_T];
     __shared__ uint64_t su[MERGE_T];
     __shared__ int64_t si[MERGE_T];
@@ -1594,6 +1621,29 @@ extern "C" int sdp_pass1(const sdp_column *col, const sdp_qplan *d_plan, void *d
     if (rc) return rc;
     hipLaunchKernelGGL(pass1_merge_kernel, dim3(1), dim3(MERGE_T), 0, s, parts, grid, d_plan, d_result);
     return check_launch("pass1_merge_kernel");
+}
+
+extern "C" int sdp_pass1_batch(const sdp_pass1_task *d_tasks, int32_t ntasks, int32_t dtype, int32_t windowed,
+                               int32_t flags, int32_t max_grid, void *stream) {
+    if (d_tasks == nullptr || ntasks < 1 || ntasks > 65535 || max_grid < 1 || max_grid > P1_MAX_GRID)
+        return set_error(SDP_EINVAL, "sdp_pass1_batch: args");
+    if (elem_size(dtype) <= 0 || dtype == SDP_BOOL) return set_error(SDP_EINVAL, "sdp_pass1_batch: dtype %d", dtype);
+    hipStream_t s = (hipStream_t)stream;
+    const dim3 grid(max_grid, ntasks);
+    if (windowed && (flags & SDP_PASS1_INCLUSIVE)) {
+        SDP_DISPATCH_NUMERIC(dtype,
+            hipLaunchKernelGGL((pass1_batch_kernel<T, true, true>), grid, dim3(P1_BLOCK), 0, s, d_tasks));
+    } else if (windowed) {
+        SDP_DISPATCH_NUMERIC(dtype,
+            hipLaunchKernelGGL((pass1_batch_kernel<T, true>), grid, dim3(P1_BLOCK), 0, s, d_tasks));
+    } else {
+        SDP_DISPATCH_NUMERIC(dtype,
+            hipLaunchKernelGGL((pass1_batch_kernel<T, false>), grid, dim3(P1_BLOCK), 0, s, d_tasks));
+    }
+    int rc = check_launch("pass1_batch_kernel");
+    if (rc) return rc;
+    hipLaunchKernelGGL(pass1_merge_batch_kernel, dim3(ntasks), dim3(MERGE_T), 0, s, d_tasks);
+    return check_launch("pass1_merge_batch_kernel");
 }
 
 extern "C" int sdp_compact_candidates(const uint64_t *d_cand, const uint32_t *d_cand_counts, int32_t nseg,

@@ -93,6 +93,12 @@ class SdpCompactTask(ctypes.Structure):
                 ('d_out_count', ctypes.c_void_p)]
 
 
+class SdpPass1Task(ctypes.Structure):
+    _fields_ = [('col', SdpColumn), ('d_plan', ctypes.c_void_p), ('d_work', ctypes.c_void_p),
+                ('d_cand', ctypes.c_void_p), ('d_cand_counts', ctypes.c_void_p), ('slot_capacity', ctypes.c_int64),
+                ('d_result', ctypes.c_void_p), ('grid', ctypes.c_int32), ('_pad', ctypes.c_int32)]
+
+
 class SdpPass2Result(ctypes.Structure):
     _fields_ = [('abs_dev_sum', ctypes.c_double), ('n_high', ctypes.c_uint64), ('n_low', ctypes.c_uint64),
                 ('n_unbinned', ctypes.c_uint64)]
@@ -121,6 +127,7 @@ _SIGNATURES = {
     'sdp_quantile_plan_batch': (ctypes.c_int, [_P, _I32, _I32, _P, _I32, _P, _P, _P]),
     'sdp_quantile_refine_batch': (ctypes.c_int, [_P, _I32, _I32, _P, _I32, _P, _P]),
     'sdp_pass1': (ctypes.c_int, [_COL, _P, _P, _I64, _P, _P, _I64, _I32, _P, _P]),
+    'sdp_pass1_batch': (ctypes.c_int, [_P, _I32, _I32, _I32, _I32, _I32, _P]),
     'sdp_compact_candidates': (ctypes.c_int, [_P, _P, _I32, _I64, _P, _P, _P, _P]),
     'sdp_radix_hist': (ctypes.c_int, [_P, _P, _U64, _I32, _P, _P]),
     'sdp_radix_filter': (ctypes.c_int, [_P, _P, _U64, _I32, _P, _P, _P]),

@@ -54,6 +54,8 @@ PART_CHUNK = 65536           # level-2 records per workgroup chunk
 BYTES_ONE_READ = os.environ.get('SDP_BYTES_TWO_READS', '0') != '1'
 # pass 1 with inclusive quantile windows where the plan allows (SDP_PASS1_EXCL=1: never, for A/B runs)
 PASS1_INCLUSIVE = os.environ.get('SDP_PASS1_EXCL', '0') != '1'
+# SDP_PASS1_BATCH=0: one sdp_pass1 launch per column instead of one sdp_pass1_batch per dtype
+PASS1_BATCH = os.environ.get('SDP_PASS1_BATCH', '0') != '0'
 CAND_FULL_BUDGET = 1 << 30   # bytes of room-for-every-row candidate slots per pass-1 batch
 
 # Test knob for the quantile edge paths (never set in production):
@@ -244,7 +246,7 @@ class Engine:
         p.shift = 0.0
         return self._to_dev(p), p
 
-    def _pass1_launch(self, col: DeviceColumn, plan_dev, plan, res_dev=None, budget=None):
+    def _pass1_launch(self, col: DeviceColumn, plan_dev, plan, res_dev=None, budget=None, defer=False):
         """Launch pass 1 of one column.  `budget` (a one-element list of bytes
         left) is shared by the columns of one batch: every column's candidate
         slots stay alive until its quantiles are resolved, so the room-for-
@@ -287,10 +289,47 @@ class Engine:
         cs = col.sdp()
         # inclusive windows when no used window needs exclusive bounds (see sdp_qplan.excl_mask)
         flags = 1 if (nw and PASS1_INCLUSIVE and not (plan.excl_mask & ((1 << nw) - 1))) else 0
+        info = {'cand': cand, 'counts': cand_counts, 'nseg': nseg, 'cap': cap, 'res_dev': res_dev}
+        if defer:
+            # sdp_pass1_batch task: launched with the other columns of its kind
+            info['task'] = nat.SdpPass1Task(cs, plan_dev.data_ptr(), work.data_ptr(), cand.data_ptr(),
+                                            cand_counts.data_ptr(), cap, res_dev.data_ptr(), grid, 0)
+            info['kind'] = (col.dtype, int(cap > 0), flags)
+            info['work'] = work
+            info['col'] = col
+            return info
         nat.annotate(_label(col), col_read_bytes(col))
         sdp.sdp_pass1(ctypes.byref(cs), ptr(plan_dev), ptr(work), work.numel(), ptr(cand), ptr(cand_counts), cap,
                       flags, ptr(res_dev), self._s())
-        return {'cand': cand, 'counts': cand_counts, 'nseg': nseg, 'cap': cap, 'res_dev': res_dev}
+        return info
+
+    def _pass1_run_batch(self, infos):
+        """Launch deferred pass-1 tasks (_pass1_launch(defer=True)): one
+        sdp_pass1_batch per (dtype, windowed, flags) kind; a kind with one
+        column takes the single-column entry."""
+        kinds = {}
+        for inf in infos:
+            kinds.setdefault(inf['kind'], []).append(inf)
+        keep = []
+        for (dtype, windowed, flags), grp in kinds.items():
+            if len(grp) == 1:
+                inf = grp[0]
+                t = inf['task']
+                nat.annotate(_label(inf['col']), col_read_bytes(inf['col']))
+                sdp.sdp_pass1(ctypes.byref(t.col), ctypes.c_void_p(t.d_plan), ctypes.c_void_p(t.d_work),
+                              inf['work'].numel(), ctypes.c_void_p(t.d_cand), ctypes.c_void_p(t.d_cand_counts),
+                              t.slot_capacity, flags, ctypes.c_void_p(t.d_result), self._s())
+                continue
+            arr = (nat.SdpPass1Task * len(grp))(*[inf['task'] for inf in grp])
+            d_tasks = self._h2d(np.frombuffer(bytearray(bytes(arr)), dtype=np.uint8))
+            nat.annotate(_label(grp[0]['col'], 'batch'), sum(col_read_bytes(inf['col']) for inf in grp))
+            sdp.sdp_pass1_batch(ptr(d_tasks), len(grp), dtype, windowed, flags, max(inf['task'].grid for inf in grp),
+                                self._s())
+            keep.append(d_tasks)
+        for inf in infos:
+            for k in ('task', 'kind', 'work', 'col'):
+                inf.pop(k, None)
+        return keep
 
     def pass1(self, col: DeviceColumn, plan_dev, plan):
         info = self._pass1_launch(col, plan_dev, plan)
@@ -966,9 +1005,13 @@ class Engine:
         rsz = ctypes.sizeof(nat.SdpPass1Result)
         res_all = self._bytes(len(cols) * rsz)
         infos = []
+        keep_tasks = None
         budget = [CAND_FULL_BUDGET]
         for i, col in enumerate(cols):
-            infos.append(self._pass1_launch(col, plans_dev[i * psz:], plans[i], res_all[i * rsz:], budget))
+            infos.append(self._pass1_launch(col, plans_dev[i * psz:], plans[i], res_all[i * rsz:], budget,
+                                            defer=PASS1_BATCH))
+        if PASS1_BATCH:
+            keep_tasks = self._pass1_run_batch(infos)     # (alive until the pass-1 readback below)
         # (sharded: the flag comes from the pooled sample, the same on every rank)
         sorted_idx = [i for i, c in enumerate(cols)
                       if mono_h[i] and c.kind == 'fixed' and (sharded or c.length >= SORTED_MIN_ROWS)]

@@ -50,7 +50,8 @@ def test_error_reporting_without_gpu():
 STRUCTS = {'sdp_column': 'SdpColumn', 'sdp_bytes_column': 'SdpBytesColumn', 'sdp_qplan': 'SdpQPlan',
            'sdp_pass1_result': 'SdpPass1Result', 'sdp_pass2_result': 'SdpPass2Result',
            'sdp_records': 'SdpRecords', 'sdp_heavy': 'SdpHeavy', 'sdp_chunk': 'SdpChunk',
-           'sdp_select_task': 'SdpSelectTask', 'sdp_compact_task': 'SdpCompactTask'}
+           'sdp_select_task': 'SdpSelectTask', 'sdp_compact_task': 'SdpCompactTask',
+           'sdp_pass1_task': 'SdpPass1Task'}
 
 
 def test_struct_layouts_match_c():
