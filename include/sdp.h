@@ -462,6 +462,10 @@ int64_t sdp_part_bucket_target(int32_t is_bytes, int32_t with_counts);
  * records.  Exactly one of col / bcol is non-NULL (as for every sdp_part_*). */
 int sdp_part_sample(const sdp_column *col, const sdp_bytes_column *bcol, int32_t n_sample,
                     uint64_t *d_h, const sdp_records *d_out, void *stream);
+/* sdp_part_sample of `ncols` fixed-width columns (d_cols: device array) in one
+ * launch; column c's n_sample hashes land in d_h[c * n_sample ..). */
+int sdp_part_sample_batch(const sdp_column *d_cols, int32_t ncols, int32_t n_sample, uint64_t *d_h,
+                          void *stream);
 /* phase 0: d_hist[b * grid + block] (u32) + heavy counts + d_stats[0];
  * phase 1: records scattered to d_out at d_offsets (exclusive scan of d_hist). */
 int sdp_part_rows(const sdp_column *col, const sdp_bytes_column *bcol, const sdp_heavy *heavy,

@@ -1453,8 +1453,7 @@ __global__ void __launch_bounds__(PT) part_compact_kernel(const uint64_t *src_a,
 }
 
 // ---- sample (heavy-key detection) ------------------------------------------------
-__global__ void part_sample_u64_kernel(sdp_column col, int32_t ns, uint64_t *out_h) {
-    const int j = blockIdx.x * blockDim.x + threadIdx.x;
+__device__ __forceinline__ void part_sample_u64_one(const sdp_column &col, int32_t ns, uint64_t *out_h, int j) {
     if (j >= ns) return;
     const int64_t n = col.length;
     const int64_t i = (int64_t)(((double)j + 0.5) * (double)n / (double)ns);
@@ -1465,6 +1464,13 @@ __global__ void part_sample_u64_kernel(sdp_column col, int32_t ns, uint64_t *out
         if (ok) h = mix64(k);
     }
     out_h[j] = h;
+}
+__global__ void part_sample_u64_kernel(sdp_column col, int32_t ns, uint64_t *out_h) {
+    part_sample_u64_one(col, ns, out_h, blockIdx.x * blockDim.x + threadIdx.x);
+}
+// every column's sample in one launch: blockIdx.y = column, out_h[c * ns ..)
+__global__ void part_sample_u64_batch_kernel(const sdp_column *cols, int32_t ns, uint64_t *out_h) {
+    part_sample_u64_one(cols[blockIdx.y], ns, out_h + (int64_t)blockIdx.y * ns, blockIdx.x * blockDim.x + threadIdx.x);
 }
 __global__ void part_sample_bytes_kernel(sdp_bytes_column col, int32_t ns, uint64_t *out_h, uint64_t *out_k0,
                                          uint64_t *out_k1, uint64_t *out_meta) {
@@ -1615,6 +1621,14 @@ int sdp_part_sample(const sdp_column *col, const sdp_bytes_column *bcol, int32_t
                            d_out->d_k1, d_out->d_meta);
     }
     return check_launch("part_sample");
+}
+
+int sdp_part_sample_batch(const sdp_column *d_cols, int32_t ncols, int32_t n_sample, uint64_t *d_h, void *stream) {
+    if (d_cols == nullptr || ncols < 1 || ncols > 65535 || n_sample < 1 || d_h == nullptr)
+        return set_error(SDP_EINVAL, "part_sample_batch: args");
+    hipLaunchKernelGGL(part_sample_u64_batch_kernel, dim3((n_sample + 255) / 256, ncols), dim3(256), 0,
+                       (hipStream_t)stream, d_cols, n_sample, d_h);
+    return check_launch("part_sample_batch");
 }
 
 int sdp_part_rows(const sdp_column *col, const sdp_bytes_column *bcol, const sdp_heavy *heavy, int32_t b1,

@@ -128,6 +128,7 @@ _SIGNATURES = {
     'sdp_quantile_refine_batch': (ctypes.c_int, [_P, _I32, _I32, _P, _I32, _P, _P]),
     'sdp_pass1': (ctypes.c_int, [_COL, _P, _P, _I64, _P, _P, _I64, _I32, _P, _P]),
     'sdp_pass1_batch': (ctypes.c_int, [_P, _I32, _I32, _I32, _I32, _I32, _P]),
+    'sdp_part_sample_batch': (ctypes.c_int, [_P, _I32, _I32, _P, _P]),
     'sdp_compact_candidates': (ctypes.c_int, [_P, _P, _I32, _I64, _P, _P, _P, _P]),
     'sdp_radix_hist': (ctypes.c_int, [_P, _P, _U64, _I32, _P, _P]),
     'sdp_radix_filter': (ctypes.c_int, [_P, _P, _U64, _I32, _P, _P, _P]),

@@ -55,7 +55,7 @@ BYTES_ONE_READ = os.environ.get('SDP_BYTES_TWO_READS', '0') != '1'
 # pass 1 with inclusive quantile windows where the plan allows (SDP_PASS1_EXCL=1: never, for A/B runs)
 PASS1_INCLUSIVE = os.environ.get('SDP_PASS1_EXCL', '0') != '1'
 # SDP_PASS1_BATCH=0: one sdp_pass1 launch per column instead of one sdp_pass1_batch per dtype
-PASS1_BATCH = os.environ.get('SDP_PASS1_BATCH', '0') != '0'
+PASS1_BATCH = os.environ.get('SDP_PASS1_BATCH', '1') != '0'
 CAND_FULL_BUDGET = 1 << 30   # bytes of room-for-every-row candidate slots per pass-1 batch
 
 # Test knob for the quantile edge paths (never set in production):
@@ -976,12 +976,17 @@ class Engine:
         if hcols:
             nsr = hn_each // world
             hs = self._u64(len(hcols) * nsr)
+            live = [i for i, col in enumerate(hcols) if col.length]
             for i, col in enumerate(hcols):
                 if col.length == 0:
                     hs[i * nsr:(i + 1) * nsr].fill_(-1)
-                    continue
-                cs = col.sdp()
-                sdp.sdp_part_sample(ctypes.byref(cs), None, nsr, ptr(hs[i * nsr:]), None, s)
+            if len(live) == len(hcols):                   # one launch for every column
+                d_hc = self._h2d(np.frombuffer(bytearray(b''.join(bytes(c.sdp()) for c in hcols)), dtype=np.uint8))
+                sdp.sdp_part_sample_batch(ptr(d_hc), len(hcols), nsr, ptr(hs), s)
+            else:
+                for i in live:
+                    cs = hcols[i].sdp()
+                    sdp.sdp_part_sample(ctypes.byref(cs), None, nsr, ptr(hs[i * nsr:]), None, s)
             if sharded:
                 hs = torch.cat([p.view(len(hcols), nsr) for p in self.comm.allgather(hs)], dim=1).contiguous()
             sdp.sdp_sort_small_batch(ptr(hs), hn_each, len(hcols), s)
