@@ -540,10 +540,31 @@ def corr_matrix(engine, table, columns, bundles):
     return pd.DataFrame(rho, index=list(columns), columns=list(columns))
 
 
+def _stats_frame(ldesc):
+    """pd.DataFrame({name: pd.Series(stats, dtype=object)}) (describe.py:102)
+    built in one piece: pandas aligns the columns' key sets to their union,
+    which is taken from one column per distinct key set (a 512-column table has
+    a handful), and the object matrix is filled directly -- 512 Series
+    alignments took ~60 ms."""
+    if not ldesc:
+        return pd.DataFrame({})
+    reps = {}
+    for k, v in ldesc.items():
+        reps.setdefault(tuple(v.keys()), k)
+    index = pd.DataFrame({k: pd.Series([None] * len(keys), index=list(keys), name=k, dtype=object)
+                          for keys, k in reps.items()}).index
+    pos = {key: i for i, key in enumerate(index)}
+    arr = np.empty((len(index), len(ldesc)), dtype=object)
+    arr[:] = np.nan
+    for j, v in enumerate(ldesc.values()):
+        for key, val in v.items():
+            arr[pos[key], j] = val
+    return pd.DataFrame(arr, index=index, columns=list(ldesc.keys()), dtype=object)
+
+
 def _assemble(ldesc, table_stats, nvar):
     """describe.py:102-133."""
-    variable_stats = pd.DataFrame({k: pd.Series(list(v.values()), index=list(v.keys()), name=k, dtype=object)
-                                   for k, v in ldesc.items()})
+    variable_stats = _stats_frame(ldesc)
     table_stats['nvar'] = nvar
     n = table_stats['n']
     n_missing = pd.to_numeric(variable_stats.loc['n_missing'], errors='coerce')

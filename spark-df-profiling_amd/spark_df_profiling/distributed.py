@@ -56,8 +56,8 @@ def exchange_fixed_groups(engine, tab, with_counts):
     owner = _owner_u64(keys, world)
     order = _owner_order(owner, world)
     keys = keys[order]
-    per = torch.zeros(world, dtype=torch.int64, device=engine.device).scatter_add_(0, owner, torch.ones_like(owner))
-    send = per.tolist()
+    bounds = torch.searchsorted(owner[order], torch.arange(world + 1, dtype=owner.dtype, device=engine.device))
+    send = (bounds[1:] - bounds[:-1]).tolist()
     recv = comm.alltoall_counts([send])[0]
     rkeys = comm.alltoallv_known(keys.contiguous(), send, recv)
     rcnt = None
@@ -125,19 +125,21 @@ def exchange_bytes_groups_batch(engine, tabs):
             o = col.offsets.to(torch.int64)
             starts = o[rows]
             lens = o[rows + 1] - starts
-        # groups and key bytes per owner, summed on the device (a host list of
-        # every group's length would cost seconds at 1e8 labels)
-        per = torch.zeros((2, world), dtype=torch.int64, device=engine.device)
-        per[0].scatter_add_(0, owner, torch.ones_like(owner))
-        per[1].scatter_add_(0, owner, lens)
+        # groups and key bytes per owner from the owner-sorted order: range
+        # bounds by searchsorted and a prefix sum of the lengths (a scatter_add
+        # into `world` counters serialised every group's atomic on a few
+        # addresses: 4.2 ms per 1.25e8-row step, profiles/r03q_*)
+        bounds = torch.searchsorted(owner, torch.arange(world + 1, dtype=owner.dtype, device=engine.device))
+        pref = torch.zeros(lens.numel() + 1, dtype=torch.int64, device=engine.device)
+        torch.cumsum(lens, 0, out=pref[1:])
+        per = torch.stack([bounds[1:] - bounds[:-1], pref[bounds[1:]] - pref[bounds[:-1]]])
         pers.append(per)
-        preps.append((tab, col, starts, lens, cnt))
+        preps.append((tab, col, starts, lens, cnt, pref[:-1]))
     allper = torch.stack(pers).cpu().tolist()                     # [column][groups | bytes][owner]
     payloads = []
-    for (tab, col, starts, lens, cnt), (send_groups, send_bytes) in zip(preps, allper):
+    for (tab, col, starts, lens, cnt, offs), (send_groups, send_bytes) in zip(preps, allper):
         # key bytes of every group, owner-major, packed by one native gather
         tot = sum(send_bytes)
-        offs = torch.cumsum(lens, 0) - lens
         payload = torch.empty(max(tot, 1), dtype=torch.uint8, device=engine.device)[:tot]
         if tot:
             sdp.sdp_gather_bytes(ptr(col.data), ptr(starts.contiguous()), ptr(lens.contiguous()), ptr(offs),
@@ -145,8 +147,8 @@ def exchange_bytes_groups_batch(engine, tabs):
         payloads.append(payload)
     recv = comm.alltoall_counts([row for pr in allper for row in pr])
     launched = []
-    for j, ((tab, col, starts, lens, cnt), (send_groups, send_bytes), payload) in enumerate(zip(preps, allper,
-                                                                                               payloads)):
+    for j, ((tab, col, starts, lens, cnt, _), (send_groups, send_bytes), payload) in enumerate(zip(preps, allper,
+                                                                                                  payloads)):
         recv_groups, recv_bytes = recv[2 * j], recv[2 * j + 1]
         # (length, count) pairs in one exchange, the key bytes in a second
         meta = torch.stack([lens, cnt], 1).contiguous().view(-1)
