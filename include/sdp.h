@@ -492,7 +492,9 @@ int sdp_part_recs(const sdp_records *in, int32_t is_bytes, const sdp_chunk *d_ch
  * keys, !with_counts): group totals in d_stats; buckets are sized for
  * sdp_part_bucket_target distinct keys, or (with_counts == 2) for 4 x that
  * when the hash bits run out (more than 2^30 rows on one device); with_counts
- * bit 4 (distinct only) claims slots with a single CAS (near-unique keys).  Otherwise the groups of f go to
+ * bit 4 (distinct only) claims slots with a single CAS (near-unique keys); a
+ * non-NULL d_ngroups then receives every bucket's group count (one launch over
+ * several columns' buckets).  Otherwise the groups of f go to
  * d_out_key/d_out_cnt at [d_starts[f], + d_ngroups[f]): fixed keys as the
  * order-preserving u64 key, byte keys as (hash tag << 40 | row + 1). */
 int sdp_part_dedup(const sdp_records *in, int32_t is_bytes, const sdp_bytes_column *bcol,

@@ -1224,10 +1224,13 @@ __device__ __forceinline__ uint32_t wave2_insert(uint64_t *T, uint64_t *O, const
     __builtin_amdgcn_wave_barrier();
     return fresh;
 }
+// ngroups (optional): groups of every bucket (a batch of columns' buckets in
+// one launch needs them per column)
 template <int MODE>
 __global__ void __launch_bounds__(WV_W * WAVE) part_dedup_u64_wave2_kernel(const uint64_t *in_h,
                                                                            const uint64_t *starts,
-                                                                           int64_t nbuckets, uint64_t *stats) {
+                                                                           int64_t nbuckets, uint32_t *ngroups,
+                                                                           uint64_t *stats) {
     __shared__ uint64_t tab[WV_W][WV_SLOTS];
     __shared__ uint64_t lst[WV_W][WV2_OVF];
     const int lane = lane_id(), w = threadIdx.x / WAVE;
@@ -1268,7 +1271,13 @@ __global__ void __launch_bounds__(WV_W * WAVE) part_dedup_u64_wave2_kernel(const
                 }
             }
             groups += fresh;
+            if (ngroups != nullptr) {
+                const uint32_t bucket = (uint32_t)wave_sum_u64(fresh);
+                if (lane == 0) ngroups[f] = bucket;
+            }
             __builtin_amdgcn_wave_barrier();
+        } else if (ngroups != nullptr && lane == 0) {
+            ngroups[f] = 0;
         }
         lo = lo_n;
         hi = hi_n;
@@ -1777,10 +1786,10 @@ int sdp_part_dedup(const sdp_records *in, int32_t is_bytes, const sdp_bytes_colu
         const bool v2 = e == nullptr || e[0] != '0';          // SDP_DEDUP_V2=0: the register-queue kernel
         if (v2 && (with_counts & 4))
             hipLaunchKernelGGL(part_dedup_u64_wave2_kernel<1>, dim3(wgrid), dim3(WV_W * WAVE), 0, s, in->d_k0,
-                               d_starts, nbuckets, d_stats);
+                               d_starts, nbuckets, d_ngroups, d_stats);
         else if (v2)
             hipLaunchKernelGGL(part_dedup_u64_wave2_kernel<0>, dim3(wgrid), dim3(WV_W * WAVE), 0, s, in->d_k0,
-                               d_starts, nbuckets, d_stats);
+                               d_starts, nbuckets, d_ngroups, d_stats);
         else if (with_counts & 4)       // near-unique keys: claim with one CAS, no read first
             hipLaunchKernelGGL(part_dedup_u64_wave_kernel<true>, dim3(wgrid), dim3(WV_W * WAVE), 0, s, in->d_k0,
                                d_starts, nbuckets, d_stats);

@@ -1245,11 +1245,18 @@ class Engine:
         if not live:
             return [None] * len(cols)
         flat = torch.cat([c['bsn_dev'] for c in live]).cpu().numpy().astype(np.int64)
-        off = 0
+        off, bsns = 0, []
         for c in live:
             m = c['bsn_dev'].numel()
-            self._group_middle(c, flat[off:off + m])
+            bsns.append(flat[off:off + m])
             off += m
+        # wide tables: columns of one geometry share their level-2 and
+        # de-duplication launches (_group_middle_fused); the rest one by one
+        fuse, single = self._fusable(live, bsns)
+        for grp in fuse:
+            self._group_middle_fused([live[i] for i in grp], [bsns[i] for i in grp])
+        for i in single:
+            self._group_middle(live[i], bsns[i])
         sizes = [c['stats_dev'].numel() for c in live]
         allst = self._host_u64(torch.cat([c['stats_dev'] for c in live]))
         out, off, it = [], 0, iter(zip(live, sizes))
@@ -1410,6 +1417,103 @@ class Engine:
         ctx.update({'starts': starts, 'ngroups': ngroups, 'out_key': out_key, 'out_cnt': out_cnt, 'nfinal': nfinal})
         del ctx['o1'], ctx['bsn_dev']
         ctx['stats_dev'] = torch.cat([stats, hcnt[:hv['n']]]) if hv else stats
+
+    FUSE_MIN_COLS = 8                  # columns of one geometry before their stages are fused
+    FUSE_BYTES = 32 << 30              # two 8-byte record buffers of a fused group alive at once
+
+    def _fusable(self, ctxs, bsns):
+        """Partition group_batch's contexts into groups whose level-2 count,
+        scatter and de-duplication run as one launch each (fixed keys,
+        distinct only, same (b1, b2), a level 2 and records, under FUSE_BYTES)
+        and singles."""
+        by, single = {}, []
+        for i, (c, bs) in enumerate(zip(ctxs, bsns)):
+            if c['isb'] or c['with_counts'] or c['large'] or c['b2'] == 0 or int(bs[-1]) == 0:
+                single.append(i)
+            else:
+                by.setdefault((c['b1'], c['b2'], id(c['col']) in self._near_unique), []).append(i)
+        fuse = []
+        for key, idx in by.items():
+            if len(idx) < self.FUSE_MIN_COLS:
+                single += idx
+                continue
+            grp, held = [], 0
+            for i in idx:
+                need = 16 * int(bsns[i][-1])
+                if grp and held + need > self.FUSE_BYTES:
+                    fuse.append(grp)
+                    grp, held = [], 0
+                grp.append(i)
+                held += need
+            fuse.append(grp)
+        single += [g[0] for g in fuse if len(g) == 1]
+        return [g for g in fuse if len(g) > 1], sorted(single)
+
+    def _group_middle_fused(self, ctxs, bsns):
+        """_group_middle of several fixed-key, distinct-only columns of one
+        (b1, b2): their level-1 scatters write into one record buffer (column c
+        from base_c), the level-2 chunk tables are concatenated (histogram
+        slots offset per column), so ONE level-2 count, ONE scan, ONE level-2
+        scatter, ONE gather of final-bucket starts and ONE de-duplication launch
+        (per-bucket group counts, summed per column on the device) serve them
+        all.  Each context then carries the same statistics vector as
+        _group_middle leaves."""
+        s = self._s()
+        b1, b2 = ctxs[0]['b1'], ctxs[0]['b2']
+        nb1, nb2 = 1 << b1, 1 << b2
+        nrecs = [int(bs[-1]) for bs in bsns]
+        base = np.concatenate([[0], np.cumsum(nrecs)]).astype(np.int64)
+        total = int(base[-1])
+        r1, keep1 = self._records(total, False)
+        ch_all, sidx_all, hb = [], [], 0
+        for ctx, bs, b0 in zip(ctxs, bsns, base[:-1]):
+            o1 = ctx['o1']
+            nat.annotate(_label(ctx['col'], 'scatter'), ctx['rb'] + int(bs[-1]) * 8)
+            rc = nat.SdpRecords(keep1[0].data_ptr() + 8 * int(b0), None, None)
+            sdp.sdp_part_rows(self._gref(ctx), None, ctypes.byref(ctx['hv']['struct']) if ctx['hv'] else None, b1, 1,
+                              None, ptr(o1), ctypes.byref(rc), ptr(ctx['hcnt']), ptr(ctx['stats']), s)
+            sizes = np.diff(bs)
+            nch = -(-sizes // PART_CHUNK)
+            k0 = np.concatenate([[0], np.cumsum(nch)[:-1]]).astype(np.int64)
+            K = int(nch.sum())
+            bof = np.repeat(np.arange(nb1), nch)
+            j = np.arange(K, dtype=np.int64) - k0[bof]
+            ch = np.empty((K, 4), dtype=np.int64)
+            ch[:, 0] = b0 + bs[bof] + j * PART_CHUNK
+            ch[:, 1] = b0 + np.minimum(bs[bof + 1], bs[bof] + j * PART_CHUNK + PART_CHUNK)
+            ch[:, 2] = hb + nb2 * k0[bof] + j
+            ch[:, 3] = nch[bof]
+            ch_all.append(ch)
+            sidx_all.append(hb + (nb2 * k0[:, None] + np.arange(nb2)[None, :] * nch[:, None]).reshape(-1))
+            hb += nb2 * K
+            del ctx['o1'], ctx['bsn_dev']
+        ch = np.concatenate(ch_all)
+        chunks = self._h2d(ch)
+        h2 = torch.empty(hb, dtype=torch.int32, device=self.device)
+        nat.annotate('u64/count', total * 8)
+        sdp.sdp_part_recs(ctypes.byref(r1), 0, ptr(chunks), len(ch), b1, b2, 0, ptr(h2), None, None, s)
+        o2 = self._scan(h2)
+        rf, keepf = self._records(total, False)
+        nat.annotate('u64/scatter', 2 * total * 8)
+        sdp.sdp_part_recs(ctypes.byref(r1), 0, ptr(chunks), len(ch), b1, b2, 1, None, ptr(o2), ctypes.byref(rf), s)
+        del keep1, r1, h2
+        starts = o2[self._h2d(np.append(np.concatenate(sidx_all), hb))].contiguous()
+        nfinal = nb1 * nb2
+        nf = nfinal * len(ctxs)
+        ngroups = torch.empty(nf, dtype=torch.int32, device=self.device)
+        stats = self._u64(68, zero=True)
+        nat.annotate('u64', total * 8)
+        direct = 4 if id(ctxs[0]['col']) in self._near_unique else 0
+        sdp.sdp_part_dedup(ctypes.byref(rf), 0, None, ptr(starts), nf, direct, None, None, ptr(ngroups), ptr(stats), s)
+        del keepf, rf
+        per_col = ngroups.view(len(ctxs), nfinal).to(torch.int64).sum(1)
+        for ci, ctx in enumerate(ctxs):
+            st = ctx['stats']
+            st[4] += per_col[ci]                     # (the count pass left 4..67 at zero)
+            st[3] |= stats[3]                        # a full table anywhere: every fused column recounts
+            hv = ctx['hv']
+            ctx['stats_dev'] = torch.cat([st, ctx['hcnt'][:hv['n']]]) if hv else st
+            ctx.update({'starts': None, 'ngroups': None, 'out_key': None, 'out_cnt': None, 'nfinal': nfinal})
 
     def _group_end(self, ctx, both, dense):
         """The tab dict from the host copy of stats_dev (see group)."""
