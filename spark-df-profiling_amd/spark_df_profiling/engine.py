@@ -1420,6 +1420,7 @@ class Engine:
 
     FUSE_MIN_COLS = 8                  # columns of one geometry before their stages are fused
     FUSE_BYTES = 32 << 30              # two 8-byte record buffers of a fused group alive at once
+    FUSE_MAX_RECS = 1 << 26            # larger columns fill the GPU alone (and recycle their buffers)
 
     def _fusable(self, ctxs, bsns):
         """Partition group_batch's contexts into groups whose level-2 count,
@@ -1428,7 +1429,8 @@ class Engine:
         and singles."""
         by, single = {}, []
         for i, (c, bs) in enumerate(zip(ctxs, bsns)):
-            if c['isb'] or c['with_counts'] or c['large'] or c['b2'] == 0 or int(bs[-1]) == 0:
+            if (c['isb'] or c['with_counts'] or c['large'] or c['b2'] == 0 or int(bs[-1]) == 0
+                    or int(bs[-1]) > self.FUSE_MAX_RECS):
                 single.append(i)
             else:
                 by.setdefault((c['b1'], c['b2'], id(c['col']) in self._near_unique), []).append(i)
