@@ -1467,29 +1467,37 @@ class Engine:
         base = np.concatenate([[0], np.cumsum(nrecs)]).astype(np.int64)
         total = int(base[-1])
         r1, keep1 = self._records(total, False)
-        ch_all, sidx_all, hb = [], [], 0
         for ctx, bs, b0 in zip(ctxs, bsns, base[:-1]):
-            o1 = ctx['o1']
             nat.annotate(_label(ctx['col'], 'scatter'), ctx['rb'] + int(bs[-1]) * 8)
             rc = nat.SdpRecords(keep1[0].data_ptr() + 8 * int(b0), None, None)
             sdp.sdp_part_rows(self._gref(ctx), None, ctypes.byref(ctx['hv']['struct']) if ctx['hv'] else None, b1, 1,
-                              None, ptr(o1), ctypes.byref(rc), ptr(ctx['hcnt']), ptr(ctx['stats']), s)
-            sizes = np.diff(bs)
-            nch = -(-sizes // PART_CHUNK)
-            k0 = np.concatenate([[0], np.cumsum(nch)[:-1]]).astype(np.int64)
-            K = int(nch.sum())
-            bof = np.repeat(np.arange(nb1), nch)
-            j = np.arange(K, dtype=np.int64) - k0[bof]
-            ch = np.empty((K, 4), dtype=np.int64)
-            ch[:, 0] = b0 + bs[bof] + j * PART_CHUNK
-            ch[:, 1] = b0 + np.minimum(bs[bof + 1], bs[bof] + j * PART_CHUNK + PART_CHUNK)
-            ch[:, 2] = hb + nb2 * k0[bof] + j
-            ch[:, 3] = nch[bof]
-            ch_all.append(ch)
-            sidx_all.append(hb + (nb2 * k0[:, None] + np.arange(nb2)[None, :] * nch[:, None]).reshape(-1))
-            hb += nb2 * K
+                              None, ptr(ctx['o1']), ctypes.byref(rc), ptr(ctx['hcnt']), ptr(ctx['stats']), s)
             del ctx['o1'], ctx['bsn_dev']
-        ch = np.concatenate(ch_all)
+        # every column's level-2 chunk table at once ([column, L1 bucket] arrays):
+        # chunks of <= PART_CHUNK records, ordered (column, bucket, chunk); the
+        # histogram slot of (column, bucket, sub-bucket, chunk) is
+        # hb[column] + nb2 * k0 + sub * nch + j
+        C = len(ctxs)
+        bs = np.stack(bsns)                                          # [C, nb1 + 1], column-local
+        sizes = np.diff(bs, axis=1)
+        nch = -(-sizes // PART_CHUNK)                                # [C, nb1]
+        Kc = nch.sum(1)
+        k0 = np.cumsum(nch, axis=1) - nch                            # column-local first chunk of each bucket
+        hbc = np.concatenate([[0], np.cumsum(nb2 * Kc)[:-1]]).astype(np.int64)
+        hb = int((nb2 * Kc).sum())
+        flat_n = nch.reshape(-1)
+        cb = np.repeat(np.arange(C * nb1), flat_n)                   # (column, bucket) of every chunk
+        first = np.cumsum(flat_n) - flat_n
+        j = np.arange(int(flat_n.sum()), dtype=np.int64) - first[cb]
+        col_of, b_of = cb // nb1, cb % nb1
+        start0 = base[col_of] + bs[col_of, b_of] + j * PART_CHUNK
+        ch = np.empty((len(cb), 4), dtype=np.int64)
+        ch[:, 0] = start0
+        ch[:, 1] = np.minimum(base[col_of] + bs[col_of, b_of + 1], start0 + PART_CHUNK)
+        ch[:, 2] = hbc[col_of] + nb2 * k0[col_of, b_of] + j
+        ch[:, 3] = nch[col_of, b_of]
+        sidx = (hbc[:, None, None] + nb2 * k0[:, :, None]
+                + np.arange(nb2)[None, None, :] * nch[:, :, None]).reshape(-1)
         chunks = self._h2d(ch)
         h2 = torch.empty(hb, dtype=torch.int32, device=self.device)
         nat.annotate('u64/count', total * 8)
@@ -1499,7 +1507,7 @@ class Engine:
         nat.annotate('u64/scatter', 2 * total * 8)
         sdp.sdp_part_recs(ctypes.byref(r1), 0, ptr(chunks), len(ch), b1, b2, 1, None, ptr(o2), ctypes.byref(rf), s)
         del keep1, r1, h2
-        starts = o2[self._h2d(np.append(np.concatenate(sidx_all), hb))].contiguous()
+        starts = o2[self._h2d(np.append(sidx, hb))].contiguous()
         nfinal = nb1 * nb2
         nf = nfinal * len(ctxs)
         ngroups = torch.empty(nf, dtype=torch.int32, device=self.device)
