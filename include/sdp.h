@@ -449,6 +449,29 @@ int sdp_pass2_count(const sdp_column *col, double mean, const double *d_edges, i
                     sdp_pass2_result *d_result, uint64_t *d_hist, const sdp_heavy *heavy, int32_t b1,
                     uint32_t *d_part_hist, uint64_t *d_heavy_counts, uint64_t *d_stats, void *stream);
 
+/* One column of sdp_pass2_count_batch: sdp_pass2_count's arguments (the
+ * workspace of sdp_pass2_count_workspace_bytes; grid and rows_per_block as
+ * sdp_part_rows_per_block gives them for the column's length). */
+typedef struct sdp_pass2_task {
+    sdp_column         col;
+    const double      *d_edges;
+    double             mean, hi_t, lo_t;
+    void              *d_work;
+    sdp_pass2_result  *d_result;
+    uint64_t          *d_hist;
+    sdp_heavy          heavy;            /* d_h and n used (fixed keys) */
+    uint32_t          *d_part_hist;
+    uint64_t          *d_heavy_counts;
+    uint64_t          *d_stats;
+    int64_t            rows_per_block;
+    int32_t            bins, edges_monotone, b1, grid;
+} sdp_pass2_task;
+
+/* sdp_pass2_count of `ntasks` columns of one dtype, bin count and edge kind
+ * in two launches (wide tables); d_tasks lives in device memory. */
+int sdp_pass2_count_batch(const sdp_pass2_task *d_tasks, int32_t ntasks, int32_t dtype, int32_t bins,
+                          int32_t edges_monotone, int32_t max_grid, void *stream);
+
 /* Packs the key bytes of n groups -- bytes [d_starts[i], d_starts[i] + d_lens[i])
  * of d_data -- at d_out + d_offs[i] (the sharded string exchange's payload). */
 int sdp_gather_bytes(const uint8_t *d_data, const int64_t *d_starts, const int64_t *d_lens,

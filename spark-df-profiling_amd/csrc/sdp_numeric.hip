@@ -1356,18 +1356,20 @@ struct P2CountLds {
     uint32_t hist[MAXB];
 };
 
-template <typename T, bool SMALL, bool MONO, int NB = P2_SMALL_BINS>
-__global__ void __launch_bounds__(P2_BLOCK, 4) pass2_count_kernel(sdp_column col, double mean, const double *edges,
-                                                               int bins, int monotone, double hi_t, double lo_t,
-                                                               double *part_mad, uint64_t *part_cnt, HeavyArg heavy,
-                                                               int b1, int64_t rows_per_block, uint32_t *hist,
-                                                               uint64_t *heavy_counts, uint64_t *stats) {
+// block g of a G-block grid (the batched launch runs several columns' grids
+// side by side, blockIdx.y = column)
+template <typename T, bool SMALL, bool MONO, int NB>
+__device__ __forceinline__ void pass2_count_body(const sdp_column &col, double mean, const double *edges, int bins,
+                                                 int monotone, double hi_t, double lo_t, double *part_mad,
+                                                 uint64_t *part_cnt, const HeavyArg &heavy, int b1,
+                                                 int64_t rows_per_block, uint32_t *hist, uint64_t *heavy_counts,
+                                                 uint64_t *stats, const int G, const int g) {
     constexpr int VPT = Vec16<T>::N;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     __shared__ P2CountLds cl;
     double *s_edges = (double *)smem;
     uint32_t *s_hist = (uint32_t *)(smem + sizeof(double) * bins);
-    const int G = gridDim.x, g = blockIdx.x, t = threadIdx.x;
+    const int t = threadIdx.x;
     const int nb = 1 << b1;
     const int shift = 64 - b1;
     for (int i = t; i < bins; i += blockDim.x) { s_edges[i] = edges[i]; s_hist[i] = 0; }
@@ -1486,10 +1488,42 @@ __global__ void __launch_bounds__(P2_BLOCK, 4) pass2_count_kernel(sdp_column col
     block_add_u64(rows, &stats[0]);
     block_add_u64(special, &stats[1]);
 }
+template <typename T, bool SMALL, bool MONO, int NB = P2_SMALL_BINS>
+__global__ void __launch_bounds__(P2_BLOCK, 4) pass2_count_kernel(sdp_column col, double mean, const double *edges,
+                                                               int bins, int monotone, double hi_t, double lo_t,
+                                                               double *part_mad, uint64_t *part_cnt, HeavyArg heavy,
+                                                               int b1, int64_t rows_per_block, uint32_t *hist,
+                                                               uint64_t *heavy_counts, uint64_t *stats) {
+    pass2_count_body<T, SMALL, MONO, NB>(col, mean, edges, bins, monotone, hi_t, lo_t, part_mad, part_cnt, heavy, b1,
+                                         rows_per_block, hist, heavy_counts, stats, (int)gridDim.x, (int)blockIdx.x);
+}
+template <typename T, bool SMALL, bool MONO, int NB = P2_SMALL_BINS>
+__global__ void __launch_bounds__(P2_BLOCK, 4) pass2_count_batch_kernel(const sdp_pass2_task *tasks) {
+    const sdp_pass2_task &tk = tasks[blockIdx.y];
+    if ((int)blockIdx.x >= tk.grid) return;
+    const HeavyArg hv{tk.heavy.d_h, nullptr, nullptr, nullptr, tk.heavy.n};
+    double *pm = (double *)tk.d_work;
+    uint64_t *pc = (uint64_t *)((char *)tk.d_work + (int64_t)tk.grid * sizeof(double));
+    pass2_count_body<T, SMALL, MONO, NB>(tk.col, tk.mean, tk.d_edges, tk.bins, tk.edges_monotone, tk.hi_t, tk.lo_t,
+                                         pm, pc, hv, tk.b1, tk.rows_per_block, tk.d_part_hist, tk.d_heavy_counts,
+                                         tk.d_stats, tk.grid, (int)blockIdx.x);
+}
 
+__device__ __forceinline__ void pass2_merge_body(const double *part_mad, const uint64_t *part_cnt, int grid,
+                                                 int bins, sdp_pass2_result *out, uint64_t *hist);
 __global__ void __launch_bounds__(MERGE_T) pass2_merge_kernel(const double *part_mad, const uint64_t *part_cnt,
                                                               int grid, int bins, sdp_pass2_result *out,
                                                               uint64_t *hist) {
+    pass2_merge_body(part_mad, part_cnt, grid, bins, out, hist);
+}
+__global__ void __launch_bounds__(MERGE_T) pass2_merge_batch_kernel(const sdp_pass2_task *tasks) {
+    const sdp_pass2_task &tk = tasks[blockIdx.x];
+    pass2_merge_body((const double *)tk.d_work,
+                     (const uint64_t *)((const char *)tk.d_work + (int64_t)tk.grid * sizeof(double)), tk.grid,
+                     tk.bins, tk.d_result, tk.d_hist);
+}
+__device__ __forceinline__ void pass2_merge_body(const double *part_mad, const uint64_t *part_cnt, int grid,
+                                                 int bins, sdp_pass2_result *out, uint64_t *hist) {
     __shared__ double sh[MERGE_T];
     __shared__ uint64_t su[MERGE_T];
     const int stride = 3 + bins;
@@ -2134,6 +2168,32 @@ extern "C" int sdp_pass2_count(const sdp_column *col, double mean, const double 
     if (rc) return rc;
     hipLaunchKernelGGL(pass2_merge_kernel, dim3(1), dim3(MERGE_T), 0, s, pm, pc, grid, bins, d_result, d_hist);
     return check_launch("pass2_merge_kernel");
+}
+
+extern "C" int sdp_pass2_count_batch(const sdp_pass2_task *d_tasks, int32_t ntasks, int32_t dtype, int32_t bins,
+                                     int32_t edges_monotone, int32_t max_grid, void *stream) {
+    if (d_tasks == nullptr || ntasks < 1 || ntasks > 65535 || max_grid < 1 || bins < 2 || bins > 8192)
+        return set_error(SDP_EINVAL, "sdp_pass2_count_batch: args");
+    if (elem_size(dtype) <= 0) return set_error(SDP_EINVAL, "sdp_pass2_count_batch: dtype %d", dtype);
+    const size_t lds = (size_t)bins * (sizeof(double) + sizeof(uint32_t)) + 16;
+    hipStream_t s = (hipStream_t)stream;
+    const dim3 grid(max_grid, ntasks);
+#define SDP_P2CB(SM, MO, ...) \
+    hipLaunchKernelGGL((pass2_count_batch_kernel<T, SM, MO, ##__VA_ARGS__>), grid, dim3(P2_BLOCK), lds, s, d_tasks)
+    if (bins <= 10 && edges_monotone) {
+        SDP_DISPATCH_NUMERIC(dtype, SDP_P2CB(true, true, 10));
+    } else if (bins <= P2_SMALL_BINS && edges_monotone) {
+        SDP_DISPATCH_NUMERIC(dtype, SDP_P2CB(true, true));
+    } else if (bins <= P2_SMALL_BINS) {
+        SDP_DISPATCH_NUMERIC(dtype, SDP_P2CB(true, false));
+    } else {
+        SDP_DISPATCH_NUMERIC(dtype, SDP_P2CB(false, false));
+    }
+#undef SDP_P2CB
+    int rc = check_launch("pass2_count_batch_kernel");
+    if (rc) return rc;
+    hipLaunchKernelGGL(pass2_merge_batch_kernel, dim3(ntasks), dim3(MERGE_T), 0, s, d_tasks);
+    return check_launch("pass2_merge_batch_kernel");
 }
 
 extern "C" int sdp_pass2(const sdp_column *col, double mean, const double *d_edges, int32_t bins,

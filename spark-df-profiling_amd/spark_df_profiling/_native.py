@@ -99,6 +99,15 @@ class SdpPass1Task(ctypes.Structure):
                 ('d_result', ctypes.c_void_p), ('grid', ctypes.c_int32), ('_pad', ctypes.c_int32)]
 
 
+class SdpPass2Task(ctypes.Structure):
+    _fields_ = [('col', SdpColumn), ('d_edges', ctypes.c_void_p), ('mean', ctypes.c_double), ('hi_t', ctypes.c_double),
+                ('lo_t', ctypes.c_double), ('d_work', ctypes.c_void_p), ('d_result', ctypes.c_void_p),
+                ('d_hist', ctypes.c_void_p), ('heavy', SdpHeavy), ('d_part_hist', ctypes.c_void_p),
+                ('d_heavy_counts', ctypes.c_void_p), ('d_stats', ctypes.c_void_p), ('rows_per_block', ctypes.c_int64),
+                ('bins', ctypes.c_int32), ('edges_monotone', ctypes.c_int32), ('b1', ctypes.c_int32),
+                ('grid', ctypes.c_int32)]
+
+
 class SdpPass2Result(ctypes.Structure):
     _fields_ = [('abs_dev_sum', ctypes.c_double), ('n_high', ctypes.c_uint64), ('n_low', ctypes.c_uint64),
                 ('n_unbinned', ctypes.c_uint64)]
@@ -129,6 +138,7 @@ _SIGNATURES = {
     'sdp_pass1': (ctypes.c_int, [_COL, _P, _P, _I64, _P, _P, _I64, _I32, _P, _P]),
     'sdp_pass1_batch': (ctypes.c_int, [_P, _I32, _I32, _I32, _I32, _I32, _P]),
     'sdp_part_sample_batch': (ctypes.c_int, [_P, _I32, _I32, _P, _P]),
+    'sdp_pass2_count_batch': (ctypes.c_int, [_P, _I32, _I32, _I32, _I32, _I32, _P]),
     'sdp_compact_candidates': (ctypes.c_int, [_P, _P, _I32, _I64, _P, _P, _P, _P]),
     'sdp_radix_hist': (ctypes.c_int, [_P, _P, _U64, _I32, _P, _P]),
     'sdp_radix_filter': (ctypes.c_int, [_P, _P, _U64, _I32, _P, _P, _P]),

@@ -56,6 +56,8 @@ BYTES_ONE_READ = os.environ.get('SDP_BYTES_TWO_READS', '0') != '1'
 PASS1_INCLUSIVE = os.environ.get('SDP_PASS1_EXCL', '0') != '1'
 # SDP_PASS1_BATCH=0: one sdp_pass1 launch per column instead of one sdp_pass1_batch per dtype
 PASS1_BATCH = os.environ.get('SDP_PASS1_BATCH', '1') != '0'
+# SDP_PASS2_BATCH=0: one sdp_pass2_count launch per column on wide tables too
+PASS2_BATCH = os.environ.get('SDP_PASS2_BATCH', '0') != '0'
 CAND_FULL_BUDGET = 1 << 30   # bytes of room-for-every-row candidate slots per pass-1 batch
 
 # Test knob for the quantile edge paths (never set in production):
@@ -694,6 +696,7 @@ class Engine:
         rsz = ctypes.sizeof(nat.SdpPass2Result)
         count_ctx = count_ctx or {}
         outs = []
+        batched = []               # (kind, SdpPass2Task, col): counted columns launched together below
         for i, (col, mean, edges, hi_t, lo_t) in enumerate(items):
             bins = len(edges)
             e = self._h2d(np.array([float(x) for x in edges], dtype=np.float64))
@@ -707,11 +710,21 @@ class Engine:
                 work = self._bytes(max(sdp.sdp_pass2_count_workspace_bytes(col.length, bins),
                                        sdp.sdp_pass2_workspace_bytes(col.length, col.dtype, bins)))
                 hv = ctx['hv']
-                nat.annotate(_label(col), col_read_bytes(col))
-                sdp.sdp_pass2_count(ctypes.byref(cs), float(mean), ptr(e), bins, int(mono), float(hi_t), float(lo_t),
-                                    ptr(work), work.numel(), ptr(res), ptr(hist),
-                                    ctypes.byref(hv['struct']) if hv else None, ctx['b1'], ptr(ctx['h1']),
-                                    ptr(ctx['hcnt']), ptr(ctx['stats']), s)
+                if PASS2_BATCH and len(items) >= 8:
+                    rpb = sdp.sdp_part_rows_per_block(col.length, 0)
+                    grid = max(1, -(-col.length // rpb))
+                    task = nat.SdpPass2Task(cs, e.data_ptr(), float(mean), float(hi_t), float(lo_t), work.data_ptr(),
+                                            res.data_ptr(), hist.data_ptr(),
+                                            hv['struct'] if hv else nat.SdpHeavy(None, None, None, None, 0, 0),
+                                            ctx['h1'].data_ptr(), ctx['hcnt'].data_ptr(), ctx['stats'].data_ptr(),
+                                            rpb, bins, int(mono), ctx['b1'], grid)
+                    batched.append(((col.dtype, bins, int(mono)), task, col))
+                else:
+                    nat.annotate(_label(col), col_read_bytes(col))
+                    sdp.sdp_pass2_count(ctypes.byref(cs), float(mean), ptr(e), bins, int(mono), float(hi_t),
+                                        float(lo_t), ptr(work), work.numel(), ptr(res), ptr(hist),
+                                        ctypes.byref(hv['struct']) if hv else None, ctx['b1'], ptr(ctx['h1']),
+                                        ptr(ctx['hcnt']), ptr(ctx['stats']), s)
                 self._counted[id(col)] = ctx
             else:
                 work = self._bytes(sdp.sdp_pass2_workspace_bytes(col.length, col.dtype, bins))
@@ -719,6 +732,18 @@ class Engine:
                 sdp.sdp_pass2(ctypes.byref(cs), float(mean), ptr(e), bins, int(mono), float(hi_t), float(lo_t),
                               ptr(work), work.numel(), ptr(res), ptr(hist), s)
             outs.append((res, hist, e, work))
+        keep_tasks = []
+        if batched:
+            # wide tables: one sdp_pass2_count_batch per (dtype, bins, edge kind)
+            kinds = {}
+            for kind, task, col in batched:
+                kinds.setdefault(kind, []).append((task, col))
+            for (dtype, bins, mono), grp in kinds.items():
+                arr = (nat.SdpPass2Task * len(grp))(*[t for t, _ in grp])
+                d_tasks = self._h2d(np.frombuffer(bytearray(bytes(arr)), dtype=np.uint8))
+                nat.annotate(_label(grp[0][1], 'batch'), sum(col_read_bytes(c) for _, c in grp))
+                sdp.sdp_pass2_count_batch(ptr(d_tasks), len(grp), dtype, bins, mono, max(t.grid for t, _ in grp), s)
+                keep_tasks.append(d_tasks)
         if not self.comm.sharded:
             raw = torch.cat([t for res, hist, _, _ in outs for t in (res[:rsz], hist.view(torch.uint8))]).cpu().numpy()
             result, off = [], 0
