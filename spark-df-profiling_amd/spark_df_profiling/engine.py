@@ -57,7 +57,7 @@ PASS1_INCLUSIVE = os.environ.get('SDP_PASS1_EXCL', '0') != '1'
 # SDP_PASS1_BATCH=0: one sdp_pass1 launch per column instead of one sdp_pass1_batch per dtype
 PASS1_BATCH = os.environ.get('SDP_PASS1_BATCH', '1') != '0'
 # SDP_PASS2_BATCH=0: one sdp_pass2_count launch per column on wide tables too
-PASS2_BATCH = os.environ.get('SDP_PASS2_BATCH', '0') != '0'
+PASS2_BATCH = os.environ.get('SDP_PASS2_BATCH', '1') != '0'
 CAND_FULL_BUDGET = 1 << 30   # bytes of room-for-every-row candidate slots per pass-1 batch
 
 # Test knob for the quantile edge paths (never set in production):
