@@ -495,6 +495,22 @@ int sdp_part_rows(const sdp_column *col, const sdp_bytes_column *bcol, const sdp
                   int32_t b1, int32_t phase, uint32_t *d_hist, const uint64_t *d_offsets,
                   const sdp_records *d_out, uint64_t *d_heavy_counts, uint64_t *d_stats,
                   void *stream);
+
+/* One column of sdp_part_rows_batch (phase 1, fixed keys): the level-1 scatter
+ * of `col` with its scanned counts d_offsets into d_out; grid and
+ * rows_per_block as sdp_part_rows_per_block gives them. */
+typedef struct sdp_rows_task {
+    sdp_column        col;
+    sdp_heavy         heavy;            /* d_h and n used */
+    const uint64_t   *d_offsets;
+    uint64_t         *d_out;
+    int64_t           rows_per_block;
+    int32_t           b1, grid;
+} sdp_rows_task;
+
+/* The level-1 scatters of `ntasks` columns of one dtype (f64/f32/i64/i32) in
+ * one launch (wide tables); d_tasks lives in device memory. */
+int sdp_part_rows_batch(const sdp_rows_task *d_tasks, int32_t ntasks, int32_t dtype, int32_t max_grid, void *stream);
 /* Byte columns, one read of the strings (replaces sdp_part_rows phase 0 + 1 for
  * bcol): every wave of every workgroup compacts the records of its strip of
  * rows to d_out at the strip's first row position (d_out holds length records),

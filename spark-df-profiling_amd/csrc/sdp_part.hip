@@ -288,17 +288,19 @@ __global__ void __launch_bounds__(CT) part_count_rows_u64_kernel(sdp_column col,
     block_add_u64(special, &stats[1]);
 }
 
+// block bx of a G-block grid (the batched launch runs several columns' grids
+// side by side, blockIdx.y = column)
 template <typename T>
-__global__ void __launch_bounds__(ST) part_scatter_rows_u64_kernel(sdp_column col, HeavyArg heavy, int b1,
-                                                                   int64_t rows_per_block, const uint64_t *offs,
-                                                                   uint64_t *out_h, int xcd_map) {
+__device__ __forceinline__ void scatter_rows_u64_body(const sdp_column &col, const HeavyArg &heavy, int b1,
+                                                      int64_t rows_per_block, const uint64_t *offs, uint64_t *out_h,
+                                                      int xcd_map, const int G, const int bx) {
     __shared__ ScatterLds s;
-    const int G = gridDim.x, t = threadIdx.x;
+    const int t = threadIdx.x;
     // XCD-aware: workgroups are dealt to the 8 XCDs round robin; with the map,
     // one XCD's workgroups take consecutive row blocks, so in every bucket the
     // runs it writes at once are adjacent (one L2 sees both halves of a line
     // two blocks share, and the XCD's write stream stays within fewer pages)
-    const int g = (xcd_map && G % 8 == 0) ? (int)((blockIdx.x % 8) * (G / 8) + blockIdx.x / 8) : (int)blockIdx.x;
+    const int g = (xcd_map && G % 8 == 0) ? (int)((bx % 8) * (G / 8) + bx / 8) : bx;
     const int nb = 1 << b1;
     const int shift = 64 - b1;
     const int64_t r0 = (int64_t)g * rows_per_block;
@@ -349,6 +351,22 @@ __global__ void __launch_bounds__(ST) part_scatter_rows_u64_kernel(sdp_column co
         }
         lds_barrier();
     }
+}
+
+template <typename T>
+__global__ void __launch_bounds__(ST) part_scatter_rows_u64_kernel(sdp_column col, HeavyArg heavy, int b1,
+                                                                   int64_t rows_per_block, const uint64_t *offs,
+                                                                   uint64_t *out_h, int xcd_map) {
+    scatter_rows_u64_body<T>(col, heavy, b1, rows_per_block, offs, out_h, xcd_map, (int)gridDim.x, (int)blockIdx.x);
+}
+template <typename T>
+__global__ void __launch_bounds__(ST) part_scatter_rows_u64_batch_kernel(const sdp_rows_task *tasks, int xcd_map) {
+    const sdp_rows_task &tk = tasks[blockIdx.y];
+    if ((int)blockIdx.x >= tk.grid) return;
+    const HeavyArg hv{tk.heavy.d_h, nullptr, nullptr, nullptr, tk.heavy.n};
+    // (the XCD map needs the column's grid to be the launch's x extent)
+    scatter_rows_u64_body<T>(tk.col, hv, tk.b1, tk.rows_per_block, tk.d_offsets, tk.d_out,
+                             xcd_map && tk.grid == (int)gridDim.x, tk.grid, (int)blockIdx.x);
 }
 
 // ---- rows -> L1 buckets (byte keys) ---------------------------------------------
@@ -1638,6 +1656,22 @@ int sdp_part_sample_batch(const sdp_column *d_cols, int32_t ncols, int32_t n_sam
     hipLaunchKernelGGL(part_sample_u64_batch_kernel, dim3((n_sample + 255) / 256, ncols), dim3(256), 0,
                        (hipStream_t)stream, d_cols, n_sample, d_h);
     return check_launch("part_sample_batch");
+}
+
+int sdp_part_rows_batch(const sdp_rows_task *d_tasks, int32_t ntasks, int32_t dtype, int32_t max_grid, void *stream) {
+    if (d_tasks == nullptr || ntasks < 1 || ntasks > 65535 || max_grid < 1 || max_grid > SDP_PART_MAX_GRID)
+        return set_error(SDP_EINVAL, "part_rows_batch: args");
+    hipStream_t s = (hipStream_t)stream;
+    const dim3 grid(max_grid, ntasks);
+    const int xm = xcd_map_enabled();
+    switch (dtype) {
+    case SDP_F64: hipLaunchKernelGGL(part_scatter_rows_u64_batch_kernel<double>, grid, dim3(ST), 0, s, d_tasks, xm); break;
+    case SDP_F32: hipLaunchKernelGGL(part_scatter_rows_u64_batch_kernel<float>, grid, dim3(ST), 0, s, d_tasks, xm); break;
+    case SDP_I64: hipLaunchKernelGGL(part_scatter_rows_u64_batch_kernel<int64_t>, grid, dim3(ST), 0, s, d_tasks, xm); break;
+    case SDP_I32: hipLaunchKernelGGL(part_scatter_rows_u64_batch_kernel<int32_t>, grid, dim3(ST), 0, s, d_tasks, xm); break;
+    default: return set_error(SDP_EINVAL, "part_rows_batch: dtype %d", dtype);
+    }
+    return check_launch("part_rows_batch");
 }
 
 int sdp_part_rows(const sdp_column *col, const sdp_bytes_column *bcol, const sdp_heavy *heavy, int32_t b1,

@@ -108,6 +108,11 @@ class SdpPass2Task(ctypes.Structure):
                 ('grid', ctypes.c_int32)]
 
 
+class SdpRowsTask(ctypes.Structure):
+    _fields_ = [('col', SdpColumn), ('heavy', SdpHeavy), ('d_offsets', ctypes.c_void_p), ('d_out', ctypes.c_void_p),
+                ('rows_per_block', ctypes.c_int64), ('b1', ctypes.c_int32), ('grid', ctypes.c_int32)]
+
+
 class SdpPass2Result(ctypes.Structure):
     _fields_ = [('abs_dev_sum', ctypes.c_double), ('n_high', ctypes.c_uint64), ('n_low', ctypes.c_uint64),
                 ('n_unbinned', ctypes.c_uint64)]
@@ -139,6 +144,7 @@ _SIGNATURES = {
     'sdp_pass1_batch': (ctypes.c_int, [_P, _I32, _I32, _I32, _I32, _I32, _P]),
     'sdp_part_sample_batch': (ctypes.c_int, [_P, _I32, _I32, _P, _P]),
     'sdp_pass2_count_batch': (ctypes.c_int, [_P, _I32, _I32, _I32, _I32, _I32, _P]),
+    'sdp_part_rows_batch': (ctypes.c_int, [_P, _I32, _I32, _I32, _P]),
     'sdp_compact_candidates': (ctypes.c_int, [_P, _P, _I32, _I64, _P, _P, _P, _P]),
     'sdp_radix_hist': (ctypes.c_int, [_P, _P, _U64, _I32, _P, _P]),
     'sdp_radix_filter': (ctypes.c_int, [_P, _P, _U64, _I32, _P, _P, _P]),

@@ -1265,19 +1265,29 @@ class Engine:
         ctxs = []
         for c in cols:
             pre = self._counted.pop(id(c), None)           # counted by pass 2 (sdp_pass2_count)
-            ctxs.append(self._group_scan(pre) if pre is not None else self._group_begin(c, False))
+            if pre is None:
+                pre = self._group_prepare(c, False)
+                if pre is not None:
+                    self._group_count(pre)
+            ctxs.append(pre)
         live = [c for c in ctxs if c is not None]
         if not live:
             return [None] * len(cols)
+        # wide tables: columns of one geometry share one scan of their level-1
+        # counts (global record positions: column c's records start where
+        # column c-1's end) and their level-1 scatter, level-2 and
+        # de-duplication launches (_group_middle_fused); the rest one by one
+        fuse, single = self._fusable(live)
+        for grp in fuse:
+            self._group_scan_shared([live[i] for i in grp])
+        for i in single:
+            self._group_scan(live[i])
         flat = torch.cat([c['bsn_dev'] for c in live]).cpu().numpy().astype(np.int64)
         off, bsns = 0, []
         for c in live:
             m = c['bsn_dev'].numel()
             bsns.append(flat[off:off + m])
             off += m
-        # wide tables: columns of one geometry share their level-2 and
-        # de-duplication launches (_group_middle_fused); the rest one by one
-        fuse, single = self._fusable(live, bsns)
         for grp in fuse:
             self._group_middle_fused([live[i] for i in grp], [bsns[i] for i in grp])
         for i in single:
@@ -1447,18 +1457,18 @@ class Engine:
     FUSE_BYTES = 32 << 30              # two 8-byte record buffers of a fused group alive at once
     FUSE_MAX_RECS = 1 << 26            # larger columns fill the GPU alone (and recycle their buffers)
 
-    def _fusable(self, ctxs, bsns):
-        """Partition group_batch's contexts into groups whose level-2 count,
-        scatter and de-duplication run as one launch each (fixed keys,
-        distinct only, same (b1, b2), a level 2 and records, under FUSE_BYTES)
-        and singles."""
+    def _fusable(self, ctxs):
+        """Partition group_batch's contexts (before their scans) into groups
+        whose stages run fused (fixed keys, distinct only, one (b1, b2), dtype
+        and DIRECT mode, a level 2, <= FUSE_MAX_RECS rows each, two 8-byte
+        record buffers under FUSE_BYTES) and singles."""
         by, single = {}, []
-        for i, (c, bs) in enumerate(zip(ctxs, bsns)):
-            if (c['isb'] or c['with_counts'] or c['large'] or c['b2'] == 0 or int(bs[-1]) == 0
-                    or int(bs[-1]) > self.FUSE_MAX_RECS):
+        for i, c in enumerate(ctxs):
+            n = c['col'].length
+            if c['isb'] or c['with_counts'] or c['large'] or c['b2'] == 0 or n == 0 or n > self.FUSE_MAX_RECS:
                 single.append(i)
             else:
-                by.setdefault((c['b1'], c['b2'], id(c['col']) in self._near_unique), []).append(i)
+                by.setdefault((c['b1'], c['b2'], c['col'].dtype, id(c['col']) in self._near_unique), []).append(i)
         fuse = []
         for key, idx in by.items():
             if len(idx) < self.FUSE_MIN_COLS:
@@ -1466,7 +1476,7 @@ class Engine:
                 continue
             grp, held = [], 0
             for i in idx:
-                need = 16 * int(bsns[i][-1])
+                need = 16 * ctxs[i]['col'].length
                 if grp and held + need > self.FUSE_BYTES:
                     fuse.append(grp)
                     grp, held = [], 0
@@ -1475,6 +1485,21 @@ class Engine:
             fuse.append(grp)
         single += [g[0] for g in fuse if len(g) == 1]
         return [g for g in fuse if len(g) > 1], sorted(single)
+
+    def _group_scan_shared(self, ctxs):
+        """ONE exclusive scan of the concatenated level-1 counts of `ctxs`
+        (bucket-major per column): o1 / bsn_dev of column c then hold global
+        positions in the group's shared record buffer."""
+        lens = [c['h1'].numel() for c in ctxs]
+        O = self._scan(torch.cat([c.pop('h1') for c in ctxs]))
+        off = 0
+        for c, m in zip(ctxs, lens):
+            o1 = O[off:off + m + 1]
+            nb1, grid = c['nb1'], c['grid']
+            c['o1'] = o1
+            c['bsn_dev'] = torch.cat([o1[0:nb1 * grid:grid], o1[-1:]])
+            off += m
+        ctxs[0]['_shared_scan'] = O
 
     def _group_middle_fused(self, ctxs, bsns):
         """_group_middle of several fixed-key, distinct-only columns of one
@@ -1488,16 +1513,25 @@ class Engine:
         s = self._s()
         b1, b2 = ctxs[0]['b1'], ctxs[0]['b2']
         nb1, nb2 = 1 << b1, 1 << b2
-        nrecs = [int(bs[-1]) for bs in bsns]
-        base = np.concatenate([[0], np.cumsum(nrecs)]).astype(np.int64)
-        total = int(base[-1])
+        # bsns hold global positions (_group_scan_shared): column c's records
+        # are [bs_c[0], bs_c[-1]) of the shared buffer
+        total = int(bsns[-1][-1])
         r1, keep1 = self._records(total, False)
-        for ctx, bs, b0 in zip(ctxs, bsns, base[:-1]):
-            nat.annotate(_label(ctx['col'], 'scatter'), ctx['rb'] + int(bs[-1]) * 8)
-            rc = nat.SdpRecords(keep1[0].data_ptr() + 8 * int(b0), None, None)
-            sdp.sdp_part_rows(self._gref(ctx), None, ctypes.byref(ctx['hv']['struct']) if ctx['hv'] else None, b1, 1,
-                              None, ptr(ctx['o1']), ctypes.byref(rc), ptr(ctx['hcnt']), ptr(ctx['stats']), s)
+        tasks = (nat.SdpRowsTask * len(ctxs))()
+        for j, ctx in enumerate(ctxs):
+            hv = ctx['hv']
+            tasks[j] = nat.SdpRowsTask(ctx['cs'], hv['struct'] if hv else nat.SdpHeavy(None, None, None, None, 0, 0),
+                                       ctx['o1'].data_ptr(), keep1[0].data_ptr(),
+                                       sdp.sdp_part_rows_per_block(ctx['col'].length, 0), b1, ctx['grid'])
+        d_tasks = self._h2d(np.frombuffer(bytearray(bytes(tasks)), dtype=np.uint8))
+        nat.annotate(_label(ctxs[0]['col'], 'scatter_batch'), sum(c['rb'] for c in ctxs) + total * 8)
+        sdp.sdp_part_rows_batch(ptr(d_tasks), len(ctxs), ctxs[0]['col'].dtype, max(c['grid'] for c in ctxs), s)
+        shared = ctxs[0].pop('_shared_scan', None)
+        for ctx in ctxs:
             del ctx['o1'], ctx['bsn_dev']
+        del shared
+        base = np.array([bs[0] for bs in bsns] + [total], dtype=np.int64)
+        bsns = [bs - bs[0] for bs in bsns]                      # column-local bucket starts
         # every column's level-2 chunk table at once ([column, L1 bucket] arrays):
         # chunks of <= PART_CHUNK records, ordered (column, bucket, chunk); the
         # histogram slot of (column, bucket, sub-bucket, chunk) is

@@ -51,7 +51,8 @@ STRUCTS = {'sdp_column': 'SdpColumn', 'sdp_bytes_column': 'SdpBytesColumn', 'sdp
            'sdp_pass1_result': 'SdpPass1Result', 'sdp_pass2_result': 'SdpPass2Result',
            'sdp_records': 'SdpRecords', 'sdp_heavy': 'SdpHeavy', 'sdp_chunk': 'SdpChunk',
            'sdp_select_task': 'SdpSelectTask', 'sdp_compact_task': 'SdpCompactTask',
-           'sdp_pass1_task': 'SdpPass1Task', 'sdp_pass2_task': 'SdpPass2Task'}
+           'sdp_pass1_task': 'SdpPass1Task', 'sdp_pass2_task': 'SdpPass2Task',
+           'sdp_rows_task': 'SdpRowsTask'}
 
 
 def test_struct_layouts_match_c():

@@ -192,30 +192,28 @@ def test_select_sizing_mirrors_the_library():
 
 
 def test_fusable_groups_wide_tables_only():
-    """group_batch fuses the level-2 / dedup stages of >= FUSE_MIN_COLS small
-    fixed-key, distinct-only columns of one geometry (Engine._fusable); byte
-    keys, counted groups, single-level and large columns stay single."""
-    import numpy as np
+    """group_batch fuses the scans, level-1 scatters, level-2 and dedup stages
+    of >= FUSE_MIN_COLS small fixed-key, distinct-only columns of one geometry
+    and dtype (Engine._fusable, decided before the scans); byte keys, counted
+    groups, single-level, empty and large columns stay single."""
     from spark_df_profiling.engine import Engine
     e = Engine(device='cpu')
 
     class Col:
-        pass
+        def __init__(self, n, dtype=9):
+            self.length, self.dtype = n, dtype
 
-    def ctx(b1=7, b2=7, isb=False, wc=False, large=False):
-        return {'isb': isb, 'with_counts': wc, 'large': large, 'b1': b1, 'b2': b2, 'col': Col()}
+    def ctx(n=10 ** 7, b1=7, b2=7, isb=False, wc=False, large=False, dtype=9):
+        return {'isb': isb, 'with_counts': wc, 'large': large, 'b1': b1, 'b2': b2, 'col': Col(n, dtype)}
 
-    small = np.array([0, 10, 10 ** 7])
-    big = np.array([0, 10, 10 ** 8])
-    ctxs = [ctx() for _ in range(10)] + [ctx(isb=True), ctx(wc=True), ctx(b2=0), ctx(b1=8)]
-    bsns = [small] * 14
-    fuse, single = e._fusable(ctxs, bsns)
+    ctxs = [ctx() for _ in range(10)] + [ctx(isb=True), ctx(wc=True), ctx(b2=0), ctx(b1=8), ctx(n=0), ctx(dtype=8)]
+    fuse, single = e._fusable(ctxs)
     assert fuse == [list(range(10))]
-    assert single == [10, 11, 12, 13]
-    fuse, single = e._fusable([ctx() for _ in range(9)], [big] * 9)        # 1e8 records each: not fused
+    assert single == [10, 11, 12, 13, 14, 15]
+    fuse, single = e._fusable([ctx(n=10 ** 8) for _ in range(9)])          # 1e8 rows each: not fused
     assert fuse == [] and single == list(range(9))
-    fuse, single = e._fusable([ctx() for _ in range(5)], [small] * 5)      # too few columns
+    fuse, single = e._fusable([ctx() for _ in range(5)])                   # too few columns
     assert fuse == [] and single == list(range(5))
     e.FUSE_BYTES = 16 * 3 * 10 ** 7                                        # three columns per group
-    fuse, single = e._fusable([ctx() for _ in range(8)], [small] * 8)
+    fuse, single = e._fusable([ctx() for _ in range(8)])
     assert fuse == [[0, 1, 2], [3, 4, 5], [6, 7]] and single == []
