@@ -58,6 +58,54 @@ template <> struct Elem<float> {
         __device__ static int64_t i(T v) { return (int64_t)v; }                  \
         __device__ static uint64_t key(T v) { return i64_key((int64_t)v); }      \
     };
+// 32-bit order-preserving keys of 4-byte types (pass 1's inclusive window
+// tests): key32 is monotone in the value and widen(key32) is the element's
+// 64-bit key, so for valid (non-NaN) elements key64 < L  <=>  key32 < lower32(L)
+// and key64 <= H  <=>  key32 <= upper32(H) (pass1_bounds32 below).
+template <typename T> struct Key32 { static constexpr bool ok = false; };
+template <> struct Key32<float> {
+    static constexpr bool ok = true;
+    __device__ static uint32_t key(float v) {            // v not NaN; -0.0 groups with 0.0
+        const uint32_t b = v == 0.0f ? 0u : __float_as_uint(v);
+        return (b >> 31) ? ~b : (b | 0x80000000u);
+    }
+    // 64-bit key of the element with key k; keys below -inf's / above +inf's
+    // (NaN patterns, never a valid element's) map to 0 / UINT64_MAX so that the
+    // map stays monotone over all of [0, 2^32)
+    __device__ static uint64_t widen(uint32_t k) {
+        if (k < 0x007FFFFFu) return 0;
+        if (k > 0xFF800000u) return EMPTY64;
+        return widen_valid(k);
+    }
+    __device__ static uint64_t widen_valid(uint32_t k) {  // k of a non-NaN value
+        const uint32_t b = (k >> 31) ? (k & 0x7FFFFFFFu) : ~k;
+        const uint64_t d = (uint64_t)__double_as_longlong((double)__uint_as_float(b));
+        return (d >> 63) ? ~d : (d | 0x8000000000000000ull);   // f64_key without the NaN / -0.0 cases
+    }
+};
+template <> struct Key32<int32_t> {
+    static constexpr bool ok = true;
+    __device__ static uint32_t key(int32_t v) { return (uint32_t)v ^ 0x80000000u; }
+    __device__ static uint64_t widen(uint32_t k) { return i64_key((int64_t)(int32_t)(k ^ 0x80000000u)); }
+    __device__ static uint64_t widen_valid(uint32_t k) { return widen(k); }
+};
+template <> struct Key32<uint32_t> {
+    static constexpr bool ok = true;
+    __device__ static uint32_t key(uint32_t v) { return v; }
+    __device__ static uint64_t widen(uint32_t k) { return i64_key((int64_t)k); }
+    __device__ static uint64_t widen_valid(uint32_t k) { return widen(k); }
+};
+// smallest k in [0, 2^32) with widen(k) >= L (2^32 - 1 if none: above every valid key)
+template <typename T>
+__device__ __forceinline__ uint32_t key32_lower(uint64_t L) {
+    uint64_t a = 0, b = 0x100000000ull;
+    while (a < b) {
+        const uint64_t mid = (a + b) >> 1;
+        if (Key32<T>::widen((uint32_t)mid) >= L) b = mid; else a = mid + 1;
+    }
+    return a >= 0x100000000ull ? 0xFFFFFFFFu : (uint32_t)a;
+}
+
 SDP_INT_ELEM(int64_t)
 SDP_INT_ELEM(int32_t)
 SDP_INT_ELEM(int16_t)

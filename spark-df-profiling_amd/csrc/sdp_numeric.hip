@@ -380,6 +380,7 @@ constexpr int P1_WPB = 4;            // waves per pass-1 block (P1_BLOCK / WAVE)
 
 struct P1Ctx {
     uint64_t lo[SDP_MAX_WINDOWS], hi[SDP_MAX_WINDOWS];
+    uint32_t lo32[SDP_MAX_WINDOWS], hi32[SDP_MAX_WINDOWS];   // 4-byte types, inclusive windows
     uint64_t *seg[SDP_MAX_WINDOWS];   // this wave's candidate slot range of window w
     int nw;
     double K;
@@ -426,6 +427,38 @@ __device__ __forceinline__ void p1_elem(P1Thread &st, const P1Ctx &cx, T x, bool
     }
     if (!WIN) return;                   // no quantile windows (date/timestamp min/max)
     const uint64_t key = ok ? Elem<T>::key(x) : 0ull;
+#ifndef SDP_NO_KEY32
+    if constexpr (INCL && Key32<T>::ok) {
+        // 4-byte types: the same inclusive test on 32-bit keys against bounds
+        // mapped into the 32-bit key space (pass1_body); a candidate is stored
+        // as its 64-bit key
+        const uint32_t k32 = ok ? Key32<T>::key(x) : 0u;
+#pragma unroll
+        for (int w = 0; w < SDP_MAX_WINDOWS; ++w) {
+            const uint32_t lo = cx.lo32[w], hi = cx.hi32[w];
+            st.gt[w] += (uint32_t)(k32 < lo);
+            const bool ge = k32 >= lo, le = k32 <= hi;
+            const bool in = ge & le;
+            const uint64_t m = __builtin_amdgcn_ballot_w64(ge) & __builtin_amdgcn_ballot_w64(le);
+            if (m) {
+                const uint32_t c = st.wcur[w];
+                const uint32_t pos = c + (uint32_t)lane_rank(m);
+#ifdef SDP_K32_INLINE
+                if (in && (int64_t)pos < cx.cap) {
+                    uint32_t kk = k32;
+                    asm volatile("" : "+v"(kk));   // widen here, in the store's lanes, not hoisted
+                    cx.seg[w][pos] = Key32<T>::widen_valid(kk);
+                }
+#else
+                // the 32-bit key; pass1_body widens the wave's slots after its sweep
+                if (in && (int64_t)pos < cx.cap) cx.seg[w][pos] = (uint64_t)k32;
+#endif
+                st.wcur[w] = c + (uint32_t)__popcll(m);
+            }
+        }
+        return;
+    }
+#endif
     if constexpr (INCL) {
         // Inclusive windows (every bound key rare in the sample, lo > 0): one
         // count #(key < lo) -- held in gt[] and turned into #(key > hi) in the
@@ -496,6 +529,25 @@ __device__ __forceinline__ void pass1_body(const sdp_column &col, const sdp_qpla
     }
     cx.K = plan->shift;
     cx.cap = cap;
+#ifndef SDP_NO_KEY32
+    if constexpr (INCL && Key32<T>::ok) {
+        // 32-bit bounds: lane j < W computes lo32[j], lane W + j hi32[j] (a
+        // 32-step search each), read back as wave-uniform values; unused windows
+        // have lo32 > hi32 (nothing inside)
+        const int ln = lane_id();
+        const int w = ln % SDP_MAX_WINDOWS;
+        uint32_t v = 0;
+        if (ln < 2 * SDP_MAX_WINDOWS) {
+            if (w < cx.nw) v = ln < SDP_MAX_WINDOWS ? key32_lower<T>(plan->lo[w]) : key32_lower<T>(plan->hi[w] + 1) - 1u;
+            else v = ln < SDP_MAX_WINDOWS ? 0xFFFFFFFFu : 0xFFFFFFFEu;
+        }
+#pragma unroll
+        for (int j = 0; j < SDP_MAX_WINDOWS; ++j) {
+            cx.lo32[j] = __builtin_amdgcn_readlane(v, j);
+            cx.hi32[j] = __builtin_amdgcn_readlane(v, SDP_MAX_WINDOWS + j);
+        }
+    }
+#endif
 
     P1Thread st;
     st.count = st.n_valid = st.n_nan = st.n_zero = st.n_skip = 0;
@@ -557,6 +609,20 @@ __device__ __forceinline__ void pass1_body(const sdp_column &col, const sdp_qpla
         p1_fold(st);
     }
 
+#if !defined(SDP_NO_KEY32) && !defined(SDP_K32_INLINE) && !defined(SDP_K32_SKIP_WIDEN)
+    if constexpr (INCL && Key32<T>::ok) {
+        // widen this wave's 32-bit candidate keys in place (its own stores,
+        // complete after the vmcnt wait; its slots are read by no other wave)
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#pragma unroll
+        for (int w = 0; w < SDP_MAX_WINDOWS; ++w) {
+            if (w >= cx.nw) break;
+            const int64_t nc = (int64_t)st.wcur[w] < cap ? (int64_t)st.wcur[w] : cap;
+            uint64_t *seg = cx.seg[w];
+            for (int64_t i = lane_id(); i < nc; i += WAVE) seg[i] = Key32<T>::widen_valid((uint32_t)seg[i]);
+        }
+    }
+#endif
     // ---- block reduction: waves, then LDS, fixed order ----------------------
     __shared__ uint64_t s_u[P1_BLOCK / WAVE][NU];
     __shared__ int64_t s_i[P1_BLOCK / WAVE][3];
