@@ -405,8 +405,8 @@ __device__ __forceinline__ void p1_elem(P1Thread &st, const P1Ctx &cx, T x, bool
     if (ok) {
         st.count += 1;
         if (Elem<T>::is_float) {
-            st.dmin = fmin(st.dmin, xd);
-            st.dmax = fmax(st.dmax, xd);
+            st.dmin = dmin_nn(st.dmin, xd);       // xd is not NaN here
+            st.dmax = dmax_nn(st.dmax, xd);
         } else {
             const int64_t xi = Elem<T>::i(x);
             st.imin = xi < st.imin ? xi : st.imin;
