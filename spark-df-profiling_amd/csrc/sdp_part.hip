@@ -425,6 +425,51 @@ __device__ __forceinline__ void bytes_tile_a(const sdp_bytes_column &col, int64_
     }
 }
 
+// stage B1: the key words of a tile (issue only; stage B2 decodes them)
+template <int RPT>
+__device__ __forceinline__ void bytes_tile_words(const sdp_bytes_column &col, const BytesOffs<RPT> &a,
+                                                 uint32_t (&w)[RPT][5]) {
+#pragma unroll
+    for (int q = 0; q < RPT; ++q) {
+        const int64_t len = a.ln[q];
+        const uint8_t *pb = col.d_data + a.o0[q];
+        const uint32_t ad = (uint32_t)((uintptr_t)pb & 3u);
+        const uint32_t *p = (const uint32_t *)(pb - ad);
+        const int64_t need = len <= SHORT_MAX ? (int64_t)(ad + len + 3) >> 2 : 0;
+        const bool ok = ((a.vmask >> q) & 1u) && need > 0;
+        const u32x4a4 v = ok ? *(const u32x4a4 *)p : u32x4a4{0u, 0u, 0u, 0u};
+        w[q][0] = v.x; w[q][1] = v.y; w[q][2] = v.z; w[q][3] = v.w;
+        w[q][4] = (ok && need > 4) ? p[4] : 0u;
+    }
+}
+template <int NT, int RPT>
+__device__ __forceinline__ void bytes_tile_decode(const sdp_bytes_column &col, int64_t base, const BytesOffs<RPT> &a,
+                                                  const uint32_t (&w)[RPT][5], uint64_t (&k0)[RPT],
+                                                  uint64_t (&k1)[RPT], uint64_t (&meta)[RPT], uint64_t (&h)[RPT],
+                                                  int t) {
+#pragma unroll
+    for (int q = 0; q < RPT; ++q) {
+        k0[q] = k1[q] = meta[q] = h[q] = 0;
+        if (!((a.vmask >> q) & 1u)) continue;
+        const int64_t row = base + (int64_t)q * NT + t;
+        const int64_t len = a.ln[q];
+        if (len <= SHORT_MAX) {
+            const uint32_t sh = (uint32_t)((uintptr_t)(col.d_data + a.o0[q]) & 3);
+            const uint64_t v0 = (uint64_t)__builtin_amdgcn_alignbyte(w[q][1], w[q][0], sh) |
+                                ((uint64_t)__builtin_amdgcn_alignbyte(w[q][2], w[q][1], sh) << 32);
+            const uint64_t v1 = (uint64_t)__builtin_amdgcn_alignbyte(w[q][3], w[q][2], sh) |
+                                ((uint64_t)__builtin_amdgcn_alignbyte(w[q][4], w[q][3], sh) << 32);
+            k0[q] = mask_bytes(v0, len);
+            k1[q] = mask_bytes(v1, len - 8);
+            h[q] = bh_short(k0[q], k1[q], (uint64_t)len);
+        } else {
+            h[q] = hash_long_global(col.d_data + a.o0[q], len);
+            k0[q] = h[q];
+        }
+        meta[q] = ((uint64_t)min((int64_t)LEN_MAX, len) << 40) | (uint64_t)(row + 1);
+    }
+}
+
 template <int NT, int RPT>
 __device__ __forceinline__ void bytes_tile_b(const sdp_bytes_column &col, int64_t base, const BytesOffs<RPT> &a,
                                              uint64_t (&k0)[RPT], uint64_t (&k1)[RPT], uint64_t (&meta)[RPT],
@@ -624,7 +669,12 @@ struct BRecLds {
     uint32_t hist[BR_W][MAXB];
 };
 
-__global__ void __launch_bounds__(BR_T, 4) part_records_rows_bytes_kernel(sdp_bytes_column col, HeavyArg heavy, int b1,
+#ifndef SDP_BREC_3STAGE
+constexpr int BR_MINB = 4;
+#else
+constexpr int BR_MINB = 3;                  // the three-stage pipeline needs ~150 VGPRs
+#endif
+__global__ void __launch_bounds__(BR_T, BR_MINB) part_records_rows_bytes_kernel(sdp_bytes_column col, HeavyArg heavy, int b1,
                                                                        int64_t rows_per_block, uint32_t *hist,
                                                                        Chunk *chunks, uint64_t *out_k0,
                                                                        uint64_t *out_k1, uint64_t *out_meta,
@@ -643,6 +693,7 @@ __global__ void __launch_bounds__(BR_T, 4) part_records_rows_bytes_kernel(sdp_by
     uint64_t rows = 0;
     int64_t cur = s0;                                               // next record slot of this strip
     constexpr int64_t STEP = (int64_t)WAVE * BR_RPT;
+#ifndef SDP_BREC_3STAGE
     BytesOffs<BR_RPT> oc, on;
     if (s0 < s1) bytes_tile_a<WAVE, BR_RPT>(col, s0, s1, oc, lane);
     for (int64_t base = s0; base < s1; base += STEP) {
@@ -652,6 +703,33 @@ __global__ void __launch_bounds__(BR_T, 4) part_records_rows_bytes_kernel(sdp_by
         bytes_tile_b<WAVE, BR_RPT>(col, base, oc, k0, k1, meta, h, lane);
         const uint32_t vmask = oc.vmask;
         if (more) oc = on;
+#else
+    // three stages in flight: the offsets of tile i + 2 and the key words of
+    // tile i + 1 are loading while tile i is hashed, looked up and written
+    BytesOffs<BR_RPT> oc, on;
+    uint32_t wc[BR_RPT][5], wn[BR_RPT][5];
+    if (s0 < s1) {
+        bytes_tile_a<WAVE, BR_RPT>(col, s0, s1, oc, lane);
+        bytes_tile_words<BR_RPT>(col, oc, wc);
+        if (s0 + STEP < s1) bytes_tile_a<WAVE, BR_RPT>(col, s0 + STEP, s1, on, lane);
+    }
+    for (int64_t base = s0; base < s1; base += STEP) {
+        uint64_t k0[BR_RPT], k1[BR_RPT], meta[BR_RPT], h[BR_RPT];
+        const bool more = base + STEP < s1, more2 = base + 2 * STEP < s1;
+        BytesOffs<BR_RPT> on2;
+        if (more) bytes_tile_words<BR_RPT>(col, on, wn);                         // tile i + 1's key words
+        if (more2) bytes_tile_a<WAVE, BR_RPT>(col, base + 2 * STEP, s1, on2, lane);   // tile i + 2's offsets
+        bytes_tile_decode<WAVE, BR_RPT>(col, base, oc, wc, k0, k1, meta, h, lane);
+        const uint32_t vmask = oc.vmask;
+        if (more) {
+            oc = on;
+#pragma unroll
+            for (int q = 0; q < BR_RPT; ++q)
+#pragma unroll
+                for (int i = 0; i < 5; ++i) wc[q][i] = wn[q][i];
+        }
+        if (more2) on = on2;
+#endif
 #pragma unroll
         for (int q = 0; q < BR_RPT; ++q) {
             bool keep = false;
@@ -1725,8 +1803,20 @@ int sdp_part_rows(const sdp_column *col, const sdp_bytes_column *bcol, const sdp
     return check_launch("part_rows_u64_kernel");
 }
 
+// the records kernel's rows per block: whole 4 K-row tiles, at most one
+// resident round of workgroups (BR_MINB per CU on 256 CUs)
+#ifndef SDP_BREC_GRID
+#define SDP_BREC_GRID (BR_MINB * 256)
+#endif
+static int64_t records_rows_per_block(int64_t length) {
+    const int64_t tiles = (length + B_S_TILE - 1) / B_S_TILE;
+    if (tiles < 1) return B_S_TILE;
+    const int64_t blocks = tiles < SDP_BREC_GRID ? tiles : SDP_BREC_GRID;
+    return ((tiles + blocks - 1) / blocks) * B_S_TILE;
+}
+
 int64_t sdp_part_records_chunks(int64_t length) {
-    const int64_t rpb = sdp_part_rows_per_block(length, 1);
+    const int64_t rpb = records_rows_per_block(length);
     const int64_t grid = (length + rpb - 1) / rpb;
     return (grid < 1 ? 1 : grid) * BR_W;
 }
@@ -1747,7 +1837,7 @@ int sdp_part_rows_records(const sdp_bytes_column *bcol, const sdp_heavy *heavy, 
             return set_error(SDP_EINVAL, "part_rows_records: byte heavy keys need k0/k1/meta and counts");
     }
     const int64_t n = bcol->length;
-    const int64_t rpb = sdp_part_rows_per_block(n, 1);
+    const int64_t rpb = records_rows_per_block(n);
     const int grid = (int)((n + rpb - 1) / rpb < 1 ? 1 : (n + rpb - 1) / rpb);
     hipLaunchKernelGGL(part_records_rows_bytes_kernel, dim3(grid), dim3(BR_T), 0, (hipStream_t)stream, *bcol, hv, b1,
                        rpb, d_hist, (Chunk *)d_chunks, d_out->d_k0, d_out->d_k1, d_out->d_meta, d_heavy_counts,

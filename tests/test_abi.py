@@ -91,10 +91,13 @@ def test_part_argument_checks_without_gpu():
     assert _native.sdp.sdp_part_bucket_target(1, 1) == 2048
     with pytest.raises(_native.NativeError, match='part_rows_records'):
         _native.sdp.sdp_part_rows_records(None, None, 4, None, None, None, None, None, None)
-    # one chunk per wave strip: 4 per workgroup of the byte-row grid
+    # one chunk per wave strip: 4 per workgroup of the records grid (whole
+    # 4 K-row tiles, at most SDP_PART_MAX_GRID workgroups)
     n = 10 ** 9
     rpb = _native.sdp.sdp_part_rows_per_block(n, 1)
-    assert _native.sdp.sdp_part_records_chunks(n) == 4 * (-(-n // rpb))
+    ch = _native.sdp.sdp_part_records_chunks(n)
+    assert ch % 4 == 0 and 4 <= ch <= 4 * 1024 and (ch // 4) * 4096 * (-(-n // 4096 // (ch // 4))) >= n
+    assert _native.sdp.sdp_part_records_chunks(0) == 4 and _native.sdp.sdp_part_records_chunks(5000) == 8
     assert rpb % 1024 == 0
 
 
