@@ -332,10 +332,13 @@ def label_kernels(label):
 TRAFFIC_SUMMARY = {'c3': 'profiles/r03ac_c3_traffic.json', 'c5': 'profiles/r02i_c5_traffic.json'}
 
 
-def pmc_traffic(label, path):
+def pmc_traffic(label, path, rows=None, workload=None):
     """HBM bytes per launch of the kernel(s) behind `label` from the PMC
     summary at `path` (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE passes over this
-    bench), or (None, None)."""
+    bench), or (None, None).  Only a summary of the same run shape counts: its
+    `rows` must equal this run's rows and its `workload` (when recorded) this
+    workload, and it must hold every kernel the label stands for -- a summary of
+    another size would give a meaningless bytes ratio."""
     if not path:
         return None, None
     full = path if os.path.isabs(path) else os.path.join(ROOT, path)
@@ -343,7 +346,14 @@ def pmc_traffic(label, path):
         return None, None
     with open(full) as fh:
         summ = json.load(fh)
+    if rows is not None and int(summ.get('rows', -1)) != int(rows):
+        return None, None
+    if workload is not None and summ.get('workload', workload) != workload:
+        return None, None
     pre = label_kernels(label)
+    if not pre or not all(any(k.startswith(p) for k in summ['kernels']) for p in pre
+                          if not p.startswith('sdp::gram_kernel<')):
+        return None, None
     hits = [v for k, v in summ['kernels'].items() if any(k.startswith(p) for p in pre)]
     if not hits:
         return None, None
@@ -352,7 +362,7 @@ def pmc_traffic(label, path):
     return sum(v['traffic_bytes'] * v['dispatches'] for v in hits) / n, path
 
 
-def roofline(rec, steps, step_s, prof_bytes, traffic_path=None):
+def roofline(rec, steps, step_s, prof_bytes, traffic_path=None, rows=None, workload=None):
     """Dominant kernel (entry point + label) by total HIP-event time -> achieved
     GB/s = its algorithmic bytes per launch / its mean launch duration."""
     torch.cuda.synchronize()
@@ -366,7 +376,7 @@ def roofline(rec, steps, step_s, prof_bytes, traffic_path=None):
     per_launch = nbytes[dom] / nl[dom]
     achieved = per_launch / (avg_ms * 1e-3) / 1e9
     prof_gbs = prof_bytes / step_s / 1e9
-    traffic, tsrc = pmc_traffic(dom, traffic_path)
+    traffic, tsrc = pmc_traffic(dom, traffic_path, rows, workload)
     out = {'bound': 'hbm', 'kernel': dom, 'achieved': round(achieved, 1), 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
            'frac': round(achieved / HBM_PEAK_GBS, 4),
            'traffic': int(traffic) if traffic is not None else None,
@@ -408,18 +418,43 @@ def shard_to_arrow(shard):
     return pa.table(arrays)
 
 
-def cpu_share():
-    """(cores the baseline uses, what the host reports): the box gives this job
-    a 16-CPU share (OMP_NUM_THREADS=16 there) while os.cpu_count() reports the
-    whole machine; the affinity mask bounds both."""
+def _cgroup_cpus():
+    """CPUs of this job's cgroup quota (cgroup v2 cpu.max, else v1 cfs), or None."""
+    try:
+        with open('/sys/fs/cgroup/cpu.max') as fh:
+            q, per = fh.read().split()[:2]
+        if q != 'max':
+            return max(1, math.ceil(int(q) / int(per)))
+    except (OSError, ValueError):
+        pass
+    try:
+        with open('/sys/fs/cgroup/cpu/cpu.cfs_quota_us') as fh:
+            q = int(fh.read())
+        with open('/sys/fs/cgroup/cpu/cpu.cfs_period_us') as fh:
+            per = int(fh.read())
+        if q > 0:
+            return max(1, math.ceil(q / per))
+    except (OSError, ValueError):
+        pass
+    return None
+
+
+def cpu_share(columns=16):
+    """(processes the baseline uses, how that was decided).  The CPUs this job
+    may run on are the affinity mask, bounded by the cgroup CPU quota when one
+    is set (os.cpu_count() reports the whole machine); the restatement runs one
+    column per process, so at most `columns` processes do work."""
     visible = os.cpu_count() or 1
     try:
         allowed = len(os.sched_getaffinity(0))
     except (AttributeError, OSError):
         allowed = visible
-    share = int(os.environ.get('OMP_NUM_THREADS', '16') or 16)
-    return max(1, min(allowed, share)), {'os_cpu_count': visible, 'affinity_cpus': allowed,
-                                         'omp_num_threads': os.environ.get('OMP_NUM_THREADS')}
+    quota = _cgroup_cpus()
+    avail = min(allowed, quota) if quota else allowed
+    src = 'cgroup cpu quota' if quota and quota < allowed else 'affinity mask'
+    return max(1, min(avail, columns)), {'os_cpu_count': visible, 'affinity_cpus': allowed,
+                                         'cgroup_quota_cpus': quota, 'available_cpus': avail,
+                                         'source': src, 'columns': columns}
 
 
 def cpu_baseline(sample_rows, device):
@@ -438,14 +473,17 @@ def cpu_baseline(sample_rows, device):
     t0 = time.perf_counter()
     fast.describe(table)
     dt = time.perf_counter() - t0
+    _, host = cpu_share()
     return {'value': round(sample_rows / dt, 1), 'unit': 'rows/s', 'cores': workers, 'kind': 'port',
-            'host_cpus': cpu_share()[1],
+            'host_cpus': host,
             'sample': '%d rows x 16 cols of the same C3 generator; oracle/fast.py vectorised numpy/Arrow '
-                      'restatement, one column per process on %d processes (CPU restatement, not reference Spark: '
-                      'no pyspark/JVM in the image), %.1f s' % (sample_rows, workers, dt)}
+                      'restatement, one column per process on %d processes (%d CPUs available by the %s; '
+                      'one column per process caps it at 16) (CPU restatement, not reference Spark: '
+                      'no pyspark/JVM in the image), %.1f s' % (sample_rows, workers, host['available_cpus'],
+                                                               host['source'], dt)}
 
 
-def gram_roofline(rec, steps, ncols, n_rows, traffic_path=None):
+def gram_roofline(rec, steps, ncols, n_rows, traffic_path=None, rows=None):
     """C5: the Pearson Gram on the fp64 matrix cores.  F_alg = n C (C + 1)
     flop per launch (symmetric X^T X, one multiply-add per
     unique entry) over the launch's average HIP-event duration."""
@@ -457,7 +495,7 @@ def gram_roofline(rec, steps, ncols, n_rows, traffic_path=None):
     flop = float(n_rows) * ncols * (ncols + 1)
     tfs = flop / (ms * 1e-3) / 1e12
     alg_bytes = sum(x for _, _, x in ev if x is not None) / len(ev)
-    traffic, tsrc = pmc_traffic('sdp_gram', traffic_path)
+    traffic, tsrc = pmc_traffic('sdp_gram', traffic_path, rows, 'c5')
     return {'bound': 'mfma', 'kernel': 'sdp_gram (gram_wide_kernel + gram_reduce_kernel<128>, v_mfma_f64_16x16x4f64)',
             'achieved': round(tfs, 2), 'peak': FP64_MFMA_PEAK_TFS, 'unit': 'TFLOP/s',
             'frac': round(tfs / FP64_MFMA_PEAK_TFS, 4),
@@ -466,6 +504,46 @@ def gram_roofline(rec, steps, ncols, n_rows, traffic_path=None):
             'flop_per_launch': flop, 'avg_launch_ms': round(ms, 4), 'launches_per_step': len(ev) // steps,
             'hbm_alg_bytes_per_launch': int(alg_bytes),
             'hbm_achieved_gbs': round(alg_bytes / (ms * 1e-3) / 1e9, 1)}
+
+
+class ReadbackCensus:
+    """Counts the device->host readbacks describe() makes while active (device
+    tensors read by .cpu() / .item() / .tolist() / .to('cpu')): each waits for
+    the stream, i.e. sits on the step's critical path.  (Host->device copies
+    are staged through pinned memory without a wait and are not counted.)
+    Run on the last warmup step, outside the timed region."""
+
+    def __init__(self):
+        self.count = 0
+        self._saved = []
+
+    def _wrap(self, owner, name, pred):
+        orig = getattr(owner, name)
+        census = self
+
+        def f(*a, **k):
+            if pred(*a, **k):
+                census.count += 1
+            return orig(*a, **k)
+        self._saved.append((owner, name, orig))
+        setattr(owner, name, f)
+
+    def __enter__(self):
+        def to_pred(t, *a, **k):
+            dev = k.get('device', a[0] if a else None)
+            if isinstance(dev, torch.dtype) or dev is None:
+                return False
+            return t.is_cuda and str(dev).startswith('cpu')
+        self._wrap(torch.Tensor, 'cpu', lambda t, *a, **k: t.is_cuda)
+        self._wrap(torch.Tensor, 'item', lambda t, *a, **k: t.is_cuda)
+        self._wrap(torch.Tensor, 'tolist', lambda t, *a, **k: t.is_cuda)
+        self._wrap(torch.Tensor, 'to', to_pred)
+        return self
+
+    def __exit__(self, *exc):
+        for owner, name, orig in reversed(self._saved):
+            setattr(owner, name, orig)
+        return False
 
 
 def main():
@@ -547,8 +625,14 @@ def main():
     def step(raw=None):
         return describe(table, comm=comm, plots=not args.no_plots, raw=raw, workers=args.workers)
 
-    for _ in range(args.warmup):
-        step()
+    readbacks = None
+    for i in range(args.warmup):
+        if i == args.warmup - 1:
+            with ReadbackCensus() as census:
+                step()
+            readbacks = census.count
+        else:
+            step()
 
     def barrier():
         # every rank's queued work done and every rank here: a one-element
@@ -580,7 +664,8 @@ def main():
         el = torch.tensor([elapsed], dtype=torch.float64, device=device)
         elapsed = float(torch.stack(comm.allgather(el)).max().item())
     step_s = elapsed / args.steps
-    rl, per_kernel = roofline(rec, args.steps, step_s, profile_alg_bytes(table, raw), traffic_path)
+    rl, per_kernel = roofline(rec, args.steps, step_s, profile_alg_bytes(table, raw), traffic_path,
+                              args.rows, args.workload)
     ncols = len(table.columns)
     # quantile-window candidates written by pass 1, as a fraction of each NUM
     # column's counted rows (sum over its windows of the keys strictly inside)
@@ -591,7 +676,7 @@ def main():
             cand[name] = round(sum(p1['w_in']) / p1['count'], 4)
     if args.workload == 'c5':
         hbm_rl = rl
-        rl = gram_roofline(rec, args.steps, ncols, table.num_rows, traffic_path)
+        rl = gram_roofline(rec, args.steps, ncols, table.num_rows, traffic_path, args.rows)
         rl['hbm_dominant'] = {k: hbm_rl[k] for k in ('kernel', 'achieved', 'frac', 'avg_launch_ms')}
         rl['whole_profile'] = hbm_rl['whole_profile']
 
@@ -616,6 +701,8 @@ def main():
                    'plots': not args.no_plots,
                    'column_workers': column_workers_used},
         'roofline': rl,
+        'whole_profile': rl.get('whole_profile'),
+        'host_readbacks_per_step': readbacks,
         'per_kernel': per_kernel,
         'quantile_candidates_frac': {'max': max(cand.values()) if cand else None,
                                      'mean': round(sum(cand.values()) / len(cand), 4) if cand else None},

@@ -508,8 +508,10 @@ typedef struct sdp_rows_task {
     int32_t           b1, grid;
 } sdp_rows_task;
 
-/* The level-1 scatters of `ntasks` columns of one dtype (f64/f32/i64/i32) in
- * one launch (wide tables); d_tasks lives in device memory. */
+/* The level-1 scatters of `ntasks` columns of one dtype (every fixed-width
+ * dtype but SDP_BOOL) in one launch (wide tables); d_tasks lives in device
+ * memory, so the caller checks each task as sdp_part_rows does (16-byte aligned
+ * values, heavy.n <= 256, grid <= max_grid). */
 int sdp_part_rows_batch(const sdp_rows_task *d_tasks, int32_t ntasks, int32_t dtype, int32_t max_grid, void *stream);
 /* Byte columns, one read of the strings (replaces sdp_part_rows phase 0 + 1 for
  * bcol): every wave of every workgroup compacts the records of its strip of

@@ -110,15 +110,17 @@ template <> struct Key32<uint32_t> {
     __device__ static uint64_t widen(uint32_t k) { return i64_key((int64_t)k); }
     __device__ static uint64_t widen_valid(uint32_t k) { return widen(k); }
 };
-// smallest k in [0, 2^32) with widen(k) >= L (2^32 - 1 if none: above every valid key)
+// smallest k in [0, 2^32) with widen(k) >= L, or 2^32 when there is none (L
+// above every 32-bit key's widening); reported apart, since 2^32 - 1 is itself
+// a valid key (INT32_MAX, UINT32_MAX)
 template <typename T>
-__device__ __forceinline__ uint32_t key32_lower(uint64_t L) {
+__device__ __forceinline__ uint64_t key32_lower(uint64_t L) {
     uint64_t a = 0, b = 0x100000000ull;
     while (a < b) {
         const uint64_t mid = (a + b) >> 1;
         if (Key32<T>::widen((uint32_t)mid) >= L) b = mid; else a = mid + 1;
     }
-    return a >= 0x100000000ull ? 0xFFFFFFFFu : (uint32_t)a;
+    return a;
 }
 
 SDP_INT_ELEM(int64_t)

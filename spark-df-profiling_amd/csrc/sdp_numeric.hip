@@ -394,7 +394,7 @@ struct P1Ctx {
 // epilogue (n_skip), as are eqhi counts of windows with lo == hi -- so each
 // window costs two compare-and-carry counts, one equality count and the
 // inside test, with no per-element validity masking.
-template <typename T, bool WIN, bool INCL = false>
+template <typename T, bool WIN, bool INCL = false, bool K32 = false>
 __device__ __forceinline__ void p1_elem(P1Thread &st, const P1Ctx &cx, T x, bool valid) {
     const double xd = Elem<T>::d(x);
     const bool isnan_ = Elem<T>::is_float && (xd != xd);
@@ -427,11 +427,11 @@ __device__ __forceinline__ void p1_elem(P1Thread &st, const P1Ctx &cx, T x, bool
     }
     if (!WIN) return;                   // no quantile windows (date/timestamp min/max)
     const uint64_t key = ok ? Elem<T>::key(x) : 0ull;
-#ifndef SDP_NO_KEY32
-    if constexpr (INCL && Key32<T>::ok) {
+    if constexpr (INCL && K32) {
         // 4-byte types: the same inclusive test on 32-bit keys against bounds
-        // mapped into the 32-bit key space (pass1_body); a candidate is stored
-        // as its 64-bit key
+        // mapped into the 32-bit key space (pass1_body; every lo32 > 0, so the
+        // skipped elements' key 0 is below every window); a candidate is
+        // stored as its 64-bit key
         const uint32_t k32 = ok ? Key32<T>::key(x) : 0u;
 #pragma unroll
         for (int w = 0; w < SDP_MAX_WINDOWS; ++w) {
@@ -443,22 +443,13 @@ __device__ __forceinline__ void p1_elem(P1Thread &st, const P1Ctx &cx, T x, bool
             if (m) {
                 const uint32_t c = st.wcur[w];
                 const uint32_t pos = c + (uint32_t)lane_rank(m);
-#ifdef SDP_K32_INLINE
-                if (in && (int64_t)pos < cx.cap) {
-                    uint32_t kk = k32;
-                    asm volatile("" : "+v"(kk));   // widen here, in the store's lanes, not hoisted
-                    cx.seg[w][pos] = Key32<T>::widen_valid(kk);
-                }
-#else
-                // the 32-bit key; pass1_body widens the wave's slots after its sweep
+                // the 32-bit key; pass1_sweep widens the wave's slots after its sweep
                 if (in && (int64_t)pos < cx.cap) cx.seg[w][pos] = (uint64_t)k32;
-#endif
                 st.wcur[w] = c + (uint32_t)__popcll(m);
             }
         }
         return;
     }
-#endif
     if constexpr (INCL) {
         // Inclusive windows (every bound key rare in the sample, lo > 0): one
         // count #(key < lo) -- held in gt[] and turned into #(key > hi) in the
@@ -510,57 +501,12 @@ __device__ __forceinline__ void p1_fold(P1Thread &st) {
     st.t1 = st.t3 = 0.0;
 }
 
-// pass 1 of one column by block bx of a G-block grid (the batched launch runs
-// several columns' grids side by side, blockIdx.y = column)
-template <typename T, bool WIN, bool INCL>
-__device__ __forceinline__ void pass1_body(const sdp_column &col, const sdp_qplan *plan, P1Partial *partials,
-                                           uint64_t *cand, uint32_t *cand_counts, int64_t cap, const int G,
-                                           const int bx) {
+// The sweep of pass 1 over block bx's tiles (+ the tail), accumulating into st.
+// K32: 4-byte types with inclusive windows test 32-bit keys (cx.lo32/hi32).
+template <typename T, bool WIN, bool INCL, bool K32>
+__device__ __forceinline__ void pass1_sweep(P1Thread &st, const P1Ctx &cx, const sdp_column &col, int64_t cap,
+                                            const int G, const int bx) {
     constexpr int VPT = Vec16<T>::N;
-
-    P1Ctx cx;
-    cx.nw = plan->n_windows;
-#pragma unroll
-    for (int w = 0; w < SDP_MAX_WINDOWS; ++w) {
-        cx.lo[w] = w < cx.nw ? plan->lo[w] : EMPTY64;
-        cx.hi[w] = w < cx.nw ? plan->hi[w] : (INCL ? EMPTY64 - 1 : EMPTY64);
-        const int64_t seg = ((int64_t)w * G + bx) * P1_WPB + (threadIdx.x / WAVE);
-        cx.seg[w] = cand + seg * cap;
-    }
-    cx.K = plan->shift;
-    cx.cap = cap;
-#ifndef SDP_NO_KEY32
-    if constexpr (INCL && Key32<T>::ok) {
-        // 32-bit bounds: lane j < W computes lo32[j], lane W + j hi32[j] (a
-        // 32-step search each), read back as wave-uniform values; unused windows
-        // have lo32 > hi32 (nothing inside)
-        const int ln = lane_id();
-        const int w = ln % SDP_MAX_WINDOWS;
-        uint32_t v = 0;
-        if (ln < 2 * SDP_MAX_WINDOWS) {
-            if (w < cx.nw) v = ln < SDP_MAX_WINDOWS ? key32_lower<T>(plan->lo[w]) : key32_lower<T>(plan->hi[w] + 1) - 1u;
-            else v = ln < SDP_MAX_WINDOWS ? 0xFFFFFFFFu : 0xFFFFFFFEu;
-        }
-#pragma unroll
-        for (int j = 0; j < SDP_MAX_WINDOWS; ++j) {
-            cx.lo32[j] = __builtin_amdgcn_readlane(v, j);
-            cx.hi32[j] = __builtin_amdgcn_readlane(v, SDP_MAX_WINDOWS + j);
-        }
-    }
-#endif
-
-    P1Thread st;
-    st.count = st.n_valid = st.n_nan = st.n_zero = st.n_skip = 0;
-    st.isum = 0;
-    st.imin = INT64_MAX;
-    st.imax = INT64_MIN;
-    st.dmin = __builtin_inf();
-    st.dmax = -__builtin_inf();
-    st.s1 = st.s1c = st.s2 = st.s3 = st.s3c = st.s4 = 0.0;
-    st.t1 = st.t3 = 0.0;
-#pragma unroll
-    for (int w = 0; w < SDP_MAX_WINDOWS; ++w) st.gt[w] = st.eqlo[w] = st.eqhi[w] = st.wcur[w] = 0;
-
     const int64_t n = col.length;
     const int64_t nvec = n / VPT;
     const Vec16<T> *vals = (const Vec16<T> *)col.d_values;
@@ -568,7 +514,6 @@ __device__ __forceinline__ void pass1_body(const sdp_column &col, const sdp_qpla
     constexpr int U = sizeof(T) >= 8 ? P1_UNROLL : 1;
     const int64_t tile_vecs = (int64_t)P1_BLOCK * U;
     const int64_t ntiles = (nvec + tile_vecs - 1) / tile_vecs;
-    (void)vals;
     // ping-pong tiles: tile i + 1 is loading while tile i is worked on
     const VBits vbm = vbits_init(col.d_validity, col.validity_bit_offset, col.d_values);
     VecIn<T> ta[U], tb[U];
@@ -581,7 +526,7 @@ __device__ __forceinline__ void pass1_body(const sdp_column &col, const sdp_qpla
         for (int u = 0; u < U; ++u) {
             const uint32_t vbits = x[u].bits(vbm);
 #pragma unroll
-            for (int e = 0; e < VPT; ++e) p1_elem<T, WIN, INCL>(st, cx, x[u].v.v[e], (vbits >> e) & 1u);
+            for (int e = 0; e < VPT; ++e) p1_elem<T, WIN, INCL, K32>(st, cx, x[u].v.v[e], (vbits >> e) & 1u);
         }
         p1_fold(st);
     };
@@ -605,12 +550,10 @@ __device__ __forceinline__ void pass1_body(const sdp_column &col, const sdp_qpla
         const bool inb = i < n;
         T x = inb ? ((const T *)col.d_values)[i] : (T)0;
         const bool valid = inb && valid_bit(col.d_validity, col.validity_bit_offset, i);
-        p1_elem<T, WIN, INCL>(st, cx, x, valid);
+        p1_elem<T, WIN, INCL, K32>(st, cx, x, valid);
         p1_fold(st);
     }
-
-#if !defined(SDP_NO_KEY32) && !defined(SDP_K32_INLINE) && !defined(SDP_K32_SKIP_WIDEN)
-    if constexpr (INCL && Key32<T>::ok) {
+    if constexpr (INCL && K32) {
         // widen this wave's 32-bit candidate keys in place (its own stores,
         // complete after the vmcnt wait; its slots are read by no other wave)
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -622,7 +565,77 @@ __device__ __forceinline__ void pass1_body(const sdp_column &col, const sdp_qpla
             for (int64_t i = lane_id(); i < nc; i += WAVE) seg[i] = Key32<T>::widen_valid((uint32_t)seg[i]);
         }
     }
-#endif
+}
+
+// pass 1 of one column by block bx of a G-block grid (the batched launch runs
+// several columns' grids side by side, blockIdx.y = column)
+template <typename T, bool WIN, bool INCL>
+__device__ __forceinline__ void pass1_body(const sdp_column &col, const sdp_qplan *plan, P1Partial *partials,
+                                           uint64_t *cand, uint32_t *cand_counts, int64_t cap, const int G,
+                                           const int bx) {
+    P1Ctx cx;
+    cx.nw = plan->n_windows;
+#pragma unroll
+    for (int w = 0; w < SDP_MAX_WINDOWS; ++w) {
+        cx.lo[w] = w < cx.nw ? plan->lo[w] : EMPTY64;
+        cx.hi[w] = w < cx.nw ? plan->hi[w] : (INCL ? EMPTY64 - 1 : EMPTY64);
+        const int64_t seg = ((int64_t)w * G + bx) * P1_WPB + (threadIdx.x / WAVE);
+        cx.seg[w] = cand + seg * cap;
+    }
+    cx.K = plan->shift;
+    cx.cap = cap;
+    bool use32 = false;
+    if constexpr (INCL && Key32<T>::ok) {
+        // 32-bit bounds: lane j < W computes lo32[j], lane W + j hi32[j] (a
+        // 32-step search each), read back as wave-uniform values; unused windows
+        // have lo32 > hi32 (nothing inside).  The 32-bit test is exact only when
+        // every used lo has a preimage above key 0 (the key skipped elements
+        // take; lo32 == 0 happens for a window starting at INT32_MIN or 0u) and
+        // below 2^32; otherwise the column takes the 64-bit test.
+        const int ln = lane_id();
+        const int w = ln % SDP_MAX_WINDOWS;
+        uint32_t v = 0;
+        bool bad = false;
+        if (ln < 2 * SDP_MAX_WINDOWS) {
+            if (w < cx.nw) {
+                if (ln < SDP_MAX_WINDOWS) {
+                    const uint64_t l = key32_lower<T>(plan->lo[w]);
+                    bad = l == 0 || l > 0xFFFFFFFFull;
+                    v = (uint32_t)l;
+                } else {
+                    // 2^32 (no preimage of hi + 1): every 32-bit key is <= hi
+                    v = (uint32_t)(key32_lower<T>(plan->hi[w] + 1) - 1);
+                }
+            } else {
+                v = ln < SDP_MAX_WINDOWS ? 0xFFFFFFFFu : 0xFFFFFFFEu;
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < SDP_MAX_WINDOWS; ++j) {
+            cx.lo32[j] = __builtin_amdgcn_readlane(v, j);
+            cx.hi32[j] = __builtin_amdgcn_readlane(v, SDP_MAX_WINDOWS + j);
+        }
+        use32 = __builtin_amdgcn_ballot_w64(bad) == 0;
+    }
+
+    P1Thread st;
+    st.count = st.n_valid = st.n_nan = st.n_zero = st.n_skip = 0;
+    st.isum = 0;
+    st.imin = INT64_MAX;
+    st.imax = INT64_MIN;
+    st.dmin = __builtin_inf();
+    st.dmax = -__builtin_inf();
+    st.s1 = st.s1c = st.s2 = st.s3 = st.s3c = st.s4 = 0.0;
+    st.t1 = st.t3 = 0.0;
+#pragma unroll
+    for (int w = 0; w < SDP_MAX_WINDOWS; ++w) st.gt[w] = st.eqlo[w] = st.eqhi[w] = st.wcur[w] = 0;
+
+    if constexpr (INCL && Key32<T>::ok) {
+        if (use32) pass1_sweep<T, WIN, INCL, true>(st, cx, col, cap, G, bx);
+        else pass1_sweep<T, WIN, INCL, false>(st, cx, col, cap, G, bx);
+    } else {
+        pass1_sweep<T, WIN, INCL, false>(st, cx, col, cap, G, bx);
+    }
     // ---- block reduction: waves, then LDS, fixed order ----------------------
     __shared__ uint64_t s_u[P1_BLOCK / WAVE][NU];
     __shared__ int64_t s_i[P1_BLOCK / WAVE][3];
@@ -2171,7 +2184,11 @@ extern "C" int sdp_sorted_distinct(const sdp_column *col, uint64_t *d_out, void 
     if (rc) return rc;
     if (d_out == nullptr) return set_error(SDP_EINVAL, "sdp_sorted_distinct: output");
     hipStream_t s = (hipStream_t)stream;
+    // (check_col has rejected every dtype SDP_DISPATCH_NUMERIC lacks, so no
+    // kernel below is queued for a column that then fails dispatch)
     hipLaunchKernelGGL(sorted_distinct_init_kernel, dim3(1), dim3(1), 0, s, d_out);
+    rc = check_launch("sorted_distinct_init_kernel");
+    if (rc) return rc;
     const int64_t groups = (col->length + SD_E - 1) / SD_E;
     const int grid = (int)std::min<int64_t>(std::max<int64_t>((groups + SD_T - 1) / SD_T, 1), 8192);
     SDP_DISPATCH_NUMERIC(col->dtype,

@@ -436,6 +436,9 @@ __device__ __forceinline__ void bytes_tile_words(const sdp_bytes_column &col, co
         const uint32_t ad = (uint32_t)((uintptr_t)pb & 3u);
         const uint32_t *p = (const uint32_t *)(pb - ad);
         const int64_t need = len <= SHORT_MAX ? (int64_t)(ad + len + 3) >> 2 : 0;
+        // words 0-3 as ONE 16-byte load (dword-aligned: unaligned-access mode;
+        // the data buffer's 16 padding bytes cover it), word 4 only when the
+        // string reaches it -- two load instructions per row instead of five
         const bool ok = ((a.vmask >> q) & 1u) && need > 0;
         const u32x4a4 v = ok ? *(const u32x4a4 *)p : u32x4a4{0u, 0u, 0u, 0u};
         w[q][0] = v.x; w[q][1] = v.y; w[q][2] = v.z; w[q][3] = v.w;
@@ -478,42 +481,8 @@ __device__ __forceinline__ void bytes_tile_b(const sdp_bytes_column &col, int64_
     // coalesced 16-byte chunks and handed to the lanes by ds_bpermute -- was
     // measured 12 % slower on the count pass: 8.8 -> 9.9 ms per 1e9 rows)
     uint32_t w[RPT][5];
-#pragma unroll
-    for (int q = 0; q < RPT; ++q) {
-        const int64_t len = a.ln[q];
-        const uint8_t *pb = col.d_data + a.o0[q];
-        const uint32_t ad = (uint32_t)((uintptr_t)pb & 3u);
-        const uint32_t *p = (const uint32_t *)(pb - ad);
-        const int64_t need = len <= SHORT_MAX ? (int64_t)(ad + len + 3) >> 2 : 0;
-        // words 0-3 as ONE 16-byte load (dword-aligned: unaligned-access mode;
-        // the data buffer's 16 padding bytes cover it), word 4 only when the
-        // string reaches it -- two load instructions per row instead of five
-        const bool ok = ((a.vmask >> q) & 1u) && need > 0;
-        const u32x4a4 v = ok ? *(const u32x4a4 *)p : u32x4a4{0u, 0u, 0u, 0u};
-        w[q][0] = v.x; w[q][1] = v.y; w[q][2] = v.z; w[q][3] = v.w;
-        w[q][4] = (ok && need > 4) ? p[4] : 0u;
-    }
-#pragma unroll
-    for (int q = 0; q < RPT; ++q) {
-        k0[q] = k1[q] = meta[q] = h[q] = 0;
-        if (!((a.vmask >> q) & 1u)) continue;
-        const int64_t row = base + (int64_t)q * NT + t;
-        const int64_t len = a.ln[q];
-        if (len <= SHORT_MAX) {
-            const uint32_t sh = (uint32_t)((uintptr_t)(col.d_data + a.o0[q]) & 3);
-            const uint64_t v0 = (uint64_t)__builtin_amdgcn_alignbyte(w[q][1], w[q][0], sh) |
-                                ((uint64_t)__builtin_amdgcn_alignbyte(w[q][2], w[q][1], sh) << 32);
-            const uint64_t v1 = (uint64_t)__builtin_amdgcn_alignbyte(w[q][3], w[q][2], sh) |
-                                ((uint64_t)__builtin_amdgcn_alignbyte(w[q][4], w[q][3], sh) << 32);
-            k0[q] = mask_bytes(v0, len);
-            k1[q] = mask_bytes(v1, len - 8);
-            h[q] = bh_short(k0[q], k1[q], (uint64_t)len);
-        } else {
-            h[q] = hash_long_global(col.d_data + a.o0[q], len);
-            k0[q] = h[q];
-        }
-        meta[q] = ((uint64_t)min((int64_t)LEN_MAX, len) << 40) | (uint64_t)(row + 1);
-    }
+    bytes_tile_words<RPT>(col, a, w);
+    bytes_tile_decode<NT, RPT>(col, base, a, w, k0, k1, meta, h, t);
 }
 
 struct BCountLds {
@@ -669,11 +638,7 @@ struct BRecLds {
     uint32_t hist[BR_W][MAXB];
 };
 
-#ifndef SDP_BREC_3STAGE
 constexpr int BR_MINB = 4;
-#else
-constexpr int BR_MINB = 3;                  // the three-stage pipeline needs ~150 VGPRs
-#endif
 __global__ void __launch_bounds__(BR_T, BR_MINB) part_records_rows_bytes_kernel(sdp_bytes_column col, HeavyArg heavy, int b1,
                                                                        int64_t rows_per_block, uint32_t *hist,
                                                                        Chunk *chunks, uint64_t *out_k0,
@@ -693,7 +658,6 @@ __global__ void __launch_bounds__(BR_T, BR_MINB) part_records_rows_bytes_kernel(
     uint64_t rows = 0;
     int64_t cur = s0;                                               // next record slot of this strip
     constexpr int64_t STEP = (int64_t)WAVE * BR_RPT;
-#ifndef SDP_BREC_3STAGE
     BytesOffs<BR_RPT> oc, on;
     if (s0 < s1) bytes_tile_a<WAVE, BR_RPT>(col, s0, s1, oc, lane);
     for (int64_t base = s0; base < s1; base += STEP) {
@@ -703,33 +667,6 @@ __global__ void __launch_bounds__(BR_T, BR_MINB) part_records_rows_bytes_kernel(
         bytes_tile_b<WAVE, BR_RPT>(col, base, oc, k0, k1, meta, h, lane);
         const uint32_t vmask = oc.vmask;
         if (more) oc = on;
-#else
-    // three stages in flight: the offsets of tile i + 2 and the key words of
-    // tile i + 1 are loading while tile i is hashed, looked up and written
-    BytesOffs<BR_RPT> oc, on;
-    uint32_t wc[BR_RPT][5], wn[BR_RPT][5];
-    if (s0 < s1) {
-        bytes_tile_a<WAVE, BR_RPT>(col, s0, s1, oc, lane);
-        bytes_tile_words<BR_RPT>(col, oc, wc);
-        if (s0 + STEP < s1) bytes_tile_a<WAVE, BR_RPT>(col, s0 + STEP, s1, on, lane);
-    }
-    for (int64_t base = s0; base < s1; base += STEP) {
-        uint64_t k0[BR_RPT], k1[BR_RPT], meta[BR_RPT], h[BR_RPT];
-        const bool more = base + STEP < s1, more2 = base + 2 * STEP < s1;
-        BytesOffs<BR_RPT> on2;
-        if (more) bytes_tile_words<BR_RPT>(col, on, wn);                         // tile i + 1's key words
-        if (more2) bytes_tile_a<WAVE, BR_RPT>(col, base + 2 * STEP, s1, on2, lane);   // tile i + 2's offsets
-        bytes_tile_decode<WAVE, BR_RPT>(col, base, oc, wc, k0, k1, meta, h, lane);
-        const uint32_t vmask = oc.vmask;
-        if (more) {
-            oc = on;
-#pragma unroll
-            for (int q = 0; q < BR_RPT; ++q)
-#pragma unroll
-                for (int i = 0; i < 5; ++i) wc[q][i] = wn[q][i];
-        }
-        if (more2) on = on2;
-#endif
 #pragma unroll
         for (int q = 0; q < BR_RPT; ++q) {
             bool keep = false;
@@ -1747,6 +1684,12 @@ int sdp_part_rows_batch(const sdp_rows_task *d_tasks, int32_t ntasks, int32_t dt
     case SDP_F32: hipLaunchKernelGGL(part_scatter_rows_u64_batch_kernel<float>, grid, dim3(ST), 0, s, d_tasks, xm); break;
     case SDP_I64: hipLaunchKernelGGL(part_scatter_rows_u64_batch_kernel<int64_t>, grid, dim3(ST), 0, s, d_tasks, xm); break;
     case SDP_I32: hipLaunchKernelGGL(part_scatter_rows_u64_batch_kernel<int32_t>, grid, dim3(ST), 0, s, d_tasks, xm); break;
+    case SDP_I16: hipLaunchKernelGGL(part_scatter_rows_u64_batch_kernel<int16_t>, grid, dim3(ST), 0, s, d_tasks, xm); break;
+    case SDP_I8: hipLaunchKernelGGL(part_scatter_rows_u64_batch_kernel<int8_t>, grid, dim3(ST), 0, s, d_tasks, xm); break;
+    case SDP_U64: hipLaunchKernelGGL(part_scatter_rows_u64_batch_kernel<uint64_t>, grid, dim3(ST), 0, s, d_tasks, xm); break;
+    case SDP_U32: hipLaunchKernelGGL(part_scatter_rows_u64_batch_kernel<uint32_t>, grid, dim3(ST), 0, s, d_tasks, xm); break;
+    case SDP_U16: hipLaunchKernelGGL(part_scatter_rows_u64_batch_kernel<uint16_t>, grid, dim3(ST), 0, s, d_tasks, xm); break;
+    case SDP_U8: hipLaunchKernelGGL(part_scatter_rows_u64_batch_kernel<uint8_t>, grid, dim3(ST), 0, s, d_tasks, xm); break;
     default: return set_error(SDP_EINVAL, "part_rows_batch: dtype %d", dtype);
     }
     return check_launch("part_rows_batch");

@@ -739,10 +739,15 @@ class Engine:
             for kind, task, col in batched:
                 kinds.setdefault(kind, []).append((task, col))
             for (dtype, bins, mono), grp in kinds.items():
+                mg = max(t.grid for t, _ in grp)
+                for t, c in grp:      # sdp_pass2_count's own argument checks (the table is device memory)
+                    if (c.values.data_ptr() % 16 or not 0 <= t.b1 <= 10 or t.heavy.n > nat.HEAVY_MAX
+                            or t.grid > mg or mg > nat.PART_MAX_GRID):
+                        raise nat.NativeError('pass2_count_batch: a task fails the sdp_pass2_count checks')
                 arr = (nat.SdpPass2Task * len(grp))(*[t for t, _ in grp])
                 d_tasks = self._h2d(np.frombuffer(bytearray(bytes(arr)), dtype=np.uint8))
                 nat.annotate(_label(grp[0][1], 'batch'), sum(col_read_bytes(c) for _, c in grp))
-                sdp.sdp_pass2_count_batch(ptr(d_tasks), len(grp), dtype, bins, mono, max(t.grid for t, _ in grp), s)
+                sdp.sdp_pass2_count_batch(ptr(d_tasks), len(grp), dtype, bins, mono, mg, s)
                 keep_tasks.append(d_tasks)
         if not self.comm.sharded:
             raw = torch.cat([t for res, hist, _, _ in outs for t in (res[:rsz], hist.view(torch.uint8))]).cpu().numpy()
@@ -1453,6 +1458,8 @@ class Engine:
         del ctx['o1'], ctx['bsn_dev']
         ctx['stats_dev'] = torch.cat([stats, hcnt[:hv['n']]]) if hv else stats
 
+    # dtypes sdp_part_rows_batch dispatches (sdp_part.hip; bit-packed bools excluded)
+    ROWS_BATCH_DTYPES = (nat.F64, nat.F32, nat.I64, nat.I32, nat.I16, nat.I8, nat.U64, nat.U32, nat.U16, nat.U8)
     FUSE_MIN_COLS = 8                  # columns of one geometry before their stages are fused
     FUSE_BYTES = 32 << 30              # two 8-byte record buffers of a fused group alive at once
     FUSE_MAX_RECS = 1 << 26            # larger columns fill the GPU alone (and recycle their buffers)
@@ -1465,7 +1472,8 @@ class Engine:
         by, single = {}, []
         for i, c in enumerate(ctxs):
             n = c['col'].length
-            if c['isb'] or c['with_counts'] or c['large'] or c['b2'] == 0 or n == 0 or n > self.FUSE_MAX_RECS:
+            if (c['isb'] or c['with_counts'] or c['large'] or c['b2'] == 0 or n == 0 or n > self.FUSE_MAX_RECS
+                    or c['col'].dtype not in self.ROWS_BATCH_DTYPES):
                 single.append(i)
             else:
                 by.setdefault((c['b1'], c['b2'], c['col'].dtype, id(c['col']) in self._near_unique), []).append(i)
@@ -1518,14 +1526,20 @@ class Engine:
         total = int(bsns[-1][-1])
         r1, keep1 = self._records(total, False)
         tasks = (nat.SdpRowsTask * len(ctxs))()
+        max_grid = max(c['grid'] for c in ctxs)
         for j, ctx in enumerate(ctxs):
             hv = ctx['hv']
+            # the task table lives in device memory, so the checks sdp_part_rows
+            # makes on its arguments are made here (sdp.h, sdp_part_rows_batch)
+            if ctx['col'].values.data_ptr() % 16 or (hv is not None and hv['n'] > nat.HEAVY_MAX) \
+                    or ctx['grid'] > max_grid or max_grid > nat.PART_MAX_GRID:
+                raise nat.NativeError('part_rows_batch: task %d fails the sdp_part_rows checks' % j)
             tasks[j] = nat.SdpRowsTask(ctx['cs'], hv['struct'] if hv else nat.SdpHeavy(None, None, None, None, 0, 0),
                                        ctx['o1'].data_ptr(), keep1[0].data_ptr(),
                                        sdp.sdp_part_rows_per_block(ctx['col'].length, 0), b1, ctx['grid'])
         d_tasks = self._h2d(np.frombuffer(bytearray(bytes(tasks)), dtype=np.uint8))
         nat.annotate(_label(ctxs[0]['col'], 'scatter_batch'), sum(c['rb'] for c in ctxs) + total * 8)
-        sdp.sdp_part_rows_batch(ptr(d_tasks), len(ctxs), ctxs[0]['col'].dtype, max(c['grid'] for c in ctxs), s)
+        sdp.sdp_part_rows_batch(ptr(d_tasks), len(ctxs), ctxs[0]['col'].dtype, max_grid, s)
         shared = ctxs[0].pop('_shared_scan', None)
         for ctx in ctxs:
             del ctx['o1'], ctx['bsn_dev']

@@ -19,5 +19,6 @@ for ctr in FETCH_SIZE WRITE_SIZE; do
       > gpurun_out/pmc_$TAG/p$i.log 2>&1 || { echo "pass $ctr failed"; tail -5 gpurun_out/pmc_$TAG/p$i.log; exit 1; }
   echo "pmc pass $ctr ok"
 done
-python3 tools/traffic_summary.py gpurun_out/${TAG}_traffic.json $ROWS gpurun_out/pmc_$TAG/p1 gpurun_out/pmc_$TAG/p2 || exit 1
+WL=$(echo "$BENCH_ARGS" | sed -n "s/.*--workload[ =]\([a-z0-9]*\).*/\1/p")
+python3 tools/traffic_summary.py gpurun_out/${TAG}_traffic.json $ROWS:${WL:-c3} gpurun_out/pmc_$TAG/p1 gpurun_out/pmc_$TAG/p2 || exit 1
 rm -rf gpurun_out/pmc_$TAG

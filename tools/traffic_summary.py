@@ -1,6 +1,6 @@
 """HBM bytes per dispatch of every sdp kernel from rocprofv3 counter CSVs.
 
-usage: python tools/traffic_summary.py OUT.json ROWS DIR [DIR ...]
+usage: python tools/traffic_summary.py OUT.json ROWS[:WORKLOAD] DIR [DIR ...]
 
 FETCH_SIZE and WRITE_SIZE are KiB per dispatch.  On gfx950 FETCH_SIZE counts
 half the bytes of a wide coalesced read (MI355X_MICROARCH.md, "HBM [CDNA4]"),
@@ -15,7 +15,9 @@ import os
 import sys
 from collections import defaultdict
 
-out, rows = sys.argv[1], int(sys.argv[2])
+out = sys.argv[1]
+rows, _, workload = sys.argv[2].partition(':')
+rows, workload = int(rows), workload or 'c3'
 vals = defaultdict(lambda: defaultdict(list))          # kernel -> counter -> per-dispatch values
 for d in sys.argv[3:]:
     for f in glob.glob(os.path.join(d, '**', '*counter_collection.csv'), recursive=True):
@@ -33,7 +35,7 @@ for k, c in sorted(vals.items()):
     res[k] = {'dispatches': max(len(f), len(w)), 'fetch_bytes': round(fb), 'write_bytes': round(wb),
               'traffic_bytes': round(fb + wb)}
 with open(out, 'w') as fh:
-    json.dump({'rows': rows, 'source': 'rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, one pass each, '
+    json.dump({'rows': rows, 'workload': workload, 'source': 'rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, one pass each, '
                                        'bench.py --steps 1 --warmup 0; FETCH_SIZE x2 (gfx950), KiB -> bytes',
                'kernels': res}, fh, indent=1)
 print('wrote', out, len(res), 'kernels')
