@@ -7,7 +7,8 @@
                                    vs independent torch code on the device:
                                    distinct counts (torch.unique), top-50 by
                                    (count desc, key asc) and the two "Other"
-                                   rows, every NUM statistic (torch_ref)
+                                   rows, every NUM statistic (torch_ref); the
+                                   hex ids again with 5 % nulls (CAT +1 quirk)
   C5  1e7 x 512 fp32               the Pearson matrix vs a torch fp64 Gram of
                                    the same device data (1e-9), every NUM
                                    column's statistics vs torch_ref
@@ -78,7 +79,21 @@ def test_c4_high_cardinality_1e9():
     assert [int(x) for x in fr.values] == want_val
     assert row['top'] == want_idx[0] and int(row['freq']) == want_val[0]
     assert not problems, '\n'.join(problems)
-    del table
+    # the same hex ids with 5 % nulls (a validity bitmap over the same strings):
+    # the CAT distinct count gains the +1 for nulls (describe.py:169-170), the
+    # top-50 and Other rows count only valid rows
+    from spark_df_profiling.columns import DeviceColumn, DeviceTable
+    from test_gpu_scale_1e9 import check_string_column
+    hx = table.column('hex_id')
+    hn = DeviceColumn('hex_id_nulls', 'string', n, 'bytes')
+    hn.offsets, hn.data, hn.offset_width = hx.offsets, hx.data, hx.offset_width
+    hn.validity = bench._validity(n, bench._gen(bench.SEED + 4003, dev), dev)
+    t2 = DeviceTable([table.column('u32_range_i64'), hn], n)
+    d2 = describe(t2, plots=False)
+    del t2
+    torch.cuda.empty_cache()
+    check_string_column(d2, hn, 'hex_id_nulls', n)
+    del table, hn, d2
     torch.cuda.empty_cache()
 
 

@@ -110,3 +110,54 @@ def test_spark_like_input(tmp_path):
     assert 'data:image/png' in html and 'reclat_city' in html
     with pytest.raises(TypeError):
         describe(object())
+
+
+def test_int32_extremes_at_window_bounds():
+    """4-byte integer columns whose quantile windows start at the type's
+    smallest key (INT32_MIN, 0u) or end at its largest (INT32_MAX,
+    UINT32_MAX), with nulls: pass 1's 32-bit window test must not take the
+    null rows' key 0 as candidates, nor drop the maximum (sdp_numeric.hip,
+    pass1_body's lo32/hi32; describe.py:203-208 percentiles)."""
+    import oracle
+    from spark_df_profiling import describe
+    rng = np.random.default_rng(41)
+    for n in (97, 300, 5000):
+        a = rng.integers(-100, 100, n).astype(np.int32)
+        a[rng.integers(0, n)] = np.iinfo(np.int32).min
+        a[rng.integers(0, n)] = np.iinfo(np.int32).max
+        u = rng.integers(0, 100, n).astype(np.uint32)
+        u[rng.integers(0, n)] = 0
+        u[rng.integers(0, n)] = np.iinfo(np.uint32).max
+        lo_only = rng.integers(-100, 100, n).astype(np.int32)
+        lo_only[rng.permutation(n)[:3]] = np.iinfo(np.int32).min + np.arange(3)
+        masks = [rng.random(n) < 0.15 for _ in range(3)]
+        t = pa.table({'i32': pa.array(a, mask=masks[0]), 'u32': pa.array(u, mask=masks[1]),
+                      'i32_low': pa.array(lo_only, mask=masks[2])})
+        assert_describe_equal(describe(t, plots=False), oracle.describe(t))
+
+
+def test_uint32_wide_fused_group(monkeypatch):
+    """Eight or more high-cardinality uint32 columns (dtype SDP_U32, range over
+    2^20, 64 K..2^26 rows) take the fused wide-table distinct-count path
+    (engine._group_middle_fused -> sdp_part_rows_batch), describe.py:143."""
+    import oracle
+    from spark_df_profiling import describe
+    rng = np.random.default_rng(43)
+    n = 100_000
+    cols = {}
+    for j in range(9):
+        v = rng.integers(0, 2 ** 32, n, dtype=np.uint64).astype(np.uint32)
+        if j % 3 == 0:
+            v[:n // 4] = v[n // 2:n // 2 + n // 4]          # repeats: distinct < rows
+        cols['u%d' % j] = pa.array(v, mask=rng.random(n) < 0.05)
+    t = pa.table(cols)
+    from spark_df_profiling.engine import Engine
+    fused = []
+    orig = Engine._group_middle_fused
+
+    def spy(self, ctxs, bsns):
+        fused.append([c['col'].dtype for c in ctxs])
+        return orig(self, ctxs, bsns)
+    monkeypatch.setattr(Engine, '_group_middle_fused', spy)
+    assert_describe_equal(describe(t, plots=False), oracle.describe(t))
+    assert fused and all(d == 9 for grp in fused for d in grp), fused     # SDP_U32 = 9

@@ -12,7 +12,10 @@ no libsdp):
   Percentile interpolation on the exact order statistics (torch.unique) --
   exact; int distinct counts (torch.unique) -- exact;
 * distinct counts of f32_uniform and date (torch.unique), and the LDS-bitmap
-  and hash-partition paths agree on i64_uniform_1e6.
+  and hash-partition paths agree on i64_uniform_1e6;
+* the three utf8 columns (5 % nulls): distinct count with the CAT +1 for
+  nulls, top-50 by (count desc, key asc) and both Other rows, against a
+  lexicographic sort of the strings as 16-byte keys.
 Needs an MI355X with ~260 GB free.
 """
 
@@ -23,6 +26,32 @@ import torch_ref
 pytestmark = pytest.mark.gpu
 
 ROWS = 10 ** 9
+
+
+OTHER = ['***Other Values***', '***Other Values Distinct Count***']
+
+
+def check_string_column(d, col, name, nrows):
+    """One CAT string column of a describe() result vs torch: the strings as
+    16-byte keys (torch_ref.short_string_keys), grouped by a lexicographic sort."""
+    valid = torch_ref.valid_mask(col, nrows)
+    n_valid = int(valid.sum().item())
+    k0, k1 = torch_ref.short_string_keys(col, nrows, valid)
+    del valid
+    D, pairs, m = torch_ref.top_groups_pairs(k0, k1, 50)
+    del k0, k1
+    row = d['variables'].loc[name]
+    assert row['type'] == 'CAT', (name, row['type'])
+    assert int(row['count']) == m == n_valid, name
+    assert int(row['n_missing']) == nrows - n_valid, name
+    # CAT: countDistinct ignores nulls, then +1 when any value is missing (describe.py:169-170)
+    assert int(row['distinct_count']) == D + (1 if nrows > n_valid else 0), (name, int(row['distinct_count']), D)
+    want_idx = [torch_ref.key_pair_to_str(*kp) for kp, _ in pairs] + OTHER
+    want_val = [c for _, c in pairs] + [m - sum(c for _, c in pairs), D - len(pairs)]
+    fr = d['freq'][name]
+    assert list(fr.index) == want_idx, (name, list(fr.index)[:5], want_idx[:5])
+    assert [int(x) for x in fr.values] == want_val, name
+    assert row['top'] == want_idx[0] and int(row['freq']) == want_val[0], name
 
 
 def test_bench_table_properties_1e9():
@@ -63,6 +92,11 @@ def test_bench_table_properties_1e9():
         del vals
         assert int(v.loc[name, 'distinct_count']) == want, name
     assert int(v.loc['i64_id', 'distinct_count']) == int(v.loc['i64_id', 'count'])
+    # utf8 columns (CAT, 5 % nulls): exact distinct + the null quirk, top-50 by
+    # (count desc, key asc) and both Other rows (describe.py:143,169-170,251-263)
+    for name in ('str_card100', 'str_card1e5', 'str_card1e8'):
+        check_string_column(d, cols[name], name, ROWS)
+        torch.cuda.empty_cache()
     eng = Engine(device=dev)
     c = cols['i64_uniform_1e6']
     by_bitmap = int(v.loc['i64_uniform_1e6', 'distinct_count'])

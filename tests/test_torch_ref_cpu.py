@@ -66,3 +66,26 @@ def test_hex_top_groups():
     want = sorted(cc.items(), key=lambda kv: (-kv[1], kv[0]))[:50]
     assert D == len(cc) and rows == 5000
     assert [(torch_ref.key_to_hex(k), c) for k, c in pairs] == want
+
+
+def test_short_string_keys_and_pair_groups():
+    """The 1e9-row string checker (torch_ref.short_string_keys +
+    top_groups_pairs) against a plain Python count on ragged strings with
+    nulls, ties and prefixes of one another."""
+    import torch
+    rng = np.random.default_rng(5)
+    alphabet = [b'a', b'b', b'ab', b'abc', b'abcdefgh', b'abcdefghi', b'zzzzzzzzzzzzzzzz', b'q', b'0123456789abcdef']
+    vals = [alphabet[i] if rng.random() > 0.1 else None for i in rng.integers(0, len(alphabet), 3000)]
+    data = b''.join(v for v in vals if v) + b'\0' * 16
+    offs = [0]
+    for v in vals:
+        offs.append(offs[-1] + (len(v) if v else 0))
+    col = types.SimpleNamespace(data=torch.tensor(list(data), dtype=torch.uint8),
+                                offsets=torch.tensor(offs, dtype=torch.int64), fixed_width=0)
+    valid = torch.tensor([v is not None for v in vals])
+    k0, k1 = torch_ref.short_string_keys(col, len(vals), valid, chunk=1000)
+    D, pairs, m = torch_ref.top_groups_pairs(k0, k1, 4)
+    cnt = collections.Counter(v for v in vals if v is not None)
+    want = sorted(cnt.items(), key=lambda kv: (-kv[1], kv[0]))[:4]
+    assert (D, m) == (len(cnt), sum(cnt.values()))
+    assert [(torch_ref.key_pair_to_str(*kp).encode(), c) for kp, c in pairs] == want

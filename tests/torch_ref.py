@@ -242,3 +242,72 @@ def top_groups(keys, k=50):
     pairs = list(zip(uk[sel].cpu().tolist(), uc[sel].cpu().tolist()))
     pairs.sort(key=lambda kc: (-kc[1], kc[0]))
     return D, pairs, int(uc.sum().item())
+
+
+def short_string_keys(col, nrows, valid, chunk=1 << 24):
+    """utf8/binary strings of <= 16 bytes with no NUL byte -> (k0, k1) int64
+    tensors of the valid rows: bytes 0-7 and 8-15, big-endian, zero padded,
+    sign bit flipped, so (k0, k1) in signed lexicographic order is the strings'
+    bytewise order and equal pairs are equal strings (the padding is
+    unambiguous without NULs).  Asserts both conditions."""
+    import torch
+    dev = col.data.device
+    offs = col.offsets
+    assert col.fixed_width == 0
+    shifts = torch.arange(56, -8, -8, dtype=torch.int64, device=dev)          # big-endian byte weights
+    j = torch.arange(16, dtype=torch.int64, device=dev)
+    k0s, k1s = [], []
+    flip = -(1 << 63)
+    for s in range(0, nrows, chunk):
+        e = min(nrows, s + chunk)
+        vm = valid[s:e]
+        o0 = offs[s:e][vm].to(torch.int64)
+        ln = offs[s + 1:e + 1][vm].to(torch.int64) - o0
+        assert int(ln.max().item()) <= 16 if ln.numel() else True
+        inb = j[None, :] < ln[:, None]
+        b = col.data[(o0[:, None] + j[None, :]).clamp(max=col.data.numel() - 1)].to(torch.int64) * inb
+        assert not bool(((b == 0) & inb).any().item()), 'NUL byte in a string key'
+        k0s.append(((b[:, :8] << shifts[None, :]).sum(1)) ^ flip)
+        k1s.append(((b[:, 8:] << shifts[None, :]).sum(1)) ^ flip)
+        del b, inb, o0, ln
+    return torch.cat(k0s), torch.cat(k1s)
+
+
+def key_pair_to_str(k0, k1):
+    """Inverse of short_string_keys for one (k0, k1) pair."""
+    raw = (((int(k0) ^ -(1 << 63)) & ((1 << 64) - 1)).to_bytes(8, 'big')
+           + ((int(k1) ^ -(1 << 63)) & ((1 << 64) - 1)).to_bytes(8, 'big'))
+    return raw.rstrip(b'\x00').decode('utf8')
+
+
+def top_groups_pairs(k0, k1, k=50):
+    """top_groups for 16-byte keys given as (k0, k1) pairs: groups by a
+    lexicographic sort (two stable sorts), then (distinct, [((k0, k1), count)]
+    top-k by count desc / key asc, rows).  Frees its inputs' copies as it goes."""
+    import torch
+    m = k0.numel()
+    perm1 = torch.sort(k1, stable=True).indices
+    k0p = k0[perm1]
+    s0, perm2 = torch.sort(k0p, stable=True)
+    del k0p
+    perm = perm1[perm2]
+    del perm1, perm2
+    s1 = k1[perm]
+    del perm
+    new = torch.ones(m, dtype=torch.bool, device=k0.device)
+    new[1:] = (s0[1:] != s0[:-1]) | (s1[1:] != s1[:-1])
+    starts = torch.nonzero(new).flatten()
+    del new
+    D = int(starts.numel())
+    counts = torch.diff(torch.cat([starts, torch.tensor([m], device=starts.device)]))
+    kk = min(k, D)
+    vals, _ = torch.topk(counts, kk)
+    T = int(vals[-1].item())
+    sel_gt = torch.nonzero(counts > T).flatten()
+    eq = torch.nonzero(counts == T).flatten()[:kk - int(sel_gt.numel())]    # groups are in key order
+    sel = torch.cat([sel_gt, eq])
+    pos = starts[sel]
+    pairs = list(zip(zip(s0[pos].cpu().tolist(), s1[pos].cpu().tolist()), counts[sel].cpu().tolist()))
+    pairs.sort(key=lambda kc: (-kc[1], kc[0]))
+    del s0, s1, starts, counts
+    return D, pairs, m
