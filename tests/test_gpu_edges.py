@@ -147,8 +147,7 @@ def test_uint32_wide_fused_group(monkeypatch):
     cols = {}
     for j in range(9):
         v = rng.integers(0, 2 ** 32, n, dtype=np.uint64).astype(np.uint32)
-        if j % 3 == 0:
-            v[:n // 4] = v[n // 2:n // 2 + n // 4]          # repeats: distinct < rows
+        v[:n // 40] = v[n // 2:n // 2 + n // 40]          # repeats: distinct < rows, still near-unique
         cols['u%d' % j] = pa.array(v, mask=rng.random(n) < 0.05)
     t = pa.table(cols)
     from spark_df_profiling.engine import Engine
