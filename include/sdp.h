@@ -572,6 +572,93 @@ int sdp_gram(const sdp_column *cols, int32_t ncols, const uint32_t *d_keep,
              const double *d_shift, void *d_work, int64_t work_bytes,
              double *d_gram, double *d_colsum, double *d_n, void *stream);
 
+/* ---- coarse entry points: one call per reference operation group ----------
+ * SURVEY.md §8(b)'s contract.  Each is a C++ orchestrator (sdp_api.cpp) over the
+ * kernels above for ONE column (or one set of columns) on one device, so a host
+ * in any language gets a statistic from this header alone (INTEGRATION.md §2
+ * shows a C caller).  Common rules:
+ *   - d_work: ONE caller-owned device workspace of at least the matching
+ *     *_workspace_bytes(...) bytes (the library carves it up; nothing is
+ *     allocated or freed);
+ *   - work is queued on `stream`; entries marked SYNC read small results back
+ *     between stages (bucket starts, group counts, count thresholds) and so
+ *     synchronise `stream` -- their outputs are HOST structs; the others are
+ *     fully stream-ordered and write DEVICE outputs;
+ *   - NaN is one value (countDistinct / groupBy), -0.0 groups with 0.0, nulls
+ *     are ignored (na.drop), as Spark does. */
+
+/* describe.py:233 (date / timestamp min and max over na.drop, and the count of
+ * describe.py:144): one pass, stream-ordered.  Integral / date (int32 days) /
+ * timestamp (int64) columns fill imin/imax; float columns dmin/dmax. */
+typedef struct sdp_minmax_result {
+    uint64_t count;                    /* valid, non-NaN rows                      */
+    int64_t  imin, imax;
+    double   dmin, dmax;
+} sdp_minmax_result;
+int64_t sdp_minmax_workspace_bytes(int64_t length, int32_t dtype);
+int sdp_minmax_int(const sdp_column *col, void *d_work, int64_t work_bytes, sdp_minmax_result *d_out,
+                   void *stream);
+
+/* describe.py:203-208: the percentiles of one numeric column at the host
+ * probabilities probs[0 .. n_probs) (n_probs <= 16), as describe() reports
+ * them -- integral columns: Spark `percentile` (linear interpolation at
+ * (N-1) p between the exact order statistics); float columns: the element of
+ * rank ceil(p N) (`percentile_approx`'s answer within its rank bound; p <=
+ * 1e-4 -> rank 1, p >= 1 - 1e-4 -> rank N).  N = na.drop rows; d_out[i] = NaN
+ * when N = 0.  Exact radix selects over the column's keys; stream-ordered (the
+ * ranks are computed on the device from the device-side N). */
+#define SDP_QUANTILES_MAX 16
+int64_t sdp_quantiles_workspace_bytes(int64_t length, int32_t n_probs);
+int sdp_quantiles(const sdp_column *col, const double *probs, int32_t n_probs, void *d_work, int64_t work_bytes,
+                  double *d_out, void *stream);
+
+/* describe.py:143: countDistinct of one column (exactly one of col / bcol
+ * non-NULL; byte keys compared bytewise).  SYNC.  Path: integral ranges <=
+ * 2^20 -> LDS bitmaps; >= 64 K rows -> two-level hash partitioning with exact
+ * offsets + LDS de-duplication (sdp_part_*); otherwise, or when the
+ * partitioning reports a collision / full table, the global table. */
+typedef struct sdp_distinct_result {
+    uint64_t distinct;                 /* groups among non-null rows               */
+    uint64_t rows;                     /* non-null rows                            */
+    int32_t  path;                     /* 0 bitmap, 1 partitioned, 2 global table  */
+    int32_t  _pad;
+} sdp_distinct_result;
+int64_t sdp_distinct_workspace_bytes(int64_t length, int32_t is_bytes);
+int sdp_hash_distinct_count(const sdp_column *col, const sdp_bytes_column *bcol, void *d_work, int64_t work_bytes,
+                            sdp_distinct_result *h_out, void *stream);
+
+/* describe.py:251-263: value counts of one column (groupBy(c).count() over
+ * na.drop rows) and the first k groups by (count desc, key asc) -- the
+ * orderBy + limit(50) of the reference, with the tie order defined.  SYNC.
+ * h_top[0 .. h_out->n_top) receive {key, count}: fixed-width columns the
+ * order-preserving 64-bit key (key_f64 / key_i64 inverses: sign-flip for
+ * integers; sign-flip / invert for floats), byte columns the 0-based row index
+ * of one row holding the value.  ***Other Values*** = rows - sum(counts);
+ * ***Other Values Distinct Count*** = groups - n_top. */
+typedef struct sdp_topk_entry {
+    uint64_t key;
+    uint64_t count;
+} sdp_topk_entry;
+typedef struct sdp_topk_result {
+    uint64_t groups;                   /* distinct values among non-null rows      */
+    uint64_t rows;                     /* non-null rows                            */
+    int32_t  n_top;                    /* min(k, groups)                           */
+    int32_t  path;                     /* 1 partitioned, 2 global table            */
+} sdp_topk_result;
+int64_t sdp_value_counts_workspace_bytes(int64_t length, int32_t is_bytes);
+int sdp_value_counts_topk(const sdp_column *col, const sdp_bytes_column *bcol, int32_t k, void *d_work,
+                          int64_t work_bytes, sdp_topk_result *h_out, sdp_topk_entry *h_top, void *stream);
+
+/* utils.py:20-36: the Pearson matrix of ncols numeric columns (host array of
+ * column structs) with listwise deletion (a row counts only if every column is
+ * valid and, for float columns, not NaN), rho[i][j] = C_ij / sqrt(C_ii C_jj)
+ * from the shifted fp64 Gram on MFMA (C = G - s s^T / n, shift = each column's
+ * sample median).  d_corr: ncols x ncols row-major doubles (device); *d_n: the
+ * rows kept (device double).  SYNC (the column descriptors are staged once). */
+int64_t sdp_pearson_workspace_bytes(int64_t length, int32_t ncols);
+int sdp_gram_f64(const sdp_column *cols, int32_t ncols, void *d_work, int64_t work_bytes, double *d_corr,
+                 double *d_n, void *stream);
+
 #ifdef __cplusplus
 }
 #endif

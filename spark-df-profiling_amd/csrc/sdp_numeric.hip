@@ -12,6 +12,7 @@
 // every result is deterministic for a given grid.
 #include <type_traits>
 #include "sdp_heavy.h"
+#include "sdp_internal.h"
 
 namespace sdp {
 
@@ -963,10 +964,13 @@ struct SelState {
     uint64_t result;
 };
 
-__global__ void select_init_kernel(SelState *st, uint64_t prefix, int64_t k, int shift, uint64_t *hist) {
+// d_k (nullable): the rank is read from device memory (a rank computed on the
+// device from a device-side count, sdp_quantiles) instead of `k`
+__global__ void select_init_kernel(SelState *st, uint64_t prefix, int64_t k, int shift, uint64_t *hist,
+                                   const int64_t *d_k) {
     if (threadIdx.x == 0) {
         st->prefix = prefix;
-        st->k = k;
+        st->k = d_k ? *d_k : k;
         st->shift = shift;
         st->done = 0;
         st->result = EMPTY64;
@@ -1825,13 +1829,20 @@ static int sel_shift0(uint64_t lo_key, uint64_t hi_key) {
 extern "C" int sdp_select_kth(const uint64_t *d_keys, const uint64_t *d_n, int64_t n_cap, int64_t k,
                               uint64_t lo_key, uint64_t hi_key, void *d_work, int64_t work_bytes,
                               uint64_t *d_result, void *stream) {
+    return select_kth_dev(d_keys, d_n, n_cap, k, nullptr, lo_key, hi_key, d_work, work_bytes, d_result, stream);
+}
+
+int select_kth_dev(const uint64_t *d_keys, const uint64_t *d_n, int64_t n_cap, int64_t k, const int64_t *d_k,
+                   uint64_t lo_key, uint64_t hi_key, void *d_work, int64_t work_bytes, uint64_t *d_result,
+                   void *stream) {
     if (n_cap < 0 || k < 0 || d_result == nullptr) return set_error(SDP_EINVAL, "sdp_select_kth: args");
     if (work_bytes < sdp_select_kth_workspace_bytes(n_cap)) return set_error(SDP_ECAP, "sdp_select_kth: workspace");
     const SelWork L = sel_layout(d_work, n_cap);
     const int shift0 = sel_shift0(lo_key, hi_key);
     const uint64_t prefix0 = shift0 + 11 < 64 ? (lo_key >> (shift0 + 11)) : 0ull;
     hipStream_t s = (hipStream_t)stream;
-    hipLaunchKernelGGL(select_init_kernel, dim3(1), dim3(256), 0, s, L.st, prefix0, k, shift0, L.hist);
+    hipLaunchKernelGGL(select_init_kernel, dim3(1), dim3(256), 0, s, L.st, prefix0, k, shift0, L.hist,
+                       (const int64_t *)d_k);
     int rc = check_launch("select_init_kernel");
     if (rc) return rc;
     const uint64_t *cur = d_keys, *cur_n = d_n;
@@ -1865,7 +1876,7 @@ extern "C" int sdp_select_init(int64_t k, uint64_t lo_key, uint64_t hi_key, void
     const int shift0 = sel_shift0(lo_key, hi_key);
     const uint64_t prefix0 = shift0 + 11 < 64 ? (lo_key >> (shift0 + 11)) : 0ull;
     hipLaunchKernelGGL(select_init_kernel, dim3(1), dim3(256), 0, (hipStream_t)stream, L.st, prefix0, k, shift0,
-                       d_hist);
+                       d_hist, (const int64_t *)nullptr);
     return check_launch("select_init_kernel");
 }
 

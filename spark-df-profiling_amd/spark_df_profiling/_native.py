@@ -118,6 +118,27 @@ class SdpPass2Result(ctypes.Structure):
                 ('n_unbinned', ctypes.c_uint64)]
 
 
+class SdpMinmaxResult(ctypes.Structure):           # sdp_minmax_result (sdp_minmax_int)
+    _fields_ = [('count', ctypes.c_uint64), ('imin', ctypes.c_int64), ('imax', ctypes.c_int64),
+                ('dmin', ctypes.c_double), ('dmax', ctypes.c_double)]
+
+
+class SdpDistinctResult(ctypes.Structure):         # sdp_distinct_result (sdp_hash_distinct_count)
+    _fields_ = [('distinct', ctypes.c_uint64), ('rows', ctypes.c_uint64), ('path', ctypes.c_int32),
+                ('_pad', ctypes.c_int32)]
+
+
+class SdpTopkEntry(ctypes.Structure):              # sdp_topk_entry
+    _fields_ = [('key', ctypes.c_uint64), ('count', ctypes.c_uint64)]
+
+
+class SdpTopkResult(ctypes.Structure):             # sdp_topk_result (sdp_value_counts_topk)
+    _fields_ = [('groups', ctypes.c_uint64), ('rows', ctypes.c_uint64), ('n_top', ctypes.c_int32),
+                ('path', ctypes.c_int32)]
+
+
+QUANTILES_MAX = 16       # SDP_QUANTILES_MAX
+
 _P = ctypes.c_void_p
 _I32 = ctypes.c_int32
 _I64 = ctypes.c_int64
@@ -201,13 +222,27 @@ _SIGNATURES = {
     'sdp_rowmask': (ctypes.c_int, [_COL, ctypes.POINTER(_I32), _I32, _P, _I64, _P, _P]),
     'sdp_gram_workspace_bytes': (_I64, [_I64, _I32]),
     'sdp_gram': (ctypes.c_int, [_COL, _I32, _P, _P, _P, _I64, _P, _P, _P, _P]),
+    # coarse entries (sdp_api.cpp): one call per reference operation group
+    'sdp_minmax_workspace_bytes': (_I64, [_I64, _I32]),
+    'sdp_minmax_int': (ctypes.c_int, [_COL, _P, _I64, _P, _P]),
+    'sdp_quantiles_workspace_bytes': (_I64, [_I64, _I32]),
+    'sdp_quantiles': (ctypes.c_int, [_COL, ctypes.POINTER(_D), _I32, _P, _I64, _P, _P]),
+    'sdp_distinct_workspace_bytes': (_I64, [_I64, _I32]),
+    'sdp_hash_distinct_count': (ctypes.c_int, [_COL, _BCOL, _P, _I64, ctypes.POINTER(SdpDistinctResult), _P]),
+    'sdp_value_counts_workspace_bytes': (_I64, [_I64, _I32]),
+    'sdp_value_counts_topk': (ctypes.c_int, [_COL, _BCOL, _I32, _P, _I64, ctypes.POINTER(SdpTopkResult),
+                                             ctypes.POINTER(SdpTopkEntry), _P]),
+    'sdp_pearson_workspace_bytes': (_I64, [_I64, _I32]),
+    'sdp_gram_f64': (ctypes.c_int, [_COL, _I32, _P, _I64, _P, _P, _P]),
 }
 
 _VALUE_FUNCS = {'sdp_last_error', 'sdp_version', 'sdp_pass1_workspace_bytes', 'sdp_pass2_workspace_bytes',
                 'sdp_pass1_grid', 'sdp_gram_workspace_bytes', 'sdp_part_rows_per_block', 'sdp_part_bucket_target',
                 'sdp_part_records_chunks', 'sdp_gk_workspace_bytes',
                 'sdp_scan_workspace_bytes', 'sdp_bitmap_workspace_bytes', 'sdp_select_kth_workspace_bytes',
-                'sdp_select_rounds', 'sdp_pass2_count_workspace_bytes'}
+                'sdp_select_rounds', 'sdp_pass2_count_workspace_bytes', 'sdp_minmax_workspace_bytes',
+                'sdp_quantiles_workspace_bytes', 'sdp_distinct_workspace_bytes', 'sdp_value_counts_workspace_bytes',
+                'sdp_pearson_workspace_bytes'}
 _STATUS_FUNCS = set(_SIGNATURES) - _VALUE_FUNCS
 
 _lib = None

@@ -52,7 +52,9 @@ STRUCTS = {'sdp_column': 'SdpColumn', 'sdp_bytes_column': 'SdpBytesColumn', 'sdp
            'sdp_records': 'SdpRecords', 'sdp_heavy': 'SdpHeavy', 'sdp_chunk': 'SdpChunk',
            'sdp_select_task': 'SdpSelectTask', 'sdp_compact_task': 'SdpCompactTask',
            'sdp_pass1_task': 'SdpPass1Task', 'sdp_pass2_task': 'SdpPass2Task',
-           'sdp_rows_task': 'SdpRowsTask'}
+           'sdp_rows_task': 'SdpRowsTask', 'sdp_minmax_result': 'SdpMinmaxResult',
+           'sdp_distinct_result': 'SdpDistinctResult', 'sdp_topk_entry': 'SdpTopkEntry',
+           'sdp_topk_result': 'SdpTopkResult'}
 
 
 def test_struct_layouts_match_c():
@@ -124,3 +126,13 @@ def test_select_rounds_host_arithmetic():
     assert sdp.sdp_select_rounds(0, 2048) == 2
     assert sdp.sdp_select_rounds(1 << 40, (1 << 40) + 5) == 1
     assert sdp.sdp_select_rounds(0, (1 << 64) - 1) == 6
+
+
+def test_c_caller_compiles_against_header():
+    """examples/c_caller/sdp_profile.c -- a C host of the coarse entry points
+    (sdp_quantiles, sdp_hash_distinct_count, sdp_value_counts_topk,
+    sdp_minmax_int, sdp_gram_f64, sdp_pass1/2) -- is plain C11 against
+    include/sdp.h and the HIP runtime header (gcc, no GPU needed)."""
+    src = os.path.join(ROOT, 'examples', 'c_caller', 'sdp_profile.c')
+    subprocess.run(['gcc', '-std=c11', '-Wall', '-Werror', '-fsyntax-only', '-D__HIP_PLATFORM_AMD__',
+                    '-I/opt/rocm/include', '-I' + os.path.join(ROOT, 'include'), src], check=True)
