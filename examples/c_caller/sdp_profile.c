@@ -219,9 +219,9 @@ static void string_column(const char *name, sdp_bytes_column bc, const int64_t *
     sdp_distinct_result dr;
     CHECK_SDP(sdp_hash_distinct_count(NULL, &bc, work, dw, &dr, s));
     CHECK_HIP(hipFree(work));
-    printf("%s\"%s\": {\"kind\": \"str\", \"rows\": %llu, \"groups\": %llu, \"distinct\": %llu, \"top\": [",
-           first ? "" : ",", name, (unsigned long long)tr.rows, (unsigned long long)tr.groups,
-           (unsigned long long)dr.distinct);
+    printf("%s\"%s\": {\"kind\": \"str\", \"rows\": %llu, \"groups\": %llu, \"distinct\": %llu, \"path\": %d, "
+           "\"top\": [", first ? "" : ",", name, (unsigned long long)tr.rows, (unsigned long long)tr.groups,
+           (unsigned long long)dr.distinct, tr.path);
     for (int i = 0; i < tr.n_top; ++i) {
         const int64_t r = (int64_t)top[i].key;
         printf("%s[", i ? ", " : "");

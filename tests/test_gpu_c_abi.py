@@ -95,6 +95,11 @@ def test_c_host_matches_oracle(tmp_path, n, seed):
     got = json.loads(out.stdout)
     want, raw = oracle.profile_raw(table)
     v = want['variables']
+    assert list(got['columns']) == [x[1] for x in spec]
+    # both grouping paths are exercised: partitions at >= 64 K rows, the global table below
+    path = 1 if n >= (1 << 16) else 2
+    assert got['columns']['label']['path'] == path and got['columns']['i64_wide']['distinct_path'] == path
+    assert got['columns']['i32_small']['distinct_path'] == 0                  # LDS bitmap (range <= 2^20)
     bad = []
     for name, c in got['columns'].items():
         row = v.loc[name]
