@@ -50,29 +50,116 @@ def as_device_table(df, device=None) -> DeviceTable:
         # the reference's inputs come from spark.read.parquet (examples/Demo.ipynb:63)
         return DeviceTable.from_parquet(str(df), device=device)
     if type(df).__module__.startswith('pyspark'):
-        return DeviceTable.from_arrow(spark_to_arrow(df), device)
+        return spark_to_device(df, device)
+    batches = _batch_stream(df)
+    if batches is not None:
+        from . import ingest
+        schema, it, rows = batches
+        return ingest.stream_batches(schema, rows, it, device)
     raise TypeError('df must be of type pyspark.sql.DataFrame, pyarrow.Table, a .parquet path or DeviceTable')
 
 
-def spark_to_arrow(df):
-    """A Spark DataFrame (pyspark is optional: only its duck type is used)
-    collected to the driver as Arrow, never row by row -- the counterpart of
-    the reference's per-statistic Spark jobs (describe.py:71-283) is one
-    columnar collect followed by HBM-resident passes:
-      Spark >= 4.0   df.toArrow()                       -> pyarrow.Table
-      Spark 2.3-3.x  df._collect_as_arrow()             -> [RecordBatch]
+def _batch_stream(obj):
+    """(schema, batch iterable, rows or None) of an Arrow RecordBatchReader, a
+    list of RecordBatches or an iterator yielding them; None for anything else."""
+    import itertools
+    if isinstance(obj, pa.RecordBatchReader):
+        return obj.schema, obj, None
+    if isinstance(obj, (list, tuple)):
+        if obj and all(isinstance(b, pa.RecordBatch) for b in obj):
+            return obj[0].schema, obj, sum(b.num_rows for b in obj)
+        return None
+    if hasattr(obj, '__next__') and hasattr(obj, '__iter__'):
+        first = next(obj, None)
+        if not isinstance(first, pa.RecordBatch):
+            return None
+        return first.schema, itertools.chain([first], obj), None
+    return None
+
+
+def spark_batches(df):
+    """A Spark DataFrame (pyspark is optional: only its duck type is used) as
+    Arrow RecordBatches for the staging pipeline, never row by row -- the
+    counterpart of the reference's per-statistic Spark jobs (describe.py:71-283)
+    is one columnar transfer followed by HBM-resident passes.  Returns
+    (schema or None, batches, rows or None):
+      Spark >= 4.0   df.toArrow()                  -> the Table's batches
+      Spark 2.3-3.x  df._collect_as_arrow()        -> its batches (a list, or an
+                                                      iterator: streamed as they come)
       otherwise      df.toPandas() (Arrow-accelerated when
-                     spark.sql.execution.arrow.enabled) -> pyarrow.Table"""
-    to_arrow = getattr(df, 'toArrow', None) or getattr(df, '_collect_as_arrow', None)
+                     spark.sql.execution.arrow.enabled)"""
+    to_arrow = getattr(df, 'toArrow', None)
     if to_arrow is not None:
-        got = to_arrow()
-        if isinstance(got, (list, tuple)):
-            got = pa.Table.from_batches(list(got)) if got else pa.table({})
-        return got
+        t = to_arrow()
+        return t.schema, t.to_batches(), t.num_rows
+    collect = getattr(df, '_collect_as_arrow', None)
+    if collect is not None:
+        got = collect()
+        if isinstance(got, pa.Table):
+            return got.schema, got.to_batches(), got.num_rows
+        st = _batch_stream(got if isinstance(got, (list, tuple)) else iter(got))
+        if st is None:
+            if isinstance(got, (list, tuple)) and not got:
+                return None, [], 0
+            raise TypeError('_collect_as_arrow() did not yield pyarrow RecordBatches')
+        return st
     to_pandas = getattr(df, 'toPandas', None)
     if to_pandas is None:
         raise TypeError('Spark DataFrame without toArrow/_collect_as_arrow/toPandas')
-    return pa.Table.from_pandas(to_pandas(), preserve_index=False)
+    t = pa.Table.from_pandas(to_pandas(), preserve_index=False)
+    return t.schema, t.to_batches(), t.num_rows
+
+
+def spark_to_arrow(df):
+    """spark_batches collected into one Arrow Table (host)."""
+    schema, batches, _ = spark_batches(df)
+    batches = list(batches)
+    if schema is None:
+        return pa.table({})
+    return pa.Table.from_batches(batches, schema=schema)
+
+
+_SPARK_KIND = {'tinyint': 'fixed', 'smallint': 'fixed', 'int': 'fixed', 'bigint': 'fixed', 'float': 'fixed',
+               'double': 'fixed', 'boolean': 'fixed', 'date': 'fixed', 'timestamp': 'fixed',
+               'string': 'bytes', 'binary': 'bytes'}
+
+
+def apply_spark_dtypes(table: DeviceTable, dtypes):
+    """Dispatch by Spark's own type strings (`df.dtypes`, describe.py:137) where
+    the DataFrame provides them: the column's spark_type becomes Spark's string
+    (e.g. 'decimal(10,2)', which describe.py:158-164 sends to CAT/UNIQUE).  A
+    string of another storage kind than the transferred Arrow column is
+    rejected (the transfer does not match the DataFrame)."""
+    for col in table.columns:
+        st = dtypes.get(col.name)
+        if st is None or st == col.spark_type:
+            continue
+        kind = 'bytes' if st.startswith('decimal') else _SPARK_KIND.get(st)
+        if kind is not None and col.kind not in (kind, 'null'):
+            raise TypeError('column %s: Spark type %s but the Arrow transfer holds %s' % (col.name, st,
+                                                                                   col.spark_type))
+        col.spark_type = st
+    return table
+
+
+def spark_to_device(df, device=None) -> DeviceTable:
+    """A Spark DataFrame straight into HBM: its Arrow batches go through the
+    pinned double-buffered staging pipeline (ingest.stream_batches) as they
+    arrive -- a batch iterator is never concatenated on the host -- and the
+    column types dispatch by `df.dtypes` (describe.py:137)."""
+    from . import ingest
+    rows_hint = None
+    count = getattr(df, 'count', None)
+    schema, batches, rows = spark_batches(df)
+    if rows is None and callable(count):
+        rows_hint = int(count())                  # the reference's n = df.count() (describe.py:71)
+    if schema is None:
+        raise ValueError('df cannot be empty')
+    table = ingest.stream_batches(schema, rows, batches, device, rows_hint=rows_hint)
+    dtypes = getattr(df, 'dtypes', None)
+    if dtypes:
+        apply_spark_dtypes(table, dict(dtypes))
+    return table
 
 
 def _series(values, col: DeviceColumn) -> pd.Series:

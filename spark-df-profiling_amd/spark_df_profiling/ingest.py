@@ -117,7 +117,10 @@ def _bitmap_bytes(buf, offset, length, start_bit):
 
 
 class _ColumnSink:
-    """Device buffers of one column, filled batch by batch."""
+    """Device buffers of one column, filled batch by batch.  `n` = the rows
+    the stream will produce when known up front (buffers sized once), else a
+    first capacity: the buffers then grow by 1.5x on the device (a stream of
+    unknown length, e.g. Spark batches without a count)."""
 
     def __init__(self, name, t: pa.DataType, n, device, stager):
         self.name, self.t, self.n, self.device, self.st = name, t, n, device, stager
@@ -126,11 +129,9 @@ class _ColumnSink:
         self.nulls = 0
         self.fallback = []                          # chunks of a type the stream does not cover
         self.kind = None
-        nbits = (n + 7) // 8 + 8
+        self.cap = n
         if pa.types.is_boolean(t):
             self.kind = 'bool'
-            self.values = torch.zeros(nbits, dtype=torch.uint8, device=device)
-            self._partials = {}
         elif pa.types.is_date32(t) or pa.types.is_timestamp(t) or t in _NUMERIC_DTYPE:
             self.kind = 'fixed'
             if pa.types.is_date32(t):
@@ -140,45 +141,72 @@ class _ColumnSink:
             else:
                 self.dtype = _NUMERIC_DTYPE[t][0]
                 self.width = nat.ELEM_SIZE[self.dtype]
-            self.values = torch.empty(n * self.width + 16, dtype=torch.uint8, device=device)
-            self.values[n * self.width:].zero_()
         elif pa.types.is_string(t) or pa.types.is_binary(t) or pa.types.is_large_string(t) \
                 or pa.types.is_large_binary(t):
             self.kind = 'bytes'
             self.owidth = 4
-            self.offsets = torch.empty(n + 1, dtype=torch.int32, device=device)
-            self.offsets[:1].zero_()
             self.data = torch.empty(max(1 << 20, 16), dtype=torch.uint8, device=device)
             self.nbytes = 0
         if self.kind is not None:
-            self.validity = torch.empty(nbits, dtype=torch.uint8, device=device)
-            self.validity[(n + 7) // 8:].zero_()
+            self._alloc_rows(n, 0)
             self._partials = {}                     # last byte written mid-byte, per bitmap
 
-    def _put_bits(self, dst: torch.Tensor, buf, offset, length):
-        """Append `length` bits (Arrow bitmap buffer at bit `offset`) at row self.row."""
+    def _alloc_rows(self, cap, used):
+        """(Re)allocate the row-indexed buffers for `cap` rows, keeping the
+        first `used` rows (copied on the staging stream, after their uploads)."""
+        nbits = (cap + 7) // 8 + 8
+        ub = (used + 7) // 8                       # bitmap bytes holding rows < used
+
+        def grow(name, numel, dtype, keep, zero_from):
+            old = getattr(self, name, None)
+            new = torch.empty(numel, dtype=dtype, device=self.device)
+            with torch.cuda.stream(self.st.stream):
+                if old is not None and keep:
+                    new[:keep].copy_(old[:keep], non_blocking=True)
+                    old.record_stream(self.st.stream)
+                new[zero_from:].zero_()
+            setattr(self, name, new)
+        grow('validity', nbits, torch.uint8, ub, ub)
+        if self.kind == 'bool':
+            grow('values', nbits, torch.uint8, ub, ub)
+        elif self.kind == 'fixed':
+            grow('values', cap * self.width + 16, torch.uint8, used * self.width, cap * self.width)   # padding
+        elif self.kind == 'bytes':
+            dt = torch.int32 if self.owidth == 4 else torch.int64
+            grow('offsets', cap + 1, dt, used + 1 if used else 1, cap + 1)
+            if not used:
+                with torch.cuda.stream(self.st.stream):
+                    self.offsets[:1].zero_()
+        self.cap = cap
+
+    def _ensure_rows(self, m):
+        if self.row + m > self.cap:
+            self._alloc_rows(max(self.row + m, int(self.cap * 1.5) + 8, 1 << 16), self.row)
+
+    def _put_bits(self, which, buf, offset, length):
+        """Append `length` bits (Arrow bitmap buffer at bit `offset`) at row
+        self.row to the bitmap `which` ('validity' or 'values')."""
+        dst = getattr(self, which)
         b, partial = _bitmap_bytes(buf, offset, length, self.row)
         first = self.row // 8
         if partial:
             # OR the first (shared) byte with what the previous chunk left in it
             b = b.copy()
-            b[0] |= np.uint8(self._last_partial(dst))
+            b[0] |= np.uint8(self._partials.get(which, 0))
         self.st.upload(b, dst[first:first + b.nbytes])
-        self._partials[id(dst)] = int(b[-1]) if (self.row + length) % 8 else 0
-
-    def _last_partial(self, dst):
-        return self._partials.get(id(dst), 0)
+        self._partials[which] = int(b[-1]) if (self.row + length) % 8 else 0
 
     def add(self, arr: pa.Array):
         if self.kind is None:
             self.fallback.append(arr)
             return
         m = len(arr)
+        self._ensure_rows(m)
         bufs = arr.buffers()
         self.nulls += arr.null_count
-        self._put_bits(self.validity, bufs[0] if arr.null_count else None, arr.offset, m)
+        self._put_bits('validity', bufs[0] if arr.null_count else None, arr.offset, m)
         if self.kind == 'bool':
-            self._put_bits(self.values, bufs[1], arr.offset, m)
+            self._put_bits('values', bufs[1], arr.offset, m)
         elif self.kind == 'fixed':
             w = self.width
             src = np.frombuffer(bufs[1], dtype=np.uint8, count=m * w, offset=arr.offset * w)
@@ -224,6 +252,7 @@ class _ColumnSink:
         self.owidth = 8
 
     def finish(self) -> DeviceColumn:
+        self.n = self.row
         if self.kind is None:
             arr = pa.chunked_array(self.fallback, type=self.t) if self.fallback else pa.array([], type=self.t)
             return column_from_arrow(self.name, arr, self.device)
@@ -250,14 +279,17 @@ def _streamable(t: pa.DataType) -> bool:
             or pa.types.is_large_binary(t))
 
 
-def stream_batches(schema: pa.Schema, num_rows: int, batches: Iterable[pa.RecordBatch], device=None,
-                   stats: Optional[dict] = None) -> DeviceTable:
-    """Upload a stream of RecordBatches (decoded on a background thread while
-    the previous one is staged) into one DeviceTable."""
+def stream_batches(schema: pa.Schema, num_rows: Optional[int], batches: Iterable[pa.RecordBatch], device=None,
+                   stats: Optional[dict] = None, rows_hint: Optional[int] = None) -> DeviceTable:
+    """Upload a stream of RecordBatches (produced on a background thread while
+    the previous one is staged) into one DeviceTable.  num_rows = the exact
+    row count when known (checked), None for a stream of unknown length (the
+    device buffers grow; `rows_hint` sizes them first)."""
     device = torch.device(device or 'cuda')
     t0 = time.perf_counter()
     st = PinnedStager(device)
-    sinks = [_ColumnSink(f.name, f.type, num_rows, device, st) for f in schema]
+    first_cap = num_rows if num_rows is not None else max(int(rows_hint or 0), 1 << 16)
+    sinks = [_ColumnSink(f.name, f.type, first_cap, device, st) for f in schema]
     q: queue.Queue = queue.Queue(maxsize=2)
     err = []
 
@@ -276,14 +308,18 @@ def stream_batches(schema: pa.Schema, num_rows: int, batches: Iterable[pa.Record
         b = q.get()
         if b is None:
             break
+        if b.schema.names != schema.names:
+            raise ValueError('record batch columns %s differ from the stream schema %s' % (b.schema.names,
+                                                                                        schema.names))
         for s, a in zip(sinks, b.columns):
             s.add(a)
         rows += b.num_rows
     th.join()
     if err:
         raise err[0]
-    if rows != num_rows:
+    if num_rows is not None and rows != num_rows:
         raise ValueError('stream produced %d rows, expected %d' % (rows, num_rows))
+    num_rows = rows
     st.finish()
     table = DeviceTable([s.finish() for s in sinks], num_rows)
     torch.cuda.synchronize(device)

@@ -265,10 +265,31 @@ def _sample_frame(df, n):
         pf = pq.ParquetFile(str(df))
         return pa.Table.from_batches([next(pf.iter_batches(batch_size=max(n, 1)))]).slice(0, n).to_pandas() \
             if pf.metadata.num_rows else pd.DataFrame()
+    if isinstance(df, (list, tuple)) and df and all(isinstance(b, pa.RecordBatch) for b in df):
+        return pa.Table.from_batches(list(df)).slice(0, n).to_pandas()
+    if isinstance(df, pa.RecordBatchReader):
+        raise TypeError('a RecordBatchReader is read once: pass describe() the reader, or ProfileReport '
+                        'an iterator of RecordBatches')
     limit = getattr(df, 'limit', None)
     if limit is not None:
         return df.limit(n).toPandas()
     raise TypeError('df must be of type pyspark.sql.DataFrame, pyarrow.Table, a .parquet path or DeviceTable')
+
+
+def _sample_batches(it, n):
+    """The first n rows of a RecordBatch iterator as pandas, and an iterator
+    that yields every batch again (the sampled ones first)."""
+    import itertools
+    head, rows = [], 0
+    for b in it:
+        head.append(b)
+        rows += b.num_rows
+        if rows >= n:
+            break
+    if head and not all(isinstance(b, pa.RecordBatch) for b in head):
+        raise TypeError('df must be of type pyspark.sql.DataFrame, pyarrow.Table, a .parquet path or DeviceTable')
+    frame = pa.Table.from_batches(head).slice(0, n).to_pandas() if head else pd.DataFrame()
+    return frame, itertools.chain(head, it)
 
 
 class ProfileReport(object):
@@ -277,7 +298,10 @@ class ProfileReport(object):
     file = None
 
     def __init__(self, df, bins=10, sample=100, corr_reject=0.9, **kwargs):
-        sample = _sample_frame(df, sample)
+        if hasattr(df, '__next__') and hasattr(df, '__iter__'):       # a stream of RecordBatches
+            sample, df = _sample_batches(df, sample)
+        else:
+            sample = _sample_frame(df, sample)
         description_set = describe(df, bins=bins, corr_reject=corr_reject, **kwargs)
         self.html = to_html(sample, description_set)
         self.description_set = description_set

@@ -129,3 +129,81 @@ def test_profile_report_to_file(tmp_path):
     assert 'data:image/png;base64' in text                  # histograms rendered
     assert set(rep.get_description()) == {'table', 'variables', 'freq'}
     assert 'reclat_city' in rep.get_rejected_variables(0.9)
+
+
+def _ragged_batches(tab, sizes):
+    """tab's rows as a generator of RecordBatches of cycling (odd) sizes."""
+    start = 0
+    while start < tab.num_rows:
+        for m in sizes:
+            if start >= tab.num_rows:
+                return
+            for b in tab.slice(start, m).to_batches():
+                yield b
+            start += m
+
+
+class _SparkStream:
+    """A Spark DataFrame duck type whose Arrow transfer is an ITERATOR of
+    RecordBatches of ragged sizes (Spark 3.x _collect_as_arrow batches as they
+    arrive), with df.count() and df.dtypes (describe.py:71,137)."""
+
+    def __init__(self, tab, sizes, dtypes=None):
+        self._t, self._sizes = tab, sizes
+        self.dtypes = dtypes if dtypes is not None else [
+            (f.name, __import__('spark_df_profiling.columns', fromlist=['x']).spark_type_string(f.type))
+            for f in tab.schema]
+        self.pulled = 0
+
+    def count(self):
+        return self._t.num_rows
+
+    def _collect_as_arrow(self):
+        for b in _ragged_batches(self._t, self._sizes):
+            self.pulled += 1
+            yield b
+
+    def limit(self, n):
+        return _SparkStream(self._t.slice(0, n), self._sizes, self.dtypes)
+
+    def toPandas(self):
+        return self._t.to_pandas()
+
+
+_SparkStream.__module__ = 'pyspark.sql.dataframe'
+
+
+@pytest.mark.parametrize('sizes', [[70_001, 3, 12_345, 8], [1000, 9, 4096, 17]])
+def test_streamed_spark_batches_vs_oracle(sizes):
+    """§8(f3): a Spark-like DataFrame's batch iterator goes straight into the
+    pinned double-buffered stager (no host concatenation; device buffers grow
+    from 64 K rows when the stream's length is unknown), ragged batch sizes,
+    every column type -- describe() equals the oracle on the same rows."""
+    import oracle
+    from spark_df_profiling import ProfileReport, describe
+    tab = _table(150_003, seed=11)
+    want = oracle.describe(tab)
+    sdf = _SparkStream(tab, sizes)
+    assert_describe_equal(describe(sdf, plots=False), want)
+    assert sdf.pulled > 3                                       # consumed batch by batch
+    # a bare iterator of batches (no count: buffers grow) and a RecordBatchReader
+    assert_describe_equal(describe(_ragged_batches(tab, sizes), plots=False), want)
+    reader = pa.RecordBatchReader.from_batches(tab.schema, _ragged_batches(tab, sizes))
+    assert_describe_equal(describe(reader, plots=False), want)
+    rep = ProfileReport(_ragged_batches(tab, sizes), sample=7)
+    assert_describe_equal(rep.get_description(), oracle.describe(tab))
+    assert 'Dataset info' in rep.to_html()
+
+
+def test_spark_dtypes_dispatch():
+    """describe.py:137 dispatches on Spark's df.dtypes strings: a column Spark
+    types as decimal(12,2) is never 'decimal', so it is profiled as CAT/UNIQUE
+    (describe.py:158-164) -- whatever the Arrow transfer looked like."""
+    from spark_df_profiling import describe
+    tab = _table(20_000, seed=5).select(['f64', 'dec', 'word'])
+    sdf = _SparkStream(tab, [4096, 77], dtypes=[('f64', 'double'), ('dec', 'decimal(12,2)'), ('word', 'string')])
+    d = describe(sdf, plots=False)
+    assert d['variables'].loc['dec', 'type'] in ('CAT', 'UNIQUE')
+    bad = _SparkStream(tab, [4096], dtypes=[('f64', 'double'), ('dec', 'decimal(12,2)'), ('word', 'bigint')])
+    with pytest.raises(TypeError, match='word'):
+        describe(bad, plots=False)

@@ -217,3 +217,52 @@ def test_fusable_groups_wide_tables_only():
     e.FUSE_BYTES = 16 * 3 * 10 ** 7                                        # three columns per group
     fuse, single = e._fusable([ctx() for _ in range(8)])
     assert fuse == [[0, 1, 2], [3, 4, 5], [6, 7]] and single == []
+
+
+def test_spark_batches_and_stream_inputs():
+    """describe.spark_batches / _batch_stream (no GPU: nothing is uploaded):
+    Spark-like objects of each transfer style and plain batch streams give
+    (schema, batches, rows or None); an iterator is not consumed up front."""
+    import pyarrow as pa
+    from spark_df_profiling.describe import _batch_stream, spark_batches
+    t = pa.table({'a': pa.array([1, 2, None, 4, 5]), 's': pa.array(['x', None, 'z', 'w', 'v'])})
+
+    class S4:
+        def toArrow(self):
+            return t
+
+    class S3:
+        def _collect_as_arrow(self):
+            return t.to_batches(max_chunksize=2)
+
+    class S3It:
+        pulled = 0
+
+        def _collect_as_arrow(self):
+            for b in t.to_batches(max_chunksize=2):
+                S3It.pulled += 1
+                yield b
+
+    sch, bs, rows = spark_batches(S4())
+    assert sch == t.schema and rows == 5 and pa.Table.from_batches(list(bs)).equals(t)
+    sch, bs, rows = spark_batches(S3())
+    assert rows == 5 and pa.Table.from_batches(list(bs)).equals(t)
+    sch, bs, rows = spark_batches(S3It())
+    assert rows is None and sch == t.schema and S3It.pulled == 1       # only the first batch peeked
+    assert pa.Table.from_batches(list(bs)).equals(t) and S3It.pulled == 3
+    assert _batch_stream([1, 2]) is None and _batch_stream(iter([1])) is None
+    rd = pa.RecordBatchReader.from_batches(t.schema, t.to_batches(max_chunksize=3))
+    assert _batch_stream(rd)[2] is None
+
+
+def test_apply_spark_dtypes_cpu():
+    import pyarrow as pa
+    import pytest
+    from spark_df_profiling.columns import DeviceTable
+    from spark_df_profiling.describe import apply_spark_dtypes
+    t = pa.table({'a': pa.array([1, 2, 3], pa.int64()), 's': pa.array(['x', 'y', 'z'])})
+    dt = DeviceTable.from_arrow(t, device='cpu', streamed=False)
+    apply_spark_dtypes(dt, {'a': 'bigint', 's': 'string'})
+    assert [c.spark_type for c in dt.columns] == ['bigint', 'string']
+    with pytest.raises(TypeError):
+        apply_spark_dtypes(dt, {'s': 'double'})
