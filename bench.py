@@ -321,6 +321,8 @@ def label_kernels(label):
         return ['sdp::part_dedup_bytes_kernel'] if dt == 'bytes' else ['sdp::part_dedup_u64']
     if name in ('sdp_pass1', 'sdp_pass2', 'sdp_pass2_count'):
         return ['sdp::%s_kernel<%s' % (name[4:], _DT.get(dt, dt))]
+    if name == 'sdp_distinct32':
+        return ['sdp::d32_']
     if name == 'sdp_gram':
         return ['sdp::gram_kernel<', 'sdp::gram_wide_kernel', 'sdp::gram_reduce_kernel']
     return []

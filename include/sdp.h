@@ -542,6 +542,18 @@ int sdp_part_dedup(const sdp_records *in, int32_t is_bytes, const sdp_bytes_colu
                    const uint64_t *d_starts, int64_t nbuckets, int32_t with_counts,
                    uint64_t *d_out_key, uint64_t *d_out_cnt, uint32_t *d_ngroups,
                    uint64_t *d_stats, void *stream);
+/* countDistinct (describe.py:143) of a column whose keys fit 32 bits: float32
+ * (NaN one value, -0.0 == 0.0), or an integral column with imax - imin < 2^32
+ * (key = v - lo, lo = imin).  Nulls are skipped.  h = mix32(key) (a bijection)
+ * is partitioned as 4-byte records into 64 x 64 buckets (the level-1 scatter
+ * also counts the level-2 buckets, so no count pass of records) and every
+ * final bucket's low 20 bits are set in a 128 KB LDS bitmap: no hash table.
+ * Stream-ordered, no host round trip.  d_out[0] += distinct values, d_out[1]
+ * += non-null rows (d_out zeroed by the caller).  Workspace:
+ * sdp_distinct32_workspace_bytes(length) (two 4-byte record buffers + scans). */
+int64_t sdp_distinct32_workspace_bytes(int64_t length);
+int sdp_distinct32(const sdp_column *col, int64_t lo, void *d_work, int64_t work_bytes, uint64_t *d_out,
+                   void *stream);
 /* Pack the per-bucket groups: src[d_starts[f] ..+ngroups[f]) -> dst[d_out_offsets[f] ..). */
 int sdp_part_compact(const uint64_t *d_src_a, const uint64_t *d_src_b, const uint64_t *d_starts,
                      const uint32_t *d_ngroups, const uint64_t *d_out_offsets, int64_t nbuckets,

@@ -1636,6 +1636,242 @@ static void launch_rows_u64(int phase, int grid, hipStream_t s, const sdp_column
                            xcd_map_enabled());
 }
 
+
+// ---- 32-bit key spaces: partitions of 4-byte records + LDS bitmaps -------------
+// countDistinct (describe.py:143) of a column whose keys fit 32 bits -- float32
+// (its order-preserving 32-bit key, NaN one value, -0.0 == 0.0) or an integral
+// column with imax - imin < 2^32 (key = v - imin).  h = mix32(key) is a
+// bijection of [0, 2^32), so distinct h == distinct keys, and h needs no
+// table: the top 6 bits pick one of 64 level-1 buckets, the next 6 one of 64
+// level-2 buckets, and the low 20 bits index a 2^20-bit LDS bitmap of the final
+// bucket.  Records are the 4-byte h (the 64-bit path moves 8-byte records
+// through a count, two scatters and a hash-table de-duplication).  The level-1
+// scatter also counts every (level-1 bucket, level-2 bucket) pair of its block
+// (64 x 64 LDS counters), so the level-2 offsets need no count pass of their
+// own; both scatters write runs of ~256 records per bucket per tile.
+constexpr int D32_B1 = 6, D32_B2 = 6;
+constexpr int D32_NB1 = 1 << D32_B1, D32_NB2 = 1 << D32_B2, D32_NF = D32_NB1 * D32_NB2;
+constexpr int D32_BM_WORDS = 1 << (32 - D32_B1 - D32_B2 - 5);   // 2^20 bits -> 32 K words (128 KB)
+
+__device__ __forceinline__ uint32_t mix32(uint32_t x) {
+    x ^= x >> 16;
+    x *= 0x85EBCA6Bu;
+    x ^= x >> 13;
+    x *= 0xC2B2AE35u;
+    x ^= x >> 16;
+    return x;
+}
+template <typename T>
+__device__ __forceinline__ uint32_t key32_rel(T v, int64_t lo) {
+    if constexpr (std::is_same<T, float>::value) return v != v ? 0xFFC00000u : Key32<float>::key(v);
+    else return (uint32_t)(uint64_t)((int64_t)v - lo);
+}
+
+// One tile of NT * RPT rows as 32-bit hashes (16-byte loads of full tiles)
+template <typename T, int NT, int RPT>
+struct RowTile32 {
+    static constexpr int VPT = Vec16<T>::N;
+    static constexpr int NV = RPT / VPT;
+    VecIn<T> v[NV];
+    bool full;
+    __device__ __forceinline__ void load(const sdp_column &c, const VBits &vbm, int64_t base, int64_t end) {
+        full = base + (int64_t)NT * RPT <= end && (base % VPT) == 0;
+        if (!full) return;
+        const Vec16<T> *vals = (const Vec16<T> *)c.d_values;
+#pragma unroll
+        for (int u = 0; u < NV; ++u) v[u].load(vals, vbm, base / VPT + (int64_t)u * NT + threadIdx.x, INT64_MAX);
+    }
+    __device__ __forceinline__ void hash(const sdp_column &c, const VBits &vbm, int64_t base, int64_t end, int64_t lo,
+                                         uint32_t (&h)[RPT], uint32_t &vmask) const {
+        vmask = 0;
+        if (full) {
+#pragma unroll
+            for (int u = 0; u < NV; ++u) {
+                const uint32_t vb = v[u].bits(vbm);
+#pragma unroll
+                for (int e = 0; e < VPT; ++e) {
+                    const int q = u * VPT + e;
+                    h[q] = mix32(key32_rel<T>(v[u].v.v[e], lo));
+                    vmask |= ((vb >> e) & 1u) << q;
+                }
+            }
+            return;
+        }
+#pragma unroll
+        for (int q = 0; q < RPT; ++q) {
+            // slot q of thread t: the same row as the vector layout above
+            const int64_t i = base + ((int64_t)(q / VPT) * NT + threadIdx.x) * VPT + q % VPT;
+            h[q] = 0;
+            if (i < end) {
+                const bool ok = valid_bit(c.d_validity, c.validity_bit_offset, i);
+                h[q] = mix32(key32_rel<T>(((const T *)c.d_values)[i], lo));
+                vmask |= (uint32_t)ok << q;
+            }
+        }
+    }
+};
+
+constexpr int D32_CT = 256, D32_C_RPT = 16;
+template <typename T>
+__global__ void __launch_bounds__(D32_CT) d32_count_kernel(sdp_column col, int64_t lo, int64_t rows_per_block,
+                                                            uint32_t *hist1, uint64_t *stats) {
+    __shared__ uint32_t s_h[D32_CT / WAVE][D32_NB1];       // wave-private counters
+    const int G = gridDim.x, g = blockIdx.x, t = threadIdx.x, w = t / WAVE;
+    for (int i = t; i < (D32_CT / WAVE) * D32_NB1; i += D32_CT) (&s_h[0][0])[i] = 0;
+    lds_barrier();
+    const int64_t r0 = (int64_t)g * rows_per_block, r1 = min(col.length, r0 + rows_per_block);
+    RowTile32<T, D32_CT, D32_C_RPT> tile;
+    const VBits vbm = vbits_init(col.d_validity, col.validity_bit_offset, col.d_values);
+    uint64_t rows = 0;
+    for (int64_t base = r0; base < r1; base += D32_CT * D32_C_RPT) {
+        uint32_t h[D32_C_RPT], vmask;
+        tile.load(col, vbm, base, r1);
+        tile.hash(col, vbm, base, r1, lo, h, vmask);
+        rows += __popc(vmask);
+#pragma unroll
+        for (int q = 0; q < D32_C_RPT; ++q)
+            if ((vmask >> q) & 1u) atomicAdd(&s_h[w][h[q] >> (32 - D32_B1)], 1u);
+    }
+    lds_barrier();
+    for (int b = t; b < D32_NB1; b += D32_CT) {
+        uint32_t s = 0;
+        for (int k = 0; k < D32_CT / WAVE; ++k) s += s_h[k][b];
+        hist1[(int64_t)b * G + g] = s;
+    }
+    block_add_u64(rows, &stats[1]);
+}
+
+struct D32ScatterLds {
+    uint32_t hist[D32_NB1];
+    uint32_t off[D32_NB1];
+    uint64_t cur[D32_NB1];
+    uint32_t h2[D32_NF];
+    uint32_t stage[S_TILE];
+    uint32_t wsum[ST / WAVE];
+};
+
+// level 1: rows -> 64 buckets of 4-byte records, + the block's (b1, b2) counts
+template <typename T>
+__global__ void __launch_bounds__(ST) d32_scatter1_kernel(sdp_column col, int64_t lo, int64_t rows_per_block,
+                                                           const uint64_t *offs1, uint32_t *out, uint32_t *h2) {
+    __shared__ D32ScatterLds s;
+    const int G = gridDim.x, g = blockIdx.x, t = threadIdx.x;
+    for (int b = t; b < D32_NB1; b += ST) {
+        s.hist[b] = 0;
+        s.cur[b] = offs1[(int64_t)b * G + g];
+    }
+    for (int f = t; f < D32_NF; f += ST) s.h2[f] = 0;
+    lds_barrier();
+    const int64_t r0 = (int64_t)g * rows_per_block, r1 = min(col.length, r0 + rows_per_block);
+    RowTile32<T, ST, S_RPT> tile;
+    const VBits vbm = vbits_init(col.d_validity, col.validity_bit_offset, col.d_values);
+    if (r0 < r1) tile.load(col, vbm, r0, r1);
+    for (int64_t base = r0; base < r1; base += S_TILE) {
+        uint32_t h[S_RPT], vmask, rank[S_RPT];
+        tile.hash(col, vbm, base, r1, lo, h, vmask);
+        if (base + S_TILE < r1) tile.load(col, vbm, base + S_TILE, r1);      // next tile in flight
+#pragma unroll
+        for (int q = 0; q < S_RPT; ++q) {
+            if ((vmask >> q) & 1u) {
+                rank[q] = atomicAdd(&s.hist[h[q] >> (32 - D32_B1)], 1u);
+                atomicAdd(&s.h2[h[q] >> (32 - D32_B1 - D32_B2)], 1u);
+            }
+        }
+        lds_barrier();
+        block_excl_scan<ST>(s.hist, s.off, D32_NB1, s.wsum);
+#pragma unroll
+        for (int q = 0; q < S_RPT; ++q)
+            if ((vmask >> q) & 1u) s.stage[s.off[h[q] >> (32 - D32_B1)] + rank[q]] = h[q];
+        lds_barrier();
+        const uint32_t total = s.off[D32_NB1 - 1] + s.hist[D32_NB1 - 1];
+        for (uint32_t j = t; j < total; j += ST) {
+            const uint32_t x = s.stage[j];
+            const int b = (int)(x >> (32 - D32_B1));
+            out[s.cur[b] + (j - s.off[b])] = x;
+        }
+        lds_barrier();
+        for (int b = t; b < D32_NB1; b += ST) {
+            s.cur[b] += s.hist[b];
+            s.hist[b] = 0;
+        }
+        lds_barrier();
+    }
+    // (b1, b2) counts of this block's runs, laid out [b1][b2][block] for the scan
+    for (int f = t; f < D32_NF; f += ST) h2[(int64_t)f * G + g] = s.h2[f];
+}
+
+// level 2: every level-1 run (bucket b1, block g) -> its 64 sub-buckets
+__global__ void __launch_bounds__(ST) d32_scatter2_kernel(const uint32_t *in, const uint64_t *offs1,
+                                                           const uint64_t *offs2, int G, uint32_t *out) {
+    __shared__ D32ScatterLds s;
+    const int t = threadIdx.x;
+    const int64_t c = blockIdx.x;                          // = b1 * G + g
+    const int b1 = (int)(c / G), g = (int)(c % G);
+    const uint64_t start = offs1[c], end = offs1[c + 1];
+    for (int b = t; b < D32_NB2; b += ST) {
+        s.hist[b] = 0;
+        s.cur[b] = offs2[((int64_t)b1 * D32_NB2 + b) * G + g];
+    }
+    lds_barrier();
+    for (uint64_t base = start; base < end; base += S_TILE) {
+        uint32_t x[S_RPT], rank[S_RPT];
+#pragma unroll
+        for (int q = 0; q < S_RPT; ++q) {
+            const uint64_t r = base + (uint64_t)q * ST + t;
+            x[q] = r < end ? in[r] : 0u;
+        }
+#pragma unroll
+        for (int q = 0; q < S_RPT; ++q)
+            if (base + (uint64_t)q * ST + t < end) rank[q] = atomicAdd(&s.hist[(x[q] >> 20) & (D32_NB2 - 1)], 1u);
+        lds_barrier();
+        block_excl_scan<ST>(s.hist, s.off, D32_NB2, s.wsum);
+#pragma unroll
+        for (int q = 0; q < S_RPT; ++q)
+            if (base + (uint64_t)q * ST + t < end) s.stage[s.off[(x[q] >> 20) & (D32_NB2 - 1)] + rank[q]] = x[q];
+        lds_barrier();
+        const uint32_t total = s.off[D32_NB2 - 1] + s.hist[D32_NB2 - 1];
+        for (uint32_t j = t; j < total; j += ST) {
+            const uint32_t y = s.stage[j];
+            const int b = (int)((y >> 20) & (D32_NB2 - 1));
+            out[s.cur[b] + (j - s.off[b])] = y;
+        }
+        lds_barrier();
+        for (int b = t; b < D32_NB2; b += ST) {
+            s.cur[b] += s.hist[b];
+            s.hist[b] = 0;
+        }
+        lds_barrier();
+    }
+}
+
+// one workgroup per final bucket: its records' low 20 bits into an LDS bitmap,
+// then the set bits counted (distinct keys of the bucket)
+__global__ void __launch_bounds__(1024) d32_bitmap_kernel(const uint32_t *in, const uint64_t *offs2, int G,
+                                                           uint64_t *out) {
+    __shared__ uint32_t bm[D32_BM_WORDS];
+    const int t = threadIdx.x;
+    const int64_t f = blockIdx.x;
+    for (int i = t; i < D32_BM_WORDS; i += 1024) bm[i] = 0;
+    lds_barrier();
+    const uint64_t start = offs2[f * G], end = offs2[(f + 1) * G];
+    constexpr int R = 8;                                   // records in flight per thread
+    for (uint64_t base = start; base < end; base += (uint64_t)1024 * R) {
+        uint32_t x[R];
+#pragma unroll
+        for (int q = 0; q < R; ++q) {
+            const uint64_t r = base + (uint64_t)q * 1024 + t;
+            x[q] = r < end ? in[r] : 0u;
+        }
+#pragma unroll
+        for (int q = 0; q < R; ++q)
+            if (base + (uint64_t)q * 1024 + t < end) atomicOr(&bm[(x[q] >> 5) & (D32_BM_WORDS - 1)], 1u << (x[q] & 31));
+    }
+    lds_barrier();
+    uint64_t cnt = 0;
+    for (int i = t; i < D32_BM_WORDS; i += 1024) cnt += (uint64_t)__popc(bm[i]);
+    block_add_u64(cnt, &out[0]);
+}
+
 }  // namespace sdp
 
 using namespace sdp;
@@ -1895,3 +2131,79 @@ int sdp_scan_u32(const uint32_t *d_in, int64_t n, uint64_t *d_out, void *d_work,
 }
 
 }  // extern "C"
+
+// ---- countDistinct of 32-bit key spaces (d32_* kernels) --------------------------
+struct D32Layout {
+    int G;
+    int64_t rpb;
+    uint32_t *hist1, *h2, *recs1, *recs2;
+    uint64_t *offs1, *offs2;
+    void *scan1, *scan2;
+    int64_t scan1_bytes, scan2_bytes, total;
+};
+static int64_t d32_align(int64_t x) { return (x + 255) / 256 * 256; }
+static D32Layout d32_layout(void *d_work, int64_t length) {
+    D32Layout L;
+    L.rpb = sdp_part_rows_per_block(length, 0);
+    L.G = (int)std::max<int64_t>(1, (length + L.rpb - 1) / L.rpb);
+    const int64_t n1 = (int64_t)D32_NB1 * L.G, n2 = (int64_t)D32_NF * L.G;
+    L.scan1_bytes = sdp_scan_workspace_bytes(n1);
+    L.scan2_bytes = sdp_scan_workspace_bytes(n2);
+    char *w = (char *)d_work;
+    int64_t o = 0;
+    auto take = [&](int64_t bytes) { char *p = w ? w + o : nullptr; o += d32_align(bytes); return p; };
+    L.hist1 = (uint32_t *)take(4 * n1);
+    L.offs1 = (uint64_t *)take(8 * (n1 + 1));
+    L.scan1 = take(L.scan1_bytes);
+    L.h2 = (uint32_t *)take(4 * n2);
+    L.offs2 = (uint64_t *)take(8 * (n2 + 1));
+    L.scan2 = take(L.scan2_bytes);
+    L.recs1 = (uint32_t *)take(4 * std::max<int64_t>(length, 1));
+    L.recs2 = (uint32_t *)take(4 * std::max<int64_t>(length, 1));
+    L.total = o;
+    return L;
+}
+
+int64_t sdp_distinct32_workspace_bytes(int64_t length) {
+    if (length < 0) return -1;
+    return d32_layout(nullptr, length).total;
+}
+
+int sdp_distinct32(const sdp_column *col, int64_t lo, void *d_work, int64_t work_bytes, uint64_t *d_out,
+                   void *stream) {
+    if (col == nullptr || d_out == nullptr || d_work == nullptr || col->length < 0)
+        return set_error(SDP_EINVAL, "distinct32: args");
+    if (col->length > 0 && col->d_values == nullptr) return set_error(SDP_EINVAL, "distinct32: null values");
+    if (!aligned16(col->d_values)) return set_error(SDP_EALIGN, "distinct32: values not 16-byte aligned");
+    const D32Layout L = d32_layout(d_work, col->length);
+    if (work_bytes < L.total) return set_error(SDP_ECAP, "distinct32: workspace %lld < %lld", (long long)work_bytes,
+                                               (long long)L.total);
+    if (col->length == 0) return 0;
+    hipStream_t s = (hipStream_t)stream;
+    const int G = L.G;
+    int rc;
+#define D32_LAUNCH_ROWS(T)                                                                                   \
+    hipLaunchKernelGGL(d32_count_kernel<T>, dim3(G), dim3(D32_CT), 0, s, *col, lo, L.rpb, L.hist1, d_out);  \
+    if ((rc = check_launch("d32_count_kernel"))) return rc;                                                  \
+    if ((rc = sdp_scan_u32(L.hist1, (int64_t)D32_NB1 * G, L.offs1, L.scan1, L.scan1_bytes, stream))) return rc; \
+    hipLaunchKernelGGL(d32_scatter1_kernel<T>, dim3(G), dim3(ST), 0, s, *col, lo, L.rpb, L.offs1, L.recs1, L.h2); \
+    if ((rc = check_launch("d32_scatter1_kernel"))) return rc;
+    switch (col->dtype) {
+    case SDP_F32: { D32_LAUNCH_ROWS(float) } break;
+    case SDP_I32: { D32_LAUNCH_ROWS(int32_t) } break;
+    case SDP_U32: { D32_LAUNCH_ROWS(uint32_t) } break;
+    case SDP_I64: { D32_LAUNCH_ROWS(int64_t) } break;
+    case SDP_U64: { D32_LAUNCH_ROWS(uint64_t) } break;
+    case SDP_I16: { D32_LAUNCH_ROWS(int16_t) } break;
+    case SDP_U16: { D32_LAUNCH_ROWS(uint16_t) } break;
+    case SDP_I8: { D32_LAUNCH_ROWS(int8_t) } break;
+    case SDP_U8: { D32_LAUNCH_ROWS(uint8_t) } break;
+    default: return set_error(SDP_EINVAL, "distinct32: dtype %d", col->dtype);
+    }
+#undef D32_LAUNCH_ROWS
+    if ((rc = sdp_scan_u32(L.h2, (int64_t)D32_NF * G, L.offs2, L.scan2, L.scan2_bytes, stream))) return rc;
+    hipLaunchKernelGGL(d32_scatter2_kernel, dim3(D32_NB1 * G), dim3(ST), 0, s, L.recs1, L.offs1, L.offs2, G, L.recs2);
+    if ((rc = check_launch("d32_scatter2_kernel"))) return rc;
+    hipLaunchKernelGGL(d32_bitmap_kernel, dim3(D32_NF), dim3(1024), 0, s, L.recs2, L.offs2, G, d_out);
+    return check_launch("d32_bitmap_kernel");
+}

@@ -214,6 +214,8 @@ _SIGNATURES = {
     'sdp_part_rows_records': (ctypes.c_int, [_BCOL, _HVY, _I32, _P, _P, _REC, _P, _P, _P]),
     'sdp_part_dedup': (ctypes.c_int, [_REC, _I32, _BCOL, _P, _I64, _I32, _P, _P, _P, _P, _P]),
     'sdp_part_compact': (ctypes.c_int, [_P, _P, _P, _P, _P, _I64, _P, _P, _P]),
+    'sdp_distinct32_workspace_bytes': (_I64, [_I64]),
+    'sdp_distinct32': (ctypes.c_int, [_COL, _I64, _P, _I64, _P, _P]),
     'sdp_scan_workspace_bytes': (_I64, [_I64]),
     'sdp_bitmap_workspace_bytes': (_I64, [_I64, _I64]),
     'sdp_distinct_bitmap': (ctypes.c_int, [_COL, _I64, _I64, _P, _I64, _P, _P, _P]),
@@ -242,7 +244,7 @@ _VALUE_FUNCS = {'sdp_last_error', 'sdp_version', 'sdp_pass1_workspace_bytes', 's
                 'sdp_scan_workspace_bytes', 'sdp_bitmap_workspace_bytes', 'sdp_select_kth_workspace_bytes',
                 'sdp_select_rounds', 'sdp_pass2_count_workspace_bytes', 'sdp_minmax_workspace_bytes',
                 'sdp_quantiles_workspace_bytes', 'sdp_distinct_workspace_bytes', 'sdp_value_counts_workspace_bytes',
-                'sdp_pearson_workspace_bytes'}
+                'sdp_pearson_workspace_bytes', 'sdp_distinct32_workspace_bytes'}
 _STATUS_FUNCS = set(_SIGNATURES) - _VALUE_FUNCS
 
 _lib = None

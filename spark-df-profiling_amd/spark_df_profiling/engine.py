@@ -56,6 +56,8 @@ BYTES_ONE_READ = os.environ.get('SDP_BYTES_TWO_READS', '0') != '1'
 PASS1_INCLUSIVE = os.environ.get('SDP_PASS1_EXCL', '0') != '1'
 # SDP_PASS1_BATCH=0: one sdp_pass1 launch per column instead of one sdp_pass1_batch per dtype
 PASS1_BATCH = os.environ.get('SDP_PASS1_BATCH', '1') != '0'
+# SDP_BITS32=0: 32-bit key spaces take the 64-bit partitioning path too (A/B runs)
+BITS32 = os.environ.get('SDP_BITS32', '1') != '0'
 # SDP_PASS2_BATCH=0: one sdp_pass2_count launch per column on wide tables too
 PASS2_BATCH = os.environ.get('SDP_PASS2_BATCH', '1') != '0'
 CAND_FULL_BUDGET = 1 << 30   # bytes of room-for-every-row candidate slots per pass-1 batch
@@ -1640,18 +1642,45 @@ class Engine:
             tab.update({'slots': keys, 'counts': counts, 'capacity': max(total, 1)})
         return tab
 
+    BITS32_DTYPES = (nat.I8, nat.I16, nat.I32, nat.I64, nat.U8, nat.U16, nat.U32, nat.U64)
+
+    def _bits32_ok(self, col, bd):
+        """The 32-bit partition + LDS bitmap distinct count (sdp_distinct32)
+        applies: float32 keys, or an integral range < 2^32; and no heavy key in
+        the pass-1 sample (a key with a large share of the rows would fill one
+        final bucket)."""
+        if not BITS32 or col.kind != 'fixed':
+            return False
+        if col.dtype == nat.F32:
+            pass
+        elif col.dtype in self.BITS32_DTYPES and bd is not None and bd[1] - bd[0] < (1 << 32):
+            pass
+        else:
+            return False
+        pre = self._heavy_pre or {}
+        return pre.get(id(col)) is None
+
     def distinct_paths(self, cols, hints, bounds):
-        """'bitmap' | 'group' | 'table' per column: the path choice of
-        describe._distinct_count / distinct_fixed on a single rank."""
+        """'bitmap' | 'bits32' | 'group' | 'table' per column: the path choice
+        of describe._distinct_count / distinct_fixed on a single rank."""
         out = []
         for col, hint, bd in zip(cols, hints, bounds):
             if (bd is not None and col.kind == 'fixed' and col.dtype in self.BITMAP_DTYPES
                     and bd[1] - bd[0] + 1 <= nat.BITMAP_MAX_BITS):
                 out.append('bitmap')
             elif hint * 4 > max(col.length, 1) and col.length >= (1 << 16):
-                out.append('group')
+                out.append('bits32' if self._bits32_ok(col, bd) else 'group')
             else:
                 out.append('table')
+        return out
+
+    def _distinct32_launch(self, col, lo):
+        """sdp_distinct32 of `col` queued; returns the [distinct, rows] device pair."""
+        out = self._u64(2, zero=True)
+        work = self._bytes(sdp.sdp_distinct32_workspace_bytes(col.length))
+        cs = col.sdp()
+        nat.annotate(_label(col, 'distinct32'), col_read_bytes(col) * 2 + 4 * 5 * col.length)
+        sdp.sdp_distinct32(ctypes.byref(cs), int(lo), ptr(work), work.numel(), ptr(out), self._s())
         return out
 
     def distinct_batch(self, cols, hints, bounds, known=None):
@@ -1664,10 +1693,16 @@ class Engine:
         out = list(known) if known is not None else [None] * len(cols)     # sorted columns: counted
         paths = self.distinct_paths(cols, hints, bounds)
         bm = [i for i, pth in enumerate(paths) if pth == 'bitmap' and out[i] is None]
+        b32 = [i for i, pth in enumerate(paths) if pth == 'bits32' and out[i] is None]
         grp = [i for i, pth in enumerate(paths) if pth == 'group' and out[i] is None]
-        if bm:
+        if bm or b32:
+            # bitmaps and 32-bit partitions queue without a host round trip: one
+            # readback of every such column's count
             outs = [self._distinct_bitmap_launch(cols[i], bounds[i][0], bounds[i][1] - bounds[i][0] + 1) for i in bm]
-            for i, v in zip(bm, self._host_u64(torch.cat(outs))):
+            outs += [self._distinct32_launch(cols[i], bounds[i][0] if bounds[i] is not None else 0)[:1] for i in b32]
+            for i in b32:                             # (their heavy-key samples go unused)
+                (self._heavy_pre or {}).pop(id(cols[i]), None)
+            for i, v in zip(bm + b32, self._host_u64(torch.cat(outs))):
                 out[i] = int(v)
         if grp:
             for i, tab in zip(grp, self.group_batch([cols[i] for i in grp])):

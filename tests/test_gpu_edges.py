@@ -150,7 +150,9 @@ def test_uint32_wide_fused_group(monkeypatch):
         v[:n // 40] = v[n // 2:n // 2 + n // 40]          # repeats: distinct < rows, still near-unique
         cols['u%d' % j] = pa.array(v, mask=rng.random(n) < 0.05)
     t = pa.table(cols)
+    from spark_df_profiling import engine as engmod
     from spark_df_profiling.engine import Engine
+    monkeypatch.setattr(engmod, 'BITS32', False)        # (uint32 keys would take sdp_distinct32)
     fused = []
     orig = Engine._group_middle_fused
 

@@ -188,3 +188,86 @@ def test_wave_dedup_kernels(v2, direct, monkeypatch):
     want = sum(len(np.unique(x)) for x in b)
     assert full == 0
     assert groups == want
+
+
+def _distinct32(arr, lo=0):
+    import torch
+    from spark_df_profiling import _native as nat
+    from spark_df_profiling._native import sdp, ptr
+    e, col = _engine_groups(arr)
+    out = torch.zeros(2, dtype=torch.int64, device='cuda')
+    work = torch.empty(sdp.sdp_distinct32_workspace_bytes(col.length), dtype=torch.uint8, device='cuda')
+    cs = col.sdp()
+    import ctypes
+    sdp.sdp_distinct32(ctypes.byref(cs), int(lo), ptr(work), work.numel(), ptr(out), nat.stream_handle(None))
+    torch.cuda.synchronize()
+    d, rows = [int(x) for x in out.cpu()]
+    return d, rows
+
+
+@pytest.mark.parametrize('case', ['f32_norm', 'f32_special', 'i32_full', 'u32_full', 'i64_window', 'tiny'])
+def test_distinct32_exact(case):
+    """sdp_distinct32 (4-byte records in 64 x 64 buckets + LDS bitmaps) vs
+    numpy, nulls skipped, NaN one value, -0.0 == 0.0, the ends of the 32-bit
+    key space (describe.py:143)."""
+    g = datagen.rng(17)
+    n = N if case != 'tiny' else 1000
+    lo = 0
+    mask = g.random(n) < 0.07
+    if case == 'f32_norm':
+        v = g.standard_normal(n).astype(np.float32)
+    elif case == 'f32_special':
+        v = g.standard_normal(n).astype(np.float32)
+        v[g.random(n) < 0.05] = np.nan
+        v[g.random(n) < 0.02] = np.float32(np.nan) * -1
+        v[g.random(n) < 0.03] = 0.0
+        v[g.random(n) < 0.03] = -0.0
+        v[:4] = [np.inf, -np.inf, np.finfo(np.float32).max, np.finfo(np.float32).tiny]
+    elif case == 'i32_full':
+        v = g.integers(-2 ** 31, 2 ** 31, n).astype(np.int32)
+        v[:2] = [np.iinfo(np.int32).min, np.iinfo(np.int32).max]
+        lo = int(v.min())
+    elif case == 'u32_full':
+        v = g.integers(0, 2 ** 32, n, dtype=np.uint64).astype(np.uint32)
+        v[:2] = [0, np.iinfo(np.uint32).max]
+        lo = int(v.min())
+    elif case == 'i64_window':
+        v = (10 ** 12 + g.integers(0, 2 ** 32, n, dtype=np.int64)).astype(np.int64)
+        v[:2] = [10 ** 12, 10 ** 12 + 2 ** 32 - 1]
+        lo = int(v.min())
+    else:
+        v = g.integers(0, 300, n).astype(np.int32)
+    mask[:2] = False
+    d, rows = _distinct32(pa.array(v, mask=mask), lo)
+    x = v[~mask]
+    if x.dtype.kind == 'f':
+        x = np.where(x == 0, np.float32(0), x)                     # -0.0 groups with 0.0
+        want = len(np.unique(x[~np.isnan(x)])) + int(np.isnan(x).any())
+    else:
+        want = len(np.unique(x))
+    assert (d, rows) == (want, int((~mask).sum()))
+
+
+def test_distinct32_describe_path():
+    """describe() routes float32 and < 2^32-range integral columns without
+    heavy keys to sdp_distinct32 and matches the oracle."""
+    import oracle
+    from spark_df_profiling import describe
+    from spark_df_profiling.engine import Engine
+    g = datagen.rng(23)
+    n = 200_003
+    t = pa.table({'f32': pa.array(g.standard_normal(n).astype(np.float32), mask=g.random(n) < 0.05),
+                  'i64_2p31': pa.array(g.integers(-2 ** 31, 2 ** 31, n)),
+                  'u32': pa.array(g.integers(0, 2 ** 32, n, dtype=np.uint64).astype(np.uint32))})
+    seen = []
+    orig = Engine._distinct32_launch
+
+    def spy(self, col, lo):
+        seen.append(col.name)
+        return orig(self, col, lo)
+    Engine._distinct32_launch = spy
+    try:
+        assert_describe_equal(describe(t, plots=False), oracle.describe(t))
+    finally:
+        Engine._distinct32_launch = orig
+    assert sorted(seen) == ['f32', 'i64_2p31', 'u32']

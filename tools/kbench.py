@@ -30,6 +30,9 @@ for r in range(reps):
         e.numeric_pass1_batch([col])
     elif what == 'pass2':
         e.numeric_stats(col)
+    elif what == 'd32':                      # sdp_distinct32 (32-bit key spaces)
+        lo = 0 if col.is_float else int(col.values[:rows].min().item())
+        out = e._distinct32_launch(col, lo)
     elif what == 'gram':
         num = [c for c in t.columns if c.kind == 'fixed' and c.spark_type != 'date']
         e.gram(num, [0.0] * len(num), [False] * len(num))
