@@ -8,7 +8,7 @@ C=$ROOT/spark-df-profiling_amd/csrc
 T0=$(mktemp -d); T=$T0/a/b
 mkdir -p $T && cp $C/*.hip $C/*.h $C/*.cpp $T/ && mkdir -p $T0/include && cp $ROOT/include/sdp.h $T0/include/
 if [ -n "$FILE" ]; then sed -i "$EXPR" $T/$FILE; fi
-for f in sdp_abi.cpp sdp_numeric.hip sdp_hash.hip sdp_part.hip sdp_gram.hip sdp_bitmap.hip; do
+for f in $(cd $T && ls *.hip *.cpp); do
   /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -Wall -Wno-unused-function -mcode-object-version=5 \
      $FLAGS -x hip -c $T/$f -o $T/$f.o &
 done

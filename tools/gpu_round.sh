@@ -1,20 +1,17 @@
 #!/bin/bash
-# One GPU call: gpu tests, smoke, default bench, rocprof kernel stats of the bench.
-# Usage (via gpurun): bash tools/gpu_round.sh TAG
+# Round validation on the box: the GPU suite, smoke(), the default bench with a
+# rocprofv3 kernel-stats pass, and the 8-GPU rank share (1.25e8 rows) single vs
+# forced-sharded.  -> gpurun_out/TAG_*
+# usage: tools/gpu_round.sh TAG
 set -o pipefail
-TAG=${1:-run}
-cd "$GRAFT_REPO_ROOT"
-mkdir -p gpurun_out
-export TMPDIR=/tmp
-timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > gpurun_out/${TAG}_tests.log 2>&1
-rc=$?; tail -3 gpurun_out/${TAG}_tests.log; [ $rc -eq 0 ] || exit $rc
-timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/${TAG}_smoke.log 2>&1 || { tail -20 gpurun_out/${TAG}_smoke.log; exit 1; }
+cd "$(dirname "$0")/.."; mkdir -p gpurun_out; export TMPDIR=/tmp
+TAG=${1:-rnd}
+timeout -k 10 900 python -u -m pytest tests -m gpu -v --timeout 600 --timeout-method thread --durations=12 \
+    > gpurun_out/${TAG}_tests.log 2>&1
+rc=$?; tail -20 gpurun_out/${TAG}_tests.log; cp gpurun_out/pytest_multirank.log gpurun_out/${TAG}_multirank.log 2>/dev/null
+[ $rc -eq 0 ] || exit $rc
+timeout -k 10 200 python -u -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/${TAG}_smoke.log 2>&1 \
+    || { tail -20 gpurun_out/${TAG}_smoke.log; exit 1; }
 tail -1 gpurun_out/${TAG}_smoke.log
-[ "${SKIP_BENCH:-0}" = 1 ] && exit 0
-timeout -k 10 600 python -u bench.py > gpurun_out/${TAG}_bench.json 2> gpurun_out/${TAG}_bench.err || { tail -20 gpurun_out/${TAG}_bench.err; exit 1; }
-cat gpurun_out/${TAG}_bench.json
-timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/${TAG}_prof -o run -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline > gpurun_out/${TAG}_prof_bench.json 2> gpurun_out/${TAG}_prof.err || { tail -20 gpurun_out/${TAG}_prof.err; exit 1; }
-f=$(find gpurun_out/${TAG}_prof -name '*kernel_stats.csv' | head -1)
-cp "$f" gpurun_out/${TAG}_kernel_stats.csv
-rm -rf gpurun_out/${TAG}_prof
-echo done
+bash tools/gpu_bench.sh $TAG || exit 1
+NOPROF=1 bash tools/gpu_rank_share.sh $TAG || exit 1
