@@ -420,43 +420,20 @@ def shard_to_arrow(shard):
     return pa.table(arrays)
 
 
-def _cgroup_cpus():
-    """CPUs of this job's cgroup quota (cgroup v2 cpu.max, else v1 cfs), or None."""
-    try:
-        with open('/sys/fs/cgroup/cpu.max') as fh:
-            q, per = fh.read().split()[:2]
-        if q != 'max':
-            return max(1, math.ceil(int(q) / int(per)))
-    except (OSError, ValueError):
-        pass
-    try:
-        with open('/sys/fs/cgroup/cpu/cpu.cfs_quota_us') as fh:
-            q = int(fh.read())
-        with open('/sys/fs/cgroup/cpu/cpu.cfs_period_us') as fh:
-            per = int(fh.read())
-        if q > 0:
-            return max(1, math.ceil(q / per))
-    except (OSError, ValueError):
-        pass
-    return None
-
-
 def cpu_share(columns=16):
     """(processes the baseline uses, how that was decided).  The CPUs this job
     may run on are the affinity mask, bounded by the cgroup CPU quota when one
     is set (os.cpu_count() reports the whole machine); the restatement runs one
     column per process, so at most `columns` processes do work."""
+    from spark_df_profiling.utils import available_cpus
     visible = os.cpu_count() or 1
     try:
         allowed = len(os.sched_getaffinity(0))
     except (AttributeError, OSError):
         allowed = visible
-    quota = _cgroup_cpus()
-    avail = min(allowed, quota) if quota else allowed
-    src = 'cgroup cpu quota' if quota and quota < allowed else 'affinity mask'
+    avail, src = available_cpus()
     return max(1, min(avail, columns)), {'os_cpu_count': visible, 'affinity_cpus': allowed,
-                                         'cgroup_quota_cpus': quota, 'available_cpus': avail,
-                                         'source': src, 'columns': columns}
+                                         'available_cpus': avail, 'source': src, 'columns': columns}
 
 
 def cpu_baseline(sample_rows, device):

@@ -160,7 +160,10 @@ def _start_pool_locked(workers):
     import multiprocessing as mp
     import os
     from concurrent.futures import ProcessPoolExecutor
-    n = workers or int(os.environ.get('SDP_PLOT_WORKERS', '0')) or min(16, os.cpu_count() or 1)
+    # one render process per CPU this job may use (affinity mask bounded by the
+    # cgroup quota; os.cpu_count() would count the whole machine)
+    from .utils import available_cpus
+    n = workers or int(os.environ.get('SDP_PLOT_WORKERS', '0')) or available_cpus()[0]
     _POOL = ProcessPoolExecutor(max_workers=n, mp_context=mp.get_context('spawn'))
     # spawn re-runs the parent's __main__ in every child unless it cannot find
     # it; hide it while the workers start (they need only this module)

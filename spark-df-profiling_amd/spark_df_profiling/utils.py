@@ -31,3 +31,36 @@ def corr_from_gram(G, s, n):
     with np.errstate(all='ignore'):
         rho = C / np.sqrt(np.outer(d, d))
     return rho
+
+
+def available_cpus():
+    """(CPUs this process may run on, how that was decided): the affinity mask,
+    bounded by the cgroup CPU quota when one is set -- os.cpu_count() reports
+    the whole machine (256 on the GPU box, whose job quota is 16)."""
+    import math
+    import os
+    try:
+        allowed = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        allowed = os.cpu_count() or 1
+    quota = None
+    try:                                            # cgroup v2
+        with open('/sys/fs/cgroup/cpu.max') as fh:
+            q, per = fh.read().split()[:2]
+        if q != 'max':
+            quota = max(1, math.ceil(int(q) / int(per)))
+    except (OSError, ValueError):
+        pass
+    if quota is None:                               # cgroup v1
+        try:
+            with open('/sys/fs/cgroup/cpu/cpu.cfs_quota_us') as fh:
+                q = int(fh.read())
+            with open('/sys/fs/cgroup/cpu/cpu.cfs_period_us') as fh:
+                per = int(fh.read())
+            if q > 0:
+                quota = max(1, math.ceil(q / per))
+        except (OSError, ValueError):
+            pass
+    if quota is not None and quota < allowed:
+        return quota, 'cgroup cpu quota'
+    return allowed, 'affinity mask'
