@@ -465,6 +465,10 @@ typedef struct sdp_pass2_task {
     uint64_t          *d_stats;
     int64_t            rows_per_block;
     int32_t            bins, edges_monotone, b1, grid;
+    /* b1 = -1: the count is sdp_distinct32's level-1 count instead (64
+     * buckets of mix32(key - key32_lo) into d_part_hist [64][grid], non-null
+     * rows added to d_stats[1]; heavy keys unused) -- its pre-count argument */
+    int64_t            key32_lo;
 } sdp_pass2_task;
 
 /* sdp_pass2_count of `ntasks` columns of one dtype, bin count and edge kind
@@ -552,8 +556,11 @@ int sdp_part_dedup(const sdp_records *in, int32_t is_bytes, const sdp_bytes_colu
  * += non-null rows (d_out zeroed by the caller).  Workspace:
  * sdp_distinct32_workspace_bytes(length) (two 4-byte record buffers + scans). */
 int64_t sdp_distinct32_workspace_bytes(int64_t length);
-int sdp_distinct32(const sdp_column *col, int64_t lo, void *d_work, int64_t work_bytes, uint64_t *d_out,
-                   void *stream);
+/* d_hist1 (nullable): the level-1 counts [64][grid] already taken (by
+ * sdp_pass2_count_batch with b1 = -1, which also added the rows to d_out[1]):
+ * the column is then read once here instead of twice. */
+int sdp_distinct32(const sdp_column *col, int64_t lo, const uint32_t *d_hist1, void *d_work, int64_t work_bytes,
+                   uint64_t *d_out, void *stream);
 /* Pack the per-bucket groups: src[d_starts[f] ..+ngroups[f]) -> dst[d_out_offsets[f] ..). */
 int sdp_part_compact(const uint64_t *d_src_a, const uint64_t *d_src_b, const uint64_t *d_starts,
                      const uint32_t *d_ngroups, const uint64_t *d_out_offsets, int64_t nbuckets,

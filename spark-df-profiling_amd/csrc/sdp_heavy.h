@@ -4,6 +4,7 @@
 // sample are counted in an LDS table and never become partition records, so
 // skewed columns (describe.py:251's hot groups) cannot pile into one bucket.
 #pragma once
+#include <type_traits>
 #include "sdp_common.h"
 
 namespace sdp {
@@ -108,6 +109,27 @@ __device__ void heavy_flush(HeavyLdsT<BYTES> &s, int n, uint64_t *counts) {
     lds_barrier();
     for (int i = threadIdx.x; i < n; i += blockDim.x)
         if (s.cnt[i]) atomicAdd((unsigned long long *)&counts[i], (unsigned long long)s.cnt[i]);
+}
+
+// ---- 32-bit key spaces (sdp_distinct32; its level-1 count rides pass 2) -------
+// float32: the order-preserving 32-bit key (NaN one value, -0.0 == 0.0);
+// integral columns with imax - imin < 2^32: v - lo.  h = mix32(key) is a
+// bijection of [0, 2^32); its top D32_B1 bits pick the level-1 bucket.
+constexpr int D32_B1 = 6;
+constexpr int D32_NB1 = 1 << D32_B1;
+__device__ __forceinline__ uint32_t mix32(uint32_t x) {
+    x ^= x >> 16;
+    x *= 0x85EBCA6Bu;
+    x ^= x >> 13;
+    x *= 0xC2B2AE35u;
+    x ^= x >> 16;
+    return x;
+}
+template <typename T>
+__device__ __forceinline__ uint32_t key32_rel(T v, int64_t lo) {
+    if constexpr (std::is_same<T, float>::value) return v != v ? 0xFFC00000u : Key32<float>::key(v);
+    else if constexpr (std::is_same<T, double>::value) return 0u;             // (never a 32-bit key space)
+    else return (uint32_t)(uint64_t)((int64_t)v - lo);
 }
 
 // ---- grouping key of a fixed-width element (order-preserving u64) ----------

@@ -1446,15 +1446,17 @@ __device__ __forceinline__ void pass2_count_body(const sdp_column &col, double m
                                                  int monotone, double hi_t, double lo_t, double *part_mad,
                                                  uint64_t *part_cnt, const HeavyArg &heavy, int b1,
                                                  int64_t rows_per_block, uint32_t *hist, uint64_t *heavy_counts,
-                                                 uint64_t *stats, const int G, const int g) {
+                                                 uint64_t *stats, const int G, const int g, int64_t lo32 = 0) {
     constexpr int VPT = Vec16<T>::N;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     __shared__ P2CountLds cl;
     double *s_edges = (double *)smem;
     uint32_t *s_hist = (uint32_t *)(smem + sizeof(double) * bins);
     const int t = threadIdx.x;
-    const int nb = 1 << b1;
-    const int shift = 64 - b1;
+    // b1 < 0: the level-1 count of sdp_distinct32 (32-bit key spaces) instead
+    const bool d32 = b1 < 0;
+    const int nb = d32 ? D32_NB1 : 1 << b1;
+    const int shift = d32 ? 0 : 64 - b1;
     for (int i = t; i < bins; i += blockDim.x) { s_edges[i] = edges[i]; s_hist[i] = 0; }
     for (int b = t; b < nb; b += P2_BLOCK) cl.hist[b] = 0;
     heavy_build<false>(cl.heavy, heavy);               // (ends with a barrier)
@@ -1477,6 +1479,12 @@ __device__ __forceinline__ void pass2_count_body(const sdp_column &col, double m
     auto count = [&](T x, bool valid) {
         if (!valid) return;
         ++rows;
+        if constexpr (!std::is_same<T, double>::value) {
+            if (d32) {
+                atomicAdd(&cl.hist[mix32(key32_rel<T>(x, lo32)) >> (32 - D32_B1)], 1u);
+                return;
+            }
+        }
         const uint64_t h = mix64(key_of<T>(x));
         const int hv = any_heavy ? heavy_find_u64(cl.heavy, heavy.n, h) : -1;
         if (hv >= 0) atomicAdd(&cl.heavy.cnt[hv], 1u);
@@ -1567,6 +1575,10 @@ __device__ __forceinline__ void pass2_count_body(const sdp_column &col, double m
     for (int i = t; i < bins; i += blockDim.x) part_cnt[(int64_t)g * stride + 3 + i] = s_hist[i];
     // ---- level-1 count outputs (as part_count_rows_u64_kernel) ----
     for (int b = t; b < nb; b += P2_BLOCK) hist[(int64_t)b * G + g] = cl.hist[b];
+    if (d32) {                                         // sdp_distinct32's out[1]: non-null rows
+        block_add_u64(rows, &stats[1]);
+        return;
+    }
     heavy_flush(cl.heavy, heavy.n, heavy_counts);
     block_add_u64(rows, &stats[0]);
     block_add_u64(special, &stats[1]);
@@ -1589,7 +1601,7 @@ __global__ void __launch_bounds__(P2_BLOCK, 4) pass2_count_batch_kernel(const sd
     uint64_t *pc = (uint64_t *)((char *)tk.d_work + (int64_t)tk.grid * sizeof(double));
     pass2_count_body<T, SMALL, MONO, NB>(tk.col, tk.mean, tk.d_edges, tk.bins, tk.edges_monotone, tk.hi_t, tk.lo_t,
                                          pm, pc, hv, tk.b1, tk.rows_per_block, tk.d_part_hist, tk.d_heavy_counts,
-                                         tk.d_stats, tk.grid, (int)blockIdx.x);
+                                         tk.d_stats, tk.grid, (int)blockIdx.x, tk.key32_lo);
 }
 
 __device__ __forceinline__ void pass2_merge_body(const double *part_mad, const uint64_t *part_cnt, int grid,

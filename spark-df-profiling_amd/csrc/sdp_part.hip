@@ -1665,23 +1665,10 @@ static void launch_rows_u64(int phase, int grid, hipStream_t s, const sdp_column
 // scatter also counts every (level-1 bucket, level-2 bucket) pair of its block
 // (64 x 64 LDS counters), so the level-2 offsets need no count pass of their
 // own; both scatters write runs of ~256 records per bucket per tile.
-constexpr int D32_B1 = 6, D32_B2 = 6;
-constexpr int D32_NB1 = 1 << D32_B1, D32_NB2 = 1 << D32_B2, D32_NF = D32_NB1 * D32_NB2;
+constexpr int D32_B2 = 6;
+constexpr int D32_NB2 = 1 << D32_B2, D32_NF = D32_NB1 * D32_NB2;
 constexpr int D32_BM_WORDS = 1 << (32 - D32_B1 - D32_B2 - 5);   // 2^20 bits -> 32 K words (128 KB)
 
-__device__ __forceinline__ uint32_t mix32(uint32_t x) {
-    x ^= x >> 16;
-    x *= 0x85EBCA6Bu;
-    x ^= x >> 13;
-    x *= 0xC2B2AE35u;
-    x ^= x >> 16;
-    return x;
-}
-template <typename T>
-__device__ __forceinline__ uint32_t key32_rel(T v, int64_t lo) {
-    if constexpr (std::is_same<T, float>::value) return v != v ? 0xFFC00000u : Key32<float>::key(v);
-    else return (uint32_t)(uint64_t)((int64_t)v - lo);
-}
 
 // One tile of NT * RPT rows as 32-bit hashes (16-byte loads of full tiles)
 template <typename T, int NT, int RPT>
@@ -2185,8 +2172,8 @@ int64_t sdp_distinct32_workspace_bytes(int64_t length) {
     return d32_layout(nullptr, length).total;
 }
 
-int sdp_distinct32(const sdp_column *col, int64_t lo, void *d_work, int64_t work_bytes, uint64_t *d_out,
-                   void *stream) {
+int sdp_distinct32(const sdp_column *col, int64_t lo, const uint32_t *d_hist1, void *d_work, int64_t work_bytes,
+                   uint64_t *d_out, void *stream) {
     if (col == nullptr || d_out == nullptr || d_work == nullptr || col->length < 0)
         return set_error(SDP_EINVAL, "distinct32: args");
     if (col->length > 0 && col->d_values == nullptr) return set_error(SDP_EINVAL, "distinct32: null values");
@@ -2198,10 +2185,13 @@ int sdp_distinct32(const sdp_column *col, int64_t lo, void *d_work, int64_t work
     hipStream_t s = (hipStream_t)stream;
     const int G = L.G;
     int rc;
+    const uint32_t *h1 = d_hist1 ? d_hist1 : L.hist1;
 #define D32_LAUNCH_ROWS(T)                                                                                   \
-    hipLaunchKernelGGL(d32_count_kernel<T>, dim3(G), dim3(D32_CT), 0, s, *col, lo, L.rpb, L.hist1, d_out);  \
-    if ((rc = check_launch("d32_count_kernel"))) return rc;                                                  \
-    if ((rc = sdp_scan_u32(L.hist1, (int64_t)D32_NB1 * G, L.offs1, L.scan1, L.scan1_bytes, stream))) return rc; \
+    if (!d_hist1) {                                                                                          \
+        hipLaunchKernelGGL(d32_count_kernel<T>, dim3(G), dim3(D32_CT), 0, s, *col, lo, L.rpb, L.hist1, d_out); \
+        if ((rc = check_launch("d32_count_kernel"))) return rc;                                              \
+    }                                                                                                        \
+    if ((rc = sdp_scan_u32(h1, (int64_t)D32_NB1 * G, L.offs1, L.scan1, L.scan1_bytes, stream))) return rc;  \
     hipLaunchKernelGGL(d32_scatter1_kernel<T>, dim3(G), dim3(ST), 0, s, *col, lo, L.rpb, L.offs1, L.recs1, L.h2); \
     if ((rc = check_launch("d32_scatter1_kernel"))) return rc;
     switch (col->dtype) {

@@ -105,7 +105,7 @@ class SdpPass2Task(ctypes.Structure):
                 ('d_hist', ctypes.c_void_p), ('heavy', SdpHeavy), ('d_part_hist', ctypes.c_void_p),
                 ('d_heavy_counts', ctypes.c_void_p), ('d_stats', ctypes.c_void_p), ('rows_per_block', ctypes.c_int64),
                 ('bins', ctypes.c_int32), ('edges_monotone', ctypes.c_int32), ('b1', ctypes.c_int32),
-                ('grid', ctypes.c_int32)]
+                ('grid', ctypes.c_int32), ('key32_lo', ctypes.c_int64)]
 
 
 class SdpRowsTask(ctypes.Structure):
@@ -215,7 +215,7 @@ _SIGNATURES = {
     'sdp_part_dedup': (ctypes.c_int, [_REC, _I32, _BCOL, _P, _I64, _I32, _P, _P, _P, _P, _P]),
     'sdp_part_compact': (ctypes.c_int, [_P, _P, _P, _P, _P, _I64, _P, _P, _P]),
     'sdp_distinct32_workspace_bytes': (_I64, [_I64]),
-    'sdp_distinct32': (ctypes.c_int, [_COL, _I64, _P, _I64, _P, _P]),
+    'sdp_distinct32': (ctypes.c_int, [_COL, _I64, _P, _P, _I64, _P, _P]),
     'sdp_scan_workspace_bytes': (_I64, [_I64]),
     'sdp_bitmap_workspace_bytes': (_I64, [_I64, _I64]),
     'sdp_distinct_bitmap': (ctypes.c_int, [_COL, _I64, _I64, _P, _I64, _P, _P, _P]),

@@ -457,8 +457,11 @@ def describe(df, bins=10, corr_reject=0.9, **kwargs):
         paths = engine.distinct_paths_sharded(num_cols, hints, bounds, n) if sharded else \
             engine.distinct_paths(num_cols, hints, bounds)
         group_cols = {i for i, pth in enumerate(paths) if pth == 'group' and known[i] is None}
+        # 32-bit key spaces (sdp_distinct32): pass 2 takes their level-1 count too
+        count32_cols = {i: (bounds[i][0] if bounds[i] is not None else 0)
+                        for i, pth in enumerate(paths) if pth == 'bits32' and known[i] is None}
         stats = engine.numeric_stats_batch(num_cols, packs, bins, [k_vals.get(c.name, 2) for c in num_cols],
-                                           group_cols=group_cols, gk=gk)
+                                           group_cols=group_cols, gk=gk, count32_cols=count32_cols)
         for col, pack, st in zip(num_cols, packs, stats):
             bundles[col.name]['p1_pack'] = pack
             if st is not None:

@@ -708,18 +708,21 @@ class Engine:
             hist = self._u64(bins)
             cs = col.sdp()
             ctx = count_ctx.get(i)
+            batch = PASS2_BATCH and len(items) >= 8
+            if ctx is not None and ctx.get('d32') and not batch:
+                ctx = None                  # (the d32 pre-count rides the batched launch only)
             if ctx is not None:
                 work = self._bytes(max(sdp.sdp_pass2_count_workspace_bytes(col.length, bins),
                                        sdp.sdp_pass2_workspace_bytes(col.length, col.dtype, bins)))
                 hv = ctx['hv']
-                if PASS2_BATCH and len(items) >= 8:
+                if batch:
                     rpb = sdp.sdp_part_rows_per_block(col.length, 0)
                     grid = max(1, -(-col.length // rpb))
                     task = nat.SdpPass2Task(cs, e.data_ptr(), float(mean), float(hi_t), float(lo_t), work.data_ptr(),
                                             res.data_ptr(), hist.data_ptr(),
                                             hv['struct'] if hv else nat.SdpHeavy(None, None, None, None, 0, 0),
                                             ctx['h1'].data_ptr(), ctx['hcnt'].data_ptr(), ctx['stats'].data_ptr(),
-                                            rpb, bins, int(mono), ctx['b1'], grid)
+                                            rpb, bins, int(mono), ctx['b1'], grid, int(ctx.get('lo', 0)))
                     batched.append(((col.dtype, bins, int(mono)), task, col))
                 else:
                     nat.annotate(_label(col), col_read_bytes(col))
@@ -743,7 +746,7 @@ class Engine:
             for (dtype, bins, mono), grp in kinds.items():
                 mg = max(t.grid for t, _ in grp)
                 for t, c in grp:      # sdp_pass2_count's own argument checks (the table is device memory)
-                    if (c.values.data_ptr() % 16 or not 0 <= t.b1 <= 10 or t.heavy.n > nat.HEAVY_MAX
+                    if (c.values.data_ptr() % 16 or not -1 <= t.b1 <= 10 or t.heavy.n > nat.HEAVY_MAX
                             or t.grid > mg or mg > nat.PART_MAX_GRID):
                         raise nat.NativeError('pass2_count_batch: a task fails the sdp_pass2_count checks')
                 arr = (nat.SdpPass2Task * len(grp))(*[t for t, _ in grp])
@@ -876,7 +879,8 @@ class Engine:
             raise RuntimeError('sdp_gk_merge: summary capacity exceeded (status %d)' % int(stv[0]))
         return {p: float(v) for p, v in zip(probs, out.cpu().numpy())}
 
-    def numeric_stats_batch(self, cols, packs, bins=10, ks=None, probs=PROBS, group_cols=(), gk=None):
+    def numeric_stats_batch(self, cols, packs, bins=10, ks=None, probs=PROBS, group_cols=(), gk=None,
+                            count32_cols=None):
         """numeric_stats of every column (None for a column with no non-null
         value) with two host readbacks in all.  A bins value the reference
         rejects (describe.py:46 with bins=1) is recorded per column and raised
@@ -924,7 +928,17 @@ class Engine:
         # columns whose countDistinct takes the partitioning path: pass 2 also
         # does their level-1 count (one column read fewer, single rank or sharded)
         count_ctx = {}
+        count32_cols = count32_cols or {}
         for j, i in enumerate(p2_idx):
+            if i in count32_cols and not self.comm.sharded:
+                # sdp_distinct32's level-1 count on pass 2's read (b1 = -1)
+                col = cols[i]
+                rpb = sdp.sdp_part_rows_per_block(col.length, 0)
+                grid = max(1, -(-col.length // rpb))
+                count_ctx[j] = {'d32': True, 'b1': -1, 'hv': None, 'lo': int(count32_cols[i]),
+                                'h1': torch.empty(64 * grid, dtype=torch.int32, device=self.device),
+                                'hcnt': self._u64(1), 'stats': self._u64(2, zero=True)}
+                continue
             if i in group_cols:
                 # sharded: group_sharded_batch's level-1 geometry (heavy keys
                 # pooled over the ranks, the same on every rank)
@@ -1672,15 +1686,30 @@ class Engine:
                 out.append('bits32' if self._bits32_ok(col, bd) else 'group')
             else:
                 out.append('table')
+        # wide tables of short columns (512 x 1e7): the
+        # partitioning path fuses same-geometry columns into a few launches
+        # (_group_middle_fused), where one sdp_distinct32 per column would pay
+        # five launches and a host call each
+        short32 = [i for i, p in enumerate(out) if p == 'bits32' and cols[i].length <= self.FUSE_MAX_RECS]
+        if len(short32) >= self.FUSE_MIN_COLS:
+            for i in short32:
+                out[i] = 'group'
         return out
 
     def _distinct32_launch(self, col, lo):
-        """sdp_distinct32 of `col` queued; returns the [distinct, rows] device pair."""
-        out = self._u64(2, zero=True)
+        """sdp_distinct32 of `col` queued; returns the [distinct, rows] device
+        pair.  When pass 2 took the level-1 count (numeric_stats_batch's
+        count32_cols), the column is read once here instead of twice."""
+        pre = self._counted.pop(id(col), None)
+        h1 = None
+        if pre is not None and pre.get('d32'):
+            h1, out = pre['h1'], pre['stats']
+        else:
+            out = self._u64(2, zero=True)
         work = self._bytes(sdp.sdp_distinct32_workspace_bytes(col.length))
         cs = col.sdp()
-        nat.annotate(_label(col, 'distinct32'), col_read_bytes(col) * 2 + 4 * 5 * col.length)
-        sdp.sdp_distinct32(ctypes.byref(cs), int(lo), ptr(work), work.numel(), ptr(out), self._s())
+        nat.annotate(_label(col, 'distinct32'), col_read_bytes(col) * (1 if h1 is not None else 2) + 4 * 5 * col.length)
+        sdp.sdp_distinct32(ctypes.byref(cs), int(lo), ptr(h1), ptr(work), work.numel(), ptr(out), self._s())
         return out
 
     def distinct_batch(self, cols, hints, bounds, known=None):

@@ -199,7 +199,7 @@ def _distinct32(arr, lo=0):
     work = torch.empty(sdp.sdp_distinct32_workspace_bytes(col.length), dtype=torch.uint8, device='cuda')
     cs = col.sdp()
     import ctypes
-    sdp.sdp_distinct32(ctypes.byref(cs), int(lo), ptr(work), work.numel(), ptr(out), nat.stream_handle(None))
+    sdp.sdp_distinct32(ctypes.byref(cs), int(lo), None, ptr(work), work.numel(), ptr(out), nat.stream_handle(None))
     torch.cuda.synchronize()
     d, rows = [int(x) for x in out.cpu()]
     return d, rows
@@ -248,26 +248,34 @@ def test_distinct32_exact(case):
     assert (d, rows) == (want, int((~mask).sum()))
 
 
-def test_distinct32_describe_path():
+@pytest.mark.parametrize('copies', [1, 3])
+def test_distinct32_describe_path(copies):
     """describe() routes float32 and < 2^32-range integral columns without
-    heavy keys to sdp_distinct32 and matches the oracle."""
+    heavy keys to sdp_distinct32 and matches the oracle; with >= 8 numeric
+    columns (the batched pass 2) their level-1 count rides pass 2's read."""
     import oracle
     from spark_df_profiling import describe
     from spark_df_profiling.engine import Engine
     g = datagen.rng(23)
     n = 200_003
-    t = pa.table({'f32': pa.array(g.standard_normal(n).astype(np.float32), mask=g.random(n) < 0.05),
-                  'i64_2p31': pa.array(g.integers(-2 ** 31, 2 ** 31, n)),
-                  'u32': pa.array(g.integers(0, 2 ** 32, n, dtype=np.uint64).astype(np.uint32))})
-    seen = []
+    cols = {}
+    for k in range(copies):
+        cols['f32_%d' % k] = pa.array(g.standard_normal(n).astype(np.float32), mask=g.random(n) < 0.05)
+        cols['i64_2p31_%d' % k] = pa.array(g.integers(-2 ** 31, 2 ** 31, n))
+        cols['u32_%d' % k] = pa.array(g.integers(0, 2 ** 32, n, dtype=np.uint64).astype(np.uint32))
+    t = pa.table(cols)
+    seen, pre = [], []
     orig = Engine._distinct32_launch
 
     def spy(self, col, lo):
         seen.append(col.name)
+        c = self._counted.get(id(col))
+        pre.append(bool(c is not None and c.get('d32')))
         return orig(self, col, lo)
     Engine._distinct32_launch = spy
     try:
         assert_describe_equal(describe(t, plots=False), oracle.describe(t))
     finally:
         Engine._distinct32_launch = orig
-    assert sorted(seen) == ['f32', 'i64_2p31', 'u32']
+    assert sorted(seen) == sorted(cols)
+    assert all(pre) == (len(cols) >= 8) and (any(pre) == (len(cols) >= 8))
