@@ -249,7 +249,7 @@ def test_distinct32_exact(case):
 
 
 @pytest.mark.parametrize('copies', [1, 3])
-def test_distinct32_describe_path(copies):
+def test_distinct32_describe_path(copies, monkeypatch):
     """describe() routes float32 and < 2^32-range integral columns without
     heavy keys to sdp_distinct32 and matches the oracle; with >= 8 numeric
     columns (the batched pass 2) their level-1 count rides pass 2's read."""
@@ -264,6 +264,8 @@ def test_distinct32_describe_path(copies):
         cols['i64_2p31_%d' % k] = pa.array(g.integers(-2 ** 31, 2 ** 31, n))
         cols['u32_%d' % k] = pa.array(g.integers(0, 2 ** 32, n, dtype=np.uint64).astype(np.uint32))
     t = pa.table(cols)
+    # (9 short columns would otherwise take the fused wide-table partitioning)
+    monkeypatch.setattr(Engine, 'FUSE_MIN_COLS', 100)
     seen, pre = [], []
     orig = Engine._distinct32_launch
 
@@ -279,3 +281,19 @@ def test_distinct32_describe_path(copies):
         Engine._distinct32_launch = orig
     assert sorted(seen) == sorted(cols)
     assert all(pre) == (len(cols) >= 8) and (any(pre) == (len(cols) >= 8))
+
+
+def test_wide_short_tables_keep_fused_partitioning():
+    """>= 8 short (<= 2^26-row) 32-bit key columns keep the fused wide-table
+    partitioning path (one launch per stage for all of them), not one
+    sdp_distinct32 each (engine.distinct_paths)."""
+    from spark_df_profiling.engine import Engine
+    from spark_df_profiling.columns import DeviceTable
+    g = datagen.rng(29)
+    n = 100_000
+    t = pa.table({'f%d' % k: pa.array(g.standard_normal(n).astype(np.float32)) for k in range(9)})
+    dt = DeviceTable.from_arrow(t)
+    e = Engine()
+    paths = e.distinct_paths(dt.columns, [n] * 9, [None] * 9)
+    assert paths == ['group'] * 9
+    assert e.distinct_paths(dt.columns[:3], [n] * 3, [None] * 3) == ['bits32'] * 3
