@@ -481,11 +481,7 @@ __device__ __forceinline__ void bytes_tile_b(const sdp_bytes_column &col, int64_
     // coalesced 16-byte chunks and handed to the lanes by ds_bpermute -- was
     // measured 12 % slower on the count pass: 8.8 -> 9.9 ms per 1e9 rows)
     uint32_t w[RPT][5];
-#ifndef SDP_X_NOWORDS
     bytes_tile_words<RPT>(col, a, w);
-#else
-    for (int q = 0; q < RPT; ++q) for (int i = 0; i < 5; ++i) w[q][i] = (uint32_t)a.o0[q] * (i + 1);
-#endif
     bytes_tile_decode<NT, RPT>(col, base, a, w, k0, k1, meta, h, t);
 }
 
@@ -676,28 +672,16 @@ __global__ void __launch_bounds__(BR_T, BR_MINB) part_records_rows_bytes_kernel(
             bool keep = false;
             if ((vmask >> q) & 1u) {
                 ++rows;
-#ifndef SDP_X_NOHEAVY
                 const int hv = heavy_find_bytes(s.heavy, heavy.n, h[q], k0[q], k1[q], (uint32_t)(meta[q] >> 40));
-#else
-                const int hv = -1;
-#endif
-#ifndef SDP_X_NOHEAVYCNT
                 if (hv >= 0) atomicAdd(&s.heavy.cnt[hv], 1u);
-#else
-                if (hv >= 0) rows += 2;
-#endif
                 else keep = true;
             }
             const uint64_t m = __ballot(keep);
             if (keep) {
                 const int64_t o = cur + lane_rank(m);
-#ifndef SDP_X_NOSTORE
                 out_k0[o] = k0[q];
                 out_k1[o] = k1[q];
                 out_meta[o] = meta[q];
-#else
-                if (k0[q] == 0x1234567ull) out_k0[o] = k1[q] + meta[q];
-#endif
                 atomicAdd(&s.hist[w][b1 ? (int)(h[q] >> shift) : 0], 1u);
             }
             cur += __popcll(m);

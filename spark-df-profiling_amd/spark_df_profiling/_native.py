@@ -319,6 +319,23 @@ def annotate(label, alg_bytes):
         _tls.pending = (label, float(alg_bytes))
 
 
+def recorded_index(key):
+    """Index of the last recorded launch keyed `key` (None when not recording)."""
+    rec = _recorder
+    return len(rec[key]) - 1 if rec is not None and rec.get(key) else None
+
+
+def annotate_output(key, index, out_bytes):
+    """Add the bytes a recorded launch (entry `index` under `key`, e.g.
+    'sdp_part_rows_records[bytes/records]') wrote, once they are known from a
+    later readback: a kernel whose output size is data dependent (the records
+    of a byte column) is annotated with its input at launch time."""
+    rec = _recorder
+    if rec is not None and index is not None and rec.get(key) and index < len(rec[key]):
+        ev0, ev1, b = rec[key][index]
+        rec[key][index] = (ev0, ev1, (b or 0.0) + float(out_bytes))
+
+
 def start_recording():
     global _recorder
     _recorder = {}

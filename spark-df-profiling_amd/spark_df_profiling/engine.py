@@ -1378,6 +1378,8 @@ class Engine:
             sdp.sdp_part_rows_records(ctypes.byref(ctx['bc']), ctypes.byref(hv['struct']) if hv else None,
                                       ctx['b1'], ptr(ctx['h1']), ptr(chunks), ctypes.byref(r0), ptr(ctx['hcnt']),
                                       ptr(ctx['stats']), self._s())
+            ctx['rec_key'] = 'sdp_part_rows_records[%s]' % _label(col, 'records')
+            ctx['rec_idx'] = nat.recorded_index(ctx['rec_key'])
             ctx.update({'r0': r0, 'keep0': keep0, 'chunks0': chunks})
             return
         nat.annotate(_label(col, 'count'), ctx['rb'])
@@ -1419,6 +1421,8 @@ class Engine:
         nrec = int(bsn[-1])
         r1, keep1 = self._records(nrec, isb)
         if ctx.get('one_read'):
+            # the records kernel's compulsory output: its nrec 24-byte records
+            nat.annotate_output(ctx['rec_key'], ctx['rec_idx'], nrec * recw)
             if nrec:                  # level-1 scatter of the compacted strip records (sequential 24-byte reads)
                 nat.annotate('bytes/l1scatter', 2 * nrec * recw)
                 sdp.sdp_part_recs(ctypes.byref(ctx['r0']), 1, ptr(ctx['chunks0']), grid, 0, b1, 1, None, ptr(o1),
