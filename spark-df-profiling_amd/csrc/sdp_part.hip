@@ -1364,12 +1364,21 @@ __global__ void __launch_bounds__(DT) part_dedup_bytes_kernel(const uint64_t *in
     __shared__ uint64_t s_k1[D_B];
     __shared__ uint64_t s_meta[D_B];
     __shared__ uint32_t s_cnt[D_B];
+    // slots claimed in this bucket, in claim order: the output and the reset of
+    // the table walk the bucket's groups only (a zipf bucket of ~2 K records
+    // holds a few hundred groups, a mid-cardinality one often a handful), not
+    // all D_B slots
+    __shared__ uint16_t s_list[D_B];
     __shared__ uint32_t s_n, s_full, s_coll;
     const int t = threadIdx.x;
     uint64_t acc_groups = 0;
     bool acc_full = false, acc_coll = false;
     int64_t f = blockIdx.x, lo = 0, hi = 0;
     DRound cur, nxt;
+    for (int i = t; i < D_B; i += DT) {                 // once: buckets reset only their own slots
+        s_h[i] = EMPTY64;
+        s_cnt[i] = 0;
+    }
     if (f < nbuckets) {
         lo = starts[f];
         hi = starts[f + 1];
@@ -1386,10 +1395,6 @@ __global__ void __launch_bounds__(DT) part_dedup_bytes_kernel(const uint64_t *in
         if (lo == hi) {
             if (t == 0) ngroups[f] = 0;
         } else {
-            for (int i = t; i < D_B; i += DT) {
-                s_h[i] = EMPTY64;
-                s_cnt[i] = 0;
-            }
             if (t == 0) { s_n = 0; s_full = 0; s_coll = 0; }
             lds_barrier();
             for (int64_t rb = lo; rb < hi; rb += (int64_t)DT * D_RPT) {
@@ -1410,7 +1415,12 @@ __global__ void __launch_bounds__(DT) part_dedup_bytes_kernel(const uint64_t *in
                         if (c == EMPTY64) {
                             c = atomicCAS((unsigned long long *)&s_h[p], (unsigned long long)EMPTY64,
                                           (unsigned long long)hk);
-                            if (c == EMPTY64) { pos[q] = (int)p; mine |= 1u << q; break; }
+                            if (c == EMPTY64) {
+                                pos[q] = (int)p;
+                                mine |= 1u << q;
+                                s_list[atomicAdd(&s_n, 1u)] = (uint16_t)p;
+                                break;
+                            }
                         }
                         if (c == hk) { pos[q] = (int)p; break; }
                         p = (p + 1) & (D_B - 1);
@@ -1445,24 +1455,22 @@ __global__ void __launch_bounds__(DT) part_dedup_bytes_kernel(const uint64_t *in
                 }
                 lds_barrier();
             }
-            for (int i0 = 0; i0 < D_B; i0 += DT) {                 // every thread runs every round: ballots
-                const int i = i0 + t;
-                const uint64_t hk = s_h[i];
-                const bool g = hk != EMPTY64;
-                const uint64_t m = __ballot(g);
-                uint32_t base = 0;
-                if (lane_id() == 0 && m) base = atomicAdd(&s_n, (uint32_t)__popcll(m));
-                base = __shfl(base, 0, WAVE);
-                if (g) {
-                    const uint32_t p = base + (uint32_t)lane_rank(m);
-                    out_key[lo + p] = ((hk >> 40) << 40) | (s_meta[i] & RMASK40);
-                    out_cnt[lo + p] = s_cnt[i];
-                }
+            const uint32_t ng = s_n;
+            for (uint32_t i = t; i < ng; i += DT) {                // the bucket's groups, claim order
+                const int p = s_list[i];
+                const uint64_t hk = s_h[p];
+                out_key[lo + i] = ((hk >> 40) << 40) | (s_meta[p] & RMASK40);
+                out_cnt[lo + i] = s_cnt[p];
             }
             lds_barrier();
+            for (uint32_t i = t; i < ng; i += DT) {                // reset the claimed slots
+                const int p = s_list[i];
+                s_h[p] = EMPTY64;
+                s_cnt[p] = 0;
+            }
             if (t == 0) {
-                ngroups[f] = s_n;
-                acc_groups += s_n;
+                ngroups[f] = ng;
+                acc_groups += ng;
                 acc_full |= s_full != 0;
                 acc_coll |= s_coll != 0;
             }
