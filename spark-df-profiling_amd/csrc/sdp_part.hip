@@ -399,9 +399,13 @@ __device__ __forceinline__ uint64_t mask_bytes(uint64_t v, int64_t avail) {
     return avail <= 0 ? 0ull : (avail >= 8 ? v : (v & ((1ull << (8 * avail)) - 1ull)));
 }
 
-// The same tile in two stages, so a kernel can issue the NEXT tile's validity
-// and offsets (stage A) before it fetches this tile's key bytes (stage B, which
-// depends on A) and works on them: one memory latency per tile instead of two.
+// A tile of rows in stages: A1 issues the validity bytes and offsets, A2 turns
+// them into a mask and lengths, B1 issues the key words (which depend on A), B2
+// decodes and hashes.  The row kernels run A2(i) B1(i) A1(i+1) B2(i): the next
+// tile's stage A is in flight while this tile is decoded and stored.  (A
+// wave-cooperative B1 -- each wave's span of key bytes read as coalesced 16-byte
+// chunks and handed to the lanes by ds_bpermute -- measured 12 % slower on the
+// count pass: 8.8 -> 9.9 ms per 1e9 rows.)
 typedef uint32_t u32x4a4 __attribute__((ext_vector_type(4), aligned(4)));
 
 template <int RPT>
@@ -410,22 +414,74 @@ struct BytesOffs {
     uint32_t ln[RPT];                   // string length (strings of >= 4 GiB are not supported)
     uint32_t vmask;
 };
+// OW: the offsets layout -- 8 or 4 (Arrow offsets of that width) or 0 (fixed
+// width) -- a template argument, so no layout test sits between the loads.
+// the OW a column's layout selects (-1: neither)
+static inline int bytes_ow(const sdp_bytes_column &col) {
+    if (col.fixed_width > 0) return 0;
+    return (col.offset_width == 8 || col.offset_width == 4) ? col.offset_width : -1;
+}
+template <int RPT>
+struct BytesRaw {                       // stage A as loaded: not yet waited on
+    int64_t o0[RPT], o1[RPT];
+    uint32_t vb[RPT];                   // the validity byte holding the row's bit
+};
+// stage A1: issue every load of the tile and use none of them.  Rows past the
+// end are clamped to the last row and offsets are read whether or not the row
+// is valid (an Arrow offsets buffer always holds length + 1 entries), so there
+// is no control flow between the loads; the layout is a template argument.
+// Testing validity right after the loads waits them out in place -- one memory
+// latency per row (the records kernel measured 71 % of its wave cycles waiting).
+template <int NT, int RPT, int OW>
+__device__ __forceinline__ void bytes_tile_issue(const sdp_bytes_column &col, int64_t base, int64_t end,
+                                                 BytesRaw<RPT> &raw, int t) {
+    // without a validity bitmap the byte comes from a buffer that is at least
+    // length / 8 bytes long and stage A2 forces it to all-valid (a load either
+    // way, so no branch splits the tile's loads)
+    const bool has_valid = col.d_validity != nullptr;
+    const uint8_t *vp = has_valid ? col.d_validity : (OW == 0 ? col.d_data : (const uint8_t *)col.d_offsets);
+    const int64_t vo = has_valid ? col.validity_bit_offset : 0;
+#pragma unroll
+    for (int q = 0; q < RPT; ++q) {
+        const int64_t r = min(base + (int64_t)q * NT + t, end - 1);
+        raw.vb[q] = vp[(vo + r) >> 3];
+        if constexpr (OW == 0) {
+            raw.o0[q] = r * (int64_t)col.fixed_width;
+            raw.o1[q] = raw.o0[q] + col.fixed_width;
+        } else if constexpr (OW == 8) {
+            raw.o0[q] = ((const int64_t *)col.d_offsets)[r];
+            raw.o1[q] = ((const int64_t *)col.d_offsets)[r + 1];
+        } else {
+            raw.o0[q] = ((const int32_t *)col.d_offsets)[r];
+            raw.o1[q] = ((const int32_t *)col.d_offsets)[r + 1];
+        }
+    }
+}
+// The row kernels issue the next tile's stage A unconditionally -- past the
+// last tile it re-reads the last row -- so the count of loads in flight is the
+// same on every path and the wait for this tile's key words leaves them flying.
+// stage A2: validity mask and lengths (register work only; the first use of
+// the loads, so it belongs where the tile is about to be worked on)
 template <int NT, int RPT>
-__device__ __forceinline__ void bytes_tile_a(const sdp_bytes_column &col, int64_t base, int64_t end,
-                                             BytesOffs<RPT> &a, int t) {
+__device__ __forceinline__ void bytes_tile_ready(const sdp_bytes_column &col, int64_t base, int64_t end,
+                                                 const BytesRaw<RPT> &raw, BytesOffs<RPT> &a, int t) {
+    const uint32_t vfill = col.d_validity ? 0u : 0xFFu;
     a.vmask = 0;
 #pragma unroll
     for (int q = 0; q < RPT; ++q) {
         const int64_t row = base + (int64_t)q * NT + t;
-        const bool ok = row < end && valid_bit(col.d_validity, col.validity_bit_offset, row);
-        a.vmask |= (uint32_t)ok << q;
-        const int64_t b0 = ok ? str_off(col, row) : 0;
-        a.o0[q] = b0;
-        a.ln[q] = ok ? (uint32_t)(str_off(col, row + 1) - b0) : 0u;
+        const uint32_t ok =
+            (uint32_t)(row < end) & ((raw.vb[q] | vfill) >> ((col.validity_bit_offset + row) & 7)) & 1u;
+        a.vmask |= ok << q;
+        a.o0[q] = ok ? raw.o0[q] : 0;
+        // (the clamp reads o1's high word: a loaded register left dead is
+        // reused for temporaries while its load is still in flight, and every
+        // such reuse waits for all outstanding loads)
+        a.ln[q] = ok ? (uint32_t)min(raw.o1[q] - raw.o0[q], (int64_t)UINT32_MAX) : 0u;
     }
 }
 
-// stage B1: the key words of a tile (issue only; stage B2 decodes them)
+// stage B1: the key words of a tile (issue only)
 template <int RPT>
 __device__ __forceinline__ void bytes_tile_words(const sdp_bytes_column &col, const BytesOffs<RPT> &a,
                                                  uint32_t (&w)[RPT][5]) {
@@ -473,18 +529,6 @@ __device__ __forceinline__ void bytes_tile_decode(const sdp_bytes_column &col, i
     }
 }
 
-template <int NT, int RPT>
-__device__ __forceinline__ void bytes_tile_b(const sdp_bytes_column &col, int64_t base, const BytesOffs<RPT> &a,
-                                             uint64_t (&k0)[RPT], uint64_t (&k1)[RPT], uint64_t (&meta)[RPT],
-                                             uint64_t (&h)[RPT], int t) {
-    // (a wave-cooperative variant -- each wave's span of key bytes read as
-    // coalesced 16-byte chunks and handed to the lanes by ds_bpermute -- was
-    // measured 12 % slower on the count pass: 8.8 -> 9.9 ms per 1e9 rows)
-    uint32_t w[RPT][5];
-    bytes_tile_words<RPT>(col, a, w);
-    bytes_tile_decode<NT, RPT>(col, base, a, w, k0, k1, meta, h, t);
-}
-
 struct BCountLds {
     HeavyLdsT<true> heavy;
     uint32_t hist[MAXB];
@@ -501,6 +545,7 @@ struct BScatterLds {
     uint32_t wsum[B_ST / WAVE];
 };
 
+template <int OW>
 __global__ void __launch_bounds__(B_CT) part_count_rows_bytes_kernel(sdp_bytes_column col, HeavyArg heavy, int b1,
                                                                      int64_t rows_per_block, uint32_t *hist,
                                                                      uint64_t *heavy_counts, uint64_t *stats) {
@@ -515,15 +560,17 @@ __global__ void __launch_bounds__(B_CT) part_count_rows_bytes_kernel(sdp_bytes_c
     lds_barrier();
     uint64_t rows = 0;
     constexpr int64_t STEP = (int64_t)B_CT * B_C_RPT;
-    BytesOffs<B_C_RPT> oc, on;
-    if (r0 < r1) bytes_tile_a<B_CT, B_C_RPT>(col, r0, r1, oc, t);
+    BytesRaw<B_C_RPT> raw;
+    if (r0 < r1) bytes_tile_issue<B_CT, B_C_RPT, OW>(col, r0, r1, raw, t);
     for (int64_t base = r0; base < r1; base += STEP) {
         uint64_t k0[B_C_RPT], k1[B_C_RPT], meta[B_C_RPT], h[B_C_RPT];
-        const bool more = base + STEP < r1;
-        if (more) bytes_tile_a<B_CT, B_C_RPT>(col, base + STEP, r1, on, t);   // next tile's offsets in flight
-        bytes_tile_b<B_CT, B_C_RPT>(col, base, oc, k0, k1, meta, h, t);
+        uint32_t wd[B_C_RPT][5];
+        BytesOffs<B_C_RPT> oc;
+        bytes_tile_ready<B_CT, B_C_RPT>(col, base, r1, raw, oc, t);
+        bytes_tile_words<B_C_RPT>(col, oc, wd);
+        bytes_tile_issue<B_CT, B_C_RPT, OW>(col, base + STEP, r1, raw, t);   // next tile in flight (see below)
+        bytes_tile_decode<B_CT, B_C_RPT>(col, base, oc, wd, k0, k1, meta, h, t);
         const uint32_t vmask = oc.vmask;
-        if (more) oc = on;
 #pragma unroll
         for (int q = 0; q < B_C_RPT; ++q) {
             if ((vmask >> q) & 1u) {
@@ -540,6 +587,7 @@ __global__ void __launch_bounds__(B_CT) part_count_rows_bytes_kernel(sdp_bytes_c
     block_add_u64(rows, &stats[0]);
 }
 
+template <int OW>
 __global__ void __launch_bounds__(B_ST) part_scatter_rows_bytes_kernel(sdp_bytes_column col, HeavyArg heavy, int b1,
                                                                        int64_t rows_per_block, const uint64_t *offs,
                                                                        uint64_t *out_k0, uint64_t *out_k1,
@@ -556,18 +604,21 @@ __global__ void __launch_bounds__(B_ST) part_scatter_rows_bytes_kernel(sdp_bytes
         s.cur[b] = offs[(int64_t)b * G + g];
     }
     lds_barrier();
-    BytesOffs<B_S_RPT> oc, on;
-    if (r0 < r1) bytes_tile_a<B_ST, B_S_RPT>(col, r0, r1, oc, t);
+    BytesRaw<B_S_RPT> raw;
+    if (r0 < r1) bytes_tile_issue<B_ST, B_S_RPT, OW>(col, r0, r1, raw, t);
     for (int64_t base = r0; base < r1; base += B_S_TILE) {
         uint64_t k0[B_S_RPT], k1[B_S_RPT], meta[B_S_RPT], h[B_S_RPT];
         uint32_t rank[B_S_RPT];
         int bk[B_S_RPT];
         uint32_t keep = 0;
-        const bool more = base + B_S_TILE < r1;
-        bytes_tile_b<B_ST, B_S_RPT>(col, base, oc, k0, k1, meta, h, t);
+        uint32_t wd[B_S_RPT][5];
+        BytesOffs<B_S_RPT> oc;
+        bytes_tile_ready<B_ST, B_S_RPT>(col, base, r1, raw, oc, t);
+        bytes_tile_words<B_S_RPT>(col, oc, wd);
+        // the next tile's stage A flies during this tile's LDS phases
+        bytes_tile_issue<B_ST, B_S_RPT, OW>(col, base + B_S_TILE, r1, raw, t);
+        bytes_tile_decode<B_ST, B_S_RPT>(col, base, oc, wd, k0, k1, meta, h, t);
         const uint32_t vmask = oc.vmask;
-        // the next tile's offsets fly during this tile's LDS phases
-        if (more) bytes_tile_a<B_ST, B_S_RPT>(col, base + B_S_TILE, r1, on, t);
 #pragma unroll
         for (int q = 0; q < B_S_RPT; ++q) {
             if ((vmask >> q) & 1u) {
@@ -606,7 +657,6 @@ __global__ void __launch_bounds__(B_ST) part_scatter_rows_bytes_kernel(sdp_bytes
             s.hist[b] = 0;
         }
         lds_barrier();
-        if (more) oc = on;
     }
 }
 
@@ -639,6 +689,7 @@ struct BRecLds {
 };
 
 constexpr int BR_MINB = 4;
+template <int OW>
 __global__ void __launch_bounds__(BR_T, BR_MINB) part_records_rows_bytes_kernel(sdp_bytes_column col, HeavyArg heavy, int b1,
                                                                        int64_t rows_per_block, uint32_t *hist,
                                                                        Chunk *chunks, uint64_t *out_k0,
@@ -658,15 +709,17 @@ __global__ void __launch_bounds__(BR_T, BR_MINB) part_records_rows_bytes_kernel(
     uint64_t rows = 0;
     int64_t cur = s0;                                               // next record slot of this strip
     constexpr int64_t STEP = (int64_t)WAVE * BR_RPT;
-    BytesOffs<BR_RPT> oc, on;
-    if (s0 < s1) bytes_tile_a<WAVE, BR_RPT>(col, s0, s1, oc, lane);
+    BytesRaw<BR_RPT> raw;
+    if (s0 < s1) bytes_tile_issue<WAVE, BR_RPT, OW>(col, s0, s1, raw, lane);
     for (int64_t base = s0; base < s1; base += STEP) {
         uint64_t k0[BR_RPT], k1[BR_RPT], meta[BR_RPT], h[BR_RPT];
-        const bool more = base + STEP < s1;
-        if (more) bytes_tile_a<WAVE, BR_RPT>(col, base + STEP, s1, on, lane);   // next tile's offsets in flight
-        bytes_tile_b<WAVE, BR_RPT>(col, base, oc, k0, k1, meta, h, lane);
+        uint32_t wd[BR_RPT][5];
+        BytesOffs<BR_RPT> oc;
+        bytes_tile_ready<WAVE, BR_RPT>(col, base, s1, raw, oc, lane);
+        bytes_tile_words<BR_RPT>(col, oc, wd);                  // this tile's key words, then
+        bytes_tile_issue<WAVE, BR_RPT, OW>(col, base + STEP, s1, raw, lane);   // the next tile's stage A
+        bytes_tile_decode<WAVE, BR_RPT>(col, base, oc, wd, k0, k1, meta, h, lane);
         const uint32_t vmask = oc.vmask;
-        if (more) oc = on;
 #pragma unroll
         for (int q = 0; q < BR_RPT; ++q) {
             bool keep = false;
@@ -1949,12 +2002,17 @@ int sdp_part_rows(const sdp_column *col, const sdp_bytes_column *bcol, const sdp
     hipStream_t s = (hipStream_t)stream;
     if (bcol) {
         if (bcol->length >= (int64_t)RMASK40) return set_error(SDP_EINVAL, "part_rows: more than 2^40 rows");
+        const int ow = bytes_ow(*bcol);
+        if (ow < 0) return set_error(SDP_EINVAL, "part_rows: offset_width must be 4 or 8");
         if (phase == 0)
-            hipLaunchKernelGGL(part_count_rows_bytes_kernel, dim3(grid), dim3(B_CT), 0, s, *bcol, hv, b1, rpb, d_hist,
-                               d_heavy_counts, d_stats);
+            hipLaunchKernelGGL(ow == 8 ? part_count_rows_bytes_kernel<8>
+                               : ow == 4 ? part_count_rows_bytes_kernel<4> : part_count_rows_bytes_kernel<0>,
+                               dim3(grid), dim3(B_CT), 0, s, *bcol, hv, b1, rpb, d_hist, d_heavy_counts, d_stats);
         else
-            hipLaunchKernelGGL(part_scatter_rows_bytes_kernel, dim3(grid), dim3(B_ST), 0, s, *bcol, hv, b1, rpb,
-                               d_offsets, d_out->d_k0, d_out->d_k1, d_out->d_meta);
+            hipLaunchKernelGGL(ow == 8 ? part_scatter_rows_bytes_kernel<8>
+                               : ow == 4 ? part_scatter_rows_bytes_kernel<4> : part_scatter_rows_bytes_kernel<0>,
+                               dim3(grid), dim3(B_ST), 0, s, *bcol, hv, b1, rpb, d_offsets, d_out->d_k0, d_out->d_k1,
+                               d_out->d_meta);
         return check_launch("part_rows_bytes_kernel");
     }
     uint64_t *out = phase ? d_out->d_k0 : nullptr;
@@ -2013,7 +2071,11 @@ int sdp_part_rows_records(const sdp_bytes_column *bcol, const sdp_heavy *heavy, 
     const int64_t n = bcol->length;
     const int64_t rpb = records_rows_per_block(n);
     const int grid = (int)((n + rpb - 1) / rpb < 1 ? 1 : (n + rpb - 1) / rpb);
-    hipLaunchKernelGGL(part_records_rows_bytes_kernel, dim3(grid), dim3(BR_T), 0, (hipStream_t)stream, *bcol, hv, b1,
+    const int ow = bytes_ow(*bcol);
+    if (ow < 0) return set_error(SDP_EINVAL, "part_records_rows: offset_width must be 4 or 8");
+    hipLaunchKernelGGL(ow == 8 ? part_records_rows_bytes_kernel<8>
+                       : ow == 4 ? part_records_rows_bytes_kernel<4> : part_records_rows_bytes_kernel<0>,
+                       dim3(grid), dim3(BR_T), 0, (hipStream_t)stream, *bcol, hv, b1,
                        rpb, d_hist, (Chunk *)d_chunks, d_out->d_k0, d_out->d_k1, d_out->d_meta, d_heavy_counts,
                        d_stats);
     return check_launch("part_records_rows_bytes_kernel");
