@@ -3,21 +3,26 @@
 The reference renders `hist_data` with matplotlib into base64 PNG data URIs
 (/root/reference/spark_df_profiling/plot.py:20-55) inside the stats engine.
 This is host-side presentation, out of the GPU path's scope; it is restated
-for current matplotlib (object API, Agg canvas, no pyplot global state, so it
-is safe to call from worker threads).
+for current matplotlib: its Agg renderer, fonts, tick locators and formatters,
+without pyplot's global state (safe in worker threads) and without the
+Figure/Axis artist machinery (see _render).
 """
 
 import base64
+import struct
 import threading
-from io import BytesIO
+import zlib
 
 import numpy as np
 import pandas as pd
-from matplotlib.backends.backend_agg import FigureCanvasAgg
+from matplotlib.backends.backend_agg import RendererAgg
 from matplotlib.figure import Figure
+from matplotlib.font_manager import FontProperties
+from matplotlib.path import Path
+from matplotlib.transforms import IdentityTransform
 
 BASE = 'data:image/png;base64,'
-BAR_COLOR = '#337ab7'
+BAR_COLOR = (0x33 / 255, 0x7a / 255, 0xb7 / 255, 1.0)      # '#337ab7'
 
 
 def hist_frame(counts, edges, width):
@@ -29,80 +34,214 @@ def hist_frame(counts, edges, width):
                          'left_edge': [float(e) for e in edges], 'width': float(width)})
 
 
-def _encode(canvas):
-    """PNG -> base64 -> percent-quoted, as plot.py:35-37 stores it.  zlib level 1
-    (the images are mostly flat colour: same pixels, ~1/6 of the encode time);
-    quote() of base64 text only ever escapes '+' and '=' (the alphabet is
-    alphanumerics, '+', '/' and '='; '/' is quote's default safe character)."""
-    buf = BytesIO()
-    canvas.print_png(buf, pil_kwargs={'compress_level': 1})
-    b64 = base64.b64encode(buf.getvalue()).decode('ascii')
-    return BASE + b64.replace('+', '%2B').replace('=', '%3D')
-
-
 def _safe_width(w):
     w = float(w)
     return w if np.isfinite(w) and w > 0 else 1.0
 
 
-# One figure per (kind, bin count) and thread, built once and re-used: only the
-# bar rectangles and the view limits change between columns.  Building a
-# Figure + Axes + tick artists costs about as much as drawing them, so a
-# re-used figure halves the cost of an image (64 -> 33 ms on this image's
-# CPU).  Thread-local, so SDP_PLOT_WORKERS=0 with column workers stays safe.
+# ----------------------------------------------------------------------------
+# The two figures of plot.py:20-55 -- bars in '#337ab7' from each left edge,
+# the axes box, outward major ticks with matplotlib's own tick locations and
+# labels (AutoLocator / ScalarFormatter, offset text included), 'Frequency' on
+# the large one's y axis, only the first and last x ticks at 8 pt on the mini
+# one -- drawn straight onto an Agg canvas.  Going through Figure.draw costs
+# ~28 ms per large image, ~70 % of it in the Axis artists' generic tick and
+# bounding-box bookkeeping; the same primitives issued directly (one compound
+# path for the bars, one for the ticks, text laid out with matplotlib's own
+# alignment rules) cost ~4 ms, and a C5 table has 1024 images.  The layout
+# constants are matplotlib's defaults at 100 dpi (tests/test_plot_cpu.py
+# compares the images with Figure.savefig's).
+# ----------------------------------------------------------------------------
+_DPI = 100.0
+_PT = _DPI / 72.0
+_TICK = 3.5 * _PT                # xtick/ytick.major.size, direction out
+_PAD = 3.5 * _PT                 # xtick/ytick.major.pad
+_OFFPAD = 3 * _PT                # Axis.OFFSETTEXTPAD
+_LABELPAD = 4 * _PT              # axes.labelpad
+_LW = 0.8                        # axes.linewidth = major tick width (points)
+_KINDS = {'complete': dict(size=(6, 4), box=(0.15, 0.1, 0.95, 0.9), yaxis=True),
+          'mini': dict(size=(2, 0.75), box=(0.15, 0.35, 0.85, 1.0), yaxis=False)}
 _TLS = threading.local()
 
 
-def _figure(kind, nbins):
-    cache = getattr(_TLS, 'figs', None)
+class _Canvas:
+    """Per thread and kind: an undrawn Axes of the figure's geometry (its
+    locators and formatters give the tick values and labels), fonts and a
+    text-metrics cache."""
+
+    def __init__(self, kind):
+        g = _KINDS[kind]
+        fig = Figure(figsize=g['size'], dpi=_DPI)
+        self.ax = fig.add_subplot(111)
+        l, b, r, t = g['box']
+        fig.subplots_adjust(left=l, right=r, top=t, bottom=b, wspace=0, hspace=0)
+        self.W, self.H = int(round(g['size'][0] * _DPI)), int(round(g['size'][1] * _DPI))
+        bb = self.ax.bbox
+        self.box = (bb.x0, bb.y0, bb.x1, bb.y1)
+        self.clip = bb.frozen()
+        self.yaxis = g['yaxis']
+        self.fonts = {8: FontProperties(size=8), 10: FontProperties(size=10)}
+        self.metrics = {}
+
+    def ticks(self, axis, lo, hi):
+        axis.set_view_interval(lo, hi, ignore=True)
+        locs = np.asarray(axis.get_majorticklocs(), dtype=np.float64)
+        fmt = axis.get_major_formatter()
+        labels = fmt.format_ticks(locs)
+        # drawn: the ticks inside the view interval, with the relative
+        # tolerance of Axis._update_ticks (transforms._interval_contains_close)
+        tol = 1e-10 * (hi - lo)
+        inside = (locs >= lo - tol) & (locs <= hi + tol)
+        return locs, labels, inside, fmt.get_offset()
+
+    def extent(self, r, s, size):
+        """(w, h, d) of a text line as Text._get_layout sizes it (at least
+        the height and descent of 'lp')."""
+        key = (s, size)
+        m = self.metrics.get(key)
+        if m is None:
+            prop = self.fonts[size]
+            w, h, d = r.get_text_width_height_descent(s, prop, ismath=False)
+            lp = self.metrics.get(('lp', size))
+            if lp is None:
+                lp = self.metrics[('lp', size)] = r.get_text_width_height_descent('lp', prop, ismath=False)
+            m = self.metrics[key] = (w, max(h, lp[1]), max(d, lp[2]))
+        return m
+
+
+def _canvas(kind):
+    cache = getattr(_TLS, 'canvases', None)
     if cache is None:
-        cache = _TLS.figs = {}
-    key = (kind, nbins)
-    if key not in cache:
-        fig = Figure(figsize=(2, 0.75) if kind == 'mini' else (6, 4))
-        ax = fig.add_subplot(111)
-        bars = ax.bar(np.arange(nbins, dtype=np.float64), np.ones(nbins), width=1.0,
-                      facecolor=BAR_COLOR, align='edge')
-        if kind == 'mini':
-            ax.get_yaxis().set_visible(False)
-            ax.set_facecolor('w')
-            fig.subplots_adjust(left=0.15, right=0.85, top=1, bottom=0.35, wspace=0, hspace=0)
-        else:
-            ax.set_ylabel('Frequency')
-            fig.subplots_adjust(left=0.15, right=0.95, top=0.9, bottom=0.1, wspace=0, hspace=0)
-        cache[key] = (FigureCanvasAgg(fig), ax, list(bars.patches))
-    return cache[key]
+        cache = _TLS.canvases = {}
+    c = cache.get(kind)
+    if c is None:
+        c = cache[kind] = _Canvas(kind)
+    return c
+
+
+def _text(c, r, gc, s, x, y, ha, va, size, draw=True):
+    """A horizontal single-line text anchored at display (x, y) (y up) with
+    Text's alignment rules; returns its box (x0, y0, x1, y1)."""
+    w, h, d = c.extent(r, s, size)
+    x0 = x - {'center': w / 2, 'right': w, 'left': 0.0}[ha]
+    base = {'top': y - (h - d), 'center_baseline': y - (h - d) / 2, 'baseline': y, 'bottom': y + d}[va]
+    if draw:
+        r.draw_text(gc, x0, c.H - base, s, c.fonts[size], 0)
+    return (x0, base - d, x0 + w, base - d + h)
+
+
+def _render(kind, left, height, w):
+    c = _canvas(kind)
+    r = RendererAgg(c.W, c.H, _DPI)
+    L, B, R, T = c.box
+    n = len(left)
+    x0, x1 = float(left.min()), float(left.max()) + w
+    y1 = float(height.max()) if n else 0.0
+    if np.isfinite(x0) and np.isfinite(x1) and x1 > x0 and np.isfinite(y1) and y1 > 0:
+        # the limits autoscale_view sets for these bars (axes margins 0.05,
+        # bars sticky at y = 0)
+        mx = 0.05 * (x1 - x0)
+        xl, yl = (x0 - mx, x1 + mx), (0.0, y1 + 0.05 * y1)
+    else:
+        xl = (x0 - 0.5, x1 + 0.5) if np.isfinite(x0) and np.isfinite(x1) else (-0.5, 0.5)
+        yl = (0.0, 1.0)
+    sx, sy = (R - L) / (xl[1] - xl[0]), (T - B) / (yl[1] - yl[0])
+    ident = IdentityTransform()
+    gc = r.new_gc()
+    gc.set_linewidth(0)
+    r.draw_path(gc, Path([(0, 0), (c.W, 0), (c.W, c.H), (0, c.H), (0, 0)], closed=True), ident,
+                (1.0, 1.0, 1.0, 1.0))                                    # figure and axes faces
+    if n:
+        xa = L + (left - xl[0]) * sx
+        xb = L + (left + w - xl[0]) * sx
+        yt = B + (height - yl[0]) * sy
+        y0 = np.full(n, B - yl[0] * sy)
+        verts = np.stack([xa, y0, xb, y0, xb, yt, xa, yt, xa, y0], 1).reshape(-1, 2)
+        codes = np.tile(np.array([Path.MOVETO, Path.LINETO, Path.LINETO, Path.LINETO, Path.CLOSEPOLY],
+                                 dtype=Path.code_type), n)
+        gc.set_clip_rectangle(c.clip)
+        r.draw_path(gc, Path(verts, codes), ident, BAR_COLOR)
+    gc.restore()
+    gl = r.new_gc()                                  # spines and ticks: 0.8 pt black, snapped
+    gl.set_linewidth(_LW)
+    gl.set_foreground('k')
+    gl.set_snap(True)
+    gl.set_capstyle('projecting')
+    gl.set_joinstyle('miter')
+    segs = [(L, B), (R, B), (L, T), (R, T), (L, B), (L, T), (R, B), (R, T)]
+    seg_codes = [Path.MOVETO, Path.LINETO] * 4
+    r.draw_path(gl, Path(segs, seg_codes), ident)
+    gl.set_capstyle('butt')
+    tick_v, label_boxes = [], []
+    size = 8 if kind == 'mini' else 10
+    locs, labels, inside, off = c.ticks(c.ax.xaxis, *xl)
+    for i in range(len(locs)):
+        if not inside[i]:
+            continue
+        px = L + (locs[i] - xl[0]) * sx
+        shown = kind != 'mini' or i == 0 or i == len(locs) - 1
+        # (the mini figure's hidden ticks keep their 10 pt labels' boxes,
+        # which place the offset text, as matplotlib's do)
+        box = _text(c, r, gl, labels[i], px, B - _TICK - _PAD, 'center', 'top', size if shown else 10,
+                    draw=shown and bool(labels[i]))
+        if labels[i]:
+            label_boxes.append(box)
+        if shown:
+            tick_v += [(px, B), (px, B - _TICK)]
+    if off:
+        bottom = min(b[1] for b in label_boxes) if label_boxes else B
+        _text(c, r, gl, off, R, bottom - _OFFPAD, 'right', 'top', 10)
+    if c.yaxis:
+        locs, labels, inside, off = c.ticks(c.ax.yaxis, *yl)
+        xmin = L - 0.5 * _LW * _PT                          # the left spine's outer edge
+        for i in range(len(locs)):
+            if not inside[i]:
+                continue
+            py = B + (locs[i] - yl[0]) * sy
+            tick_v += [(L, py), (L - _TICK, py)]
+            if labels[i]:
+                xmin = min(xmin, _text(c, r, gl, labels[i], L - _TICK - _PAD, py, 'right', 'center_baseline', 10)[0])
+        if off:
+            _text(c, r, gl, off, L, T + _OFFPAD, 'left', 'baseline', 10)
+        # 'Frequency': rotated 90 degrees, anchored (rotation_mode 'anchor',
+        # ha center, va bottom) labelpad left of the tick labels
+        w_, h_, d_ = c.extent(r, 'Frequency', 10)
+        ax_, ay_ = xmin - _LABELPAD, (B + T) / 2
+        r.draw_text(gl, ax_ - d_, c.H - (ay_ - w_ / 2), 'Frequency', c.fonts[10], 90)
+    if tick_v:
+        r.draw_path(gl, Path(tick_v, [Path.MOVETO, Path.LINETO] * (len(tick_v) // 2)), ident)
+    gl.restore()
+    return _png(np.asarray(r.buffer_rgba()))
+
+
+def _chunk(tag, data):
+    return struct.pack('>I', len(data)) + tag + data + struct.pack('>I', zlib.crc32(tag + data) & 0xFFFFFFFF)
+
+
+def _png(rgba):
+    """An opaque RGBA canvas as an 8-bit RGB PNG (filter 0, zlib level 1: the
+    images are mostly flat colour)."""
+    h, w = rgba.shape[:2]
+    raw = np.empty((h, 1 + 3 * w), dtype=np.uint8)
+    raw[:, 0] = 0
+    raw[:, 1:].reshape(h, w, 3)[...] = rgba[:, :, :3]
+    return (b'\x89PNG\r\n\x1a\n' + _chunk(b'IHDR', struct.pack('>IIBBBBB', w, h, 8, 2, 0, 0, 0)) +
+            _chunk(b'IDAT', zlib.compress(raw.tobytes(), 1)) + _chunk(b'IEND', b''))
+
+
+def _encode(png):
+    """base64 -> percent-quoted, as plot.py:35-37 stores it (quote() of base64
+    text only ever escapes '+' and '=': the alphabet is alphanumerics, '+', '/'
+    and '=', and '/' is quote's default safe character)."""
+    b64 = base64.b64encode(png).decode('ascii')
+    return BASE + b64.replace('+', '%2B').replace('=', '%3D')
 
 
 def _draw(kind, hist_data):
     left = np.asarray(hist_data['left_edge'], dtype=np.float64)
     height = np.asarray(hist_data['count'], dtype=np.float64)
-    w = _safe_width(hist_data['width'].iloc[0])
-    canvas, ax, bars = _figure(kind, len(left))
-    for r, x, h in zip(bars, left, height):
-        r.set_x(x)
-        r.set_width(w)
-        r.set_height(h)
-    x0, x1 = float(left.min()), float(left.max()) + w
-    y1 = float(height.max()) if height.size else 0.0
-    if np.isfinite(x0) and np.isfinite(x1) and x1 > x0 and np.isfinite(y1) and y1 > 0:
-        # the limits autoscale_view would set for these bars (axes.[xy]margin
-        # 0.05, bars sticky at y = 0), without relim's walk over every patch
-        mx = 0.05 * (x1 - x0)
-        ax.set_xlim(x0 - mx, x1 + mx)
-        ax.set_ylim(0.0, y1 + 0.05 * y1)
-    else:
-        ax.relim()
-        ax.autoscale_view()
-    if kind == 'mini':
-        # only the first and last x tick labels, in 8 pt (plot.py:27-36)
-        ticks = ax.xaxis.get_major_ticks()
-        for i, t in enumerate(ticks):
-            edge = i == 0 or i == len(ticks) - 1
-            t.set_visible(edge)
-            if edge:
-                t.label1.set_fontsize(8)
-    return _encode(canvas)
+    w = _safe_width(hist_data['width'].iloc[0]) if len(hist_data) else 1.0
+    return _encode(_render(kind, left, height, w))
 
 
 def mini_histogram(hist_data):
