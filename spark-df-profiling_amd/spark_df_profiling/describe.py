@@ -462,6 +462,7 @@ def describe(df, bins=10, corr_reject=0.9, **kwargs):
                         for i, pth in enumerate(paths) if pth == 'bits32' and known[i] is None}
         stats = engine.numeric_stats_batch(num_cols, packs, bins, [k_vals.get(c.name, 2) for c in num_cols],
                                            group_cols=group_cols, gk=gk, count32_cols=count32_cols)
+        to_plot = []
         for col, pack, st in zip(num_cols, packs, stats):
             bundles[col.name]['p1_pack'] = pack
             if st is not None:
@@ -469,7 +470,8 @@ def describe(df, bins=10, corr_reject=0.9, **kwargs):
                 # the histogram images render while the distinct counts run; a
                 # column that turns out CONST (one distinct value) is never NUM
                 if plots and st.error is None and owner[col.name] == rank and not _const_numeric(st):
-                    early_plots[col.name] = _submit_plot(st)
+                    to_plot.append((col.name, st))
+        early_plots.update(zip([name for name, _ in to_plot], _submit_plots([st for _, st in to_plot])))
         # every NUM column's countDistinct with shared readbacks (and, sharded,
         # shared collectives)
         # (date columns join the batch: their distinct hint is the day range)
@@ -613,11 +615,16 @@ def _describe_concurrent(engine, columns, one, workers):
 def _submit_plot(st):
     """describe.py:227-228 histogram + mini_histogram for one NUM column: a
     pool future, or the strings themselves when SDP_PLOT_WORKERS=0."""
+    return _submit_plots([st])[0]
+
+
+def _submit_plots(sts):
+    """_submit_plot of many columns, grouped into a few pool tasks."""
     from . import plot
     import os
     if os.environ.get('SDP_PLOT_WORKERS', '') == '0':
-        return plot.render_pair(st.hist_counts, st.edges, st.width)
-    return plot.submit(st.hist_counts, st.edges, st.width)
+        return [plot.render_pair(st.hist_counts, st.edges, st.width) for st in sts]
+    return plot.submit_batch([(st.hist_counts, st.edges, st.width) for st in sts])
 
 
 def corr_matrix(engine, table, columns, bundles):
