@@ -104,6 +104,11 @@ __device__ uint64_t hash_long_lds(const uint32_t *s, int64_t off, int64_t len) {
     return mix64(h);
 }
 __device__ bool rows_equal_global(const sdp_bytes_column &c, int64_t ra, int64_t rb) {
+    // row indices come from record metas: records that are not what the
+    // kernels were told (e.g. a layout mismatch between library and caller)
+    // must not turn into reads outside the column -- unequal, so the caller
+    // flags a collision and recounts on the exact path
+    if (ra < 0 || rb < 0 || ra >= c.length || rb >= c.length) return false;
     const int64_t a0 = str_off(c, ra), a1 = str_off(c, ra + 1);
     const int64_t b0 = str_off(c, rb), b1 = str_off(c, rb + 1);
     const int64_t len = a1 - a0;
@@ -2101,15 +2106,8 @@ int sdp_part_recs(const sdp_records *in, int32_t is_bytes, const sdp_chunk *d_ch
                                in->d_meta, ch, nchunks, b1, b2, d_offsets, o0, o1, o2, xcd_map_enabled());
     } else {
         if (phase == 0)
-        {
-            const char *e = getenv("SDP_COUNT_PAIRS");
-            if (e && e[0] == '0')
-                hipLaunchKernelGGL(part_count_recs_kernel<false>, dim3(grid), dim3(CT), 0, s, in->d_k0, nullptr,
-                                   nullptr, ch, nchunks, b1, b2, d_hist);
-            else
-                hipLaunchKernelGGL(part_count_recs_u64_kernel, dim3(grid), dim3(CT), 0, s, in->d_k0, ch, nchunks, b1,
-                                   b2, d_hist);
-        }
+            hipLaunchKernelGGL(part_count_recs_u64_kernel, dim3(grid), dim3(CT), 0, s, in->d_k0, ch, nchunks, b1, b2,
+                               d_hist);
         else
             hipLaunchKernelGGL(part_scatter_recs_kernel<false>, dim3(grid), dim3(ST), 0, s, in->d_k0, nullptr, nullptr,
                                ch, nchunks, b1, b2, d_offsets, o0, nullptr, nullptr, xcd_map_enabled());

@@ -30,6 +30,9 @@ for r in range(reps):
         e.numeric_pass1_batch([col])
     elif what == 'pass2':
         e.numeric_stats(col)
+    elif what == 'p2count':                  # the describe() path: pass 1, then pass 2 + level-1 count
+        packs = e.numeric_pass1_batch([col])
+        e.numeric_stats_batch([col], packs, 10, [2], group_cols={0})
     elif what == 'd32':                      # sdp_distinct32 (32-bit key spaces)
         lo = 0 if col.is_float else int(col.values[:rows].min().item())
         out = e._distinct32_launch(col, lo)
