@@ -26,7 +26,7 @@ constexpr int64_t ARENA_ALIGN = 256;
 constexpr int PART_SAMPLE = 16384;          // heavy-key sample rows (engine.PART_SAMPLE)
 constexpr int HEAVY_MIN = 3;                // sample occurrences that make a key heavy
 constexpr int HEAVY_N = 256;                // SDP heavy-key capacity (sdp_heavy.h HEAVY_MAX)
-constexpr int64_t PART_CHUNK = 65536;       // level-2 records per chunk (engine.PART_CHUNK)
+constexpr int64_t PART_CHUNK = 131072;      // level-2 records per chunk (engine.PART_CHUNK)
 constexpr int64_t GSORT_MAX = 8192;         // groups one sort_groups launch orders
 constexpr int64_t SMALL_BYTES = 64ll << 20; // headroom for tables, histograms, chunk lists
 

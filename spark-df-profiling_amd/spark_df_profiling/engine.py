@@ -48,7 +48,11 @@ EMPTY64 = 0xFFFFFFFFFFFFFFFF
 U64 = (1 << 64) - 1
 PART_SAMPLE = 16384          # rows sampled for heavy keys (sdp_part_sample)
 HEAVY_MIN = 3                # sample occurrences that make a key heavy
-PART_CHUNK = 65536           # level-2 records per workgroup chunk
+# level-2 records per workgroup chunk: each chunk pays its header and bucket
+# offsets before its first tile (131072 vs 65536: f64 level-2 scatter 4.4-4.7
+# -> 4.1-4.3 ms per 1e9 records; 262144 loses on skewed columns,
+# profiles/r04z_part_chunk_ab.log)
+PART_CHUNK = 131072
 # byte columns: strings read once into compacted records, then a record scatter
 # (SDP_BYTES_TWO_READS=1: the count + re-read scatter of round 1, for A/B runs)
 BYTES_ONE_READ = os.environ.get('SDP_BYTES_TWO_READS', '0') != '1'

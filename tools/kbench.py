@@ -33,6 +33,10 @@ for r in range(reps):
     elif what == 'p2count':                  # the describe() path: pass 1, then pass 2 + level-1 count
         packs = e.numeric_pass1_batch([col])
         e.numeric_stats_batch([col], packs, 10, [2], group_cols={0})
+    elif what == 'p2countb':                 # the same for every column of the column's dtype (batched launch)
+        same = [c for c in t.columns if c.kind == 'fixed' and c.dtype == col.dtype and c.spark_type != 'date']
+        packs = e.numeric_pass1_batch(same)
+        e.numeric_stats_batch(same, packs, 10, [2] * len(same), group_cols=set(range(len(same))))
     elif what == 'd32':                      # sdp_distinct32 (32-bit key spaces)
         lo = 0 if col.is_float else int(col.values[:rows].min().item())
         out = e._distinct32_launch(col, lo)
