@@ -867,22 +867,46 @@ __global__ void __launch_bounds__(ST) part_scatter_recs_kernel(const uint64_t *i
     const int64_t c0 = xm ? (int64_t)(blockIdx.x % 8) * per + blockIdx.x / 8 : (int64_t)blockIdx.x;
     const int64_t c1 = xm ? min(nchunks, (int64_t)(blockIdx.x % 8 + 1) * per) : nchunks;
     const int64_t cstep = xm ? gridDim.x / 8 : gridDim.x;
-    for (int64_t c = c0; c < c1; c += cstep) {
-        const Chunk ch = chunks[c];
-        for (int b = t; b < nb; b += ST) {
-            s.hist[b] = 0;
-            s.cur[b] = offs[ch.hbase + (int64_t)b * ch.hstride];
-        }
-        lds_barrier();
-        uint64_t k0[RPT], k1[RPT], meta[RPT];
+    // A chunk's bucket offsets and first tile are loaded while the previous
+    // chunk's last tile is sorted (nb <= ST: thread t owns sub-bucket t), so a
+    // chunk no longer starts with three dependent memory latencies (header,
+    // offsets, first tile) in front of an otherwise idle workgroup.
+    auto load_tile = [&](int64_t base, int64_t end, uint64_t (&a0)[RPT], uint64_t (&a1)[RPT],
+                         uint64_t (&am)[RPT]) {
 #pragma unroll
         for (int q = 0; q < RPT; ++q) {
-            const int64_t r = ch.start + (int64_t)q * ST + t;
-            if (r < ch.end) {
-                k0[q] = in_k0[r];
-                if (BYTES) { k1[q] = in_k1[r]; meta[q] = in_meta[r]; }
+            const int64_t r = base + (int64_t)q * ST + t;
+            if (r < end) {
+                a0[q] = in_k0[r];
+                if (BYTES) { a1[q] = in_k1[r]; am[q] = in_meta[r]; }
             }
         }
+    };
+    // chunk headers are wave-uniform: kept in scalar registers
+    auto uniform_chunk = [](const Chunk &x) {
+        auto u = [](int64_t v) {
+            const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v);
+            const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)((uint64_t)v >> 32));
+            return (int64_t)(((uint64_t)hi << 32) | lo);
+        };
+        return Chunk{u(x.start), u(x.end), u(x.hbase), u(x.hstride)};
+    };
+    uint64_t k0[RPT], k1[RPT], meta[RPT];
+    Chunk ch{0, 0, 0, 0};
+    uint64_t cur_next = 0;
+    if (c0 < c1) {
+        ch = uniform_chunk(chunks[c0]);
+        if (t < nb) cur_next = offs[ch.hbase + (int64_t)t * ch.hstride];
+        load_tile(ch.start, ch.end, k0, k1, meta);
+    }
+    for (int64_t c = c0; c < c1; c += cstep) {
+        if (t < nb) {
+            s.hist[t] = 0;
+            s.cur[t] = cur_next;
+        }
+        const int64_t cn = c + cstep;
+        const Chunk chn = cn < c1 ? uniform_chunk(chunks[cn]) : Chunk{0, 0, 0, 0};
+        lds_barrier();
         for (int64_t base = ch.start; base < ch.end; base += TILE) {
             uint32_t rank[RPT];
             int bk[RPT];
@@ -900,18 +924,12 @@ __global__ void __launch_bounds__(ST) part_scatter_recs_kernel(const uint64_t *i
                     rank[q] = atomicAdd(&s.hist[bk[q]], 1u);
                 }
             }
-            // next tile of this chunk in flight during the LDS work
+            // the next tile (of this chunk, or the next chunk's first with its
+            // bucket offsets) in flight during the LDS work
             const int64_t nbase = base + TILE;
-            if (nbase < ch.end) {
-#pragma unroll
-                for (int q = 0; q < RPT; ++q) {
-                    const int64_t r = nbase + (int64_t)q * ST + t;
-                    if (r < ch.end) {
-                        k0[q] = in_k0[r];
-                        if (BYTES) { k1[q] = in_k1[r]; meta[q] = in_meta[r]; }
-                    }
-                }
-            }
+            const bool last = nbase >= ch.end;                 // wave-uniform
+            if (last && cn < c1 && t < nb) cur_next = offs[chn.hbase + (int64_t)t * chn.hstride];
+            load_tile(last ? chn.start : nbase, last ? chn.end : ch.end, k0, k1, meta);
             lds_barrier();
             block_excl_scan<ST>(s.hist, s.off, nb, s.wsum);
 #pragma unroll
@@ -938,6 +956,11 @@ __global__ void __launch_bounds__(ST) part_scatter_recs_kernel(const uint64_t *i
             }
             lds_barrier();
         }
+        if (ch.start >= ch.end && cn < c1) {               // (an empty chunk prefetched nothing)
+            if (t < nb) cur_next = offs[chn.hbase + (int64_t)t * chn.hstride];
+            load_tile(chn.start, chn.end, k0, k1, meta);
+        }
+        ch = chn;
     }
 }
 

@@ -1,4 +1,6 @@
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"; mkdir -p gpurun_out; export TMPDIR=/tmp
-timeout -k 10 800 python -u -m pytest -m gpu -x -q --timeout 300 --timeout-method thread tests/test_gpu_grouping.py tests/test_gpu_parity.py tests/test_gpu_edges.py tests/test_gpu_c_abi.py tests/test_gpu_multirank.py tests/test_gpu_configs.py > gpurun_out/r04za_tests.log 2>&1; rc=$?
-tail -3 gpurun_out/r04za_tests.log; exit $rc
+# tree = HEAD + cross-chunk prefetch in the record scatter (sdp_part.hip only; the
+# engine and the record layout are HEAD's, so the HEAD library is a valid baseline)
+LIBS="head=build_ab/libsdp_head.so tree=spark-df-profiling_amd/spark_df_profiling/lib/libsdp.so" REPS=4 bash tools/gpu_ab.sh r04zc group f64_norm f64_uniform > /dev/null || exit 1
+grep -E "==|u64/scatter" gpurun_out/r04zc_ab.log
