@@ -495,6 +495,15 @@ class ReadbackCensus:
     def __init__(self):
         self.count = 0
         self._saved = []
+        # SDP_READBACK_SITES=1: also tally the package line each readback comes from
+        self.sites = {} if os.environ.get('SDP_READBACK_SITES') == '1' else None
+
+    def _site(self):
+        import traceback
+        for fr in reversed(traceback.extract_stack()[:-2]):
+            if 'spark_df_profiling' in fr.filename:
+                return '%s:%d %s' % (os.path.basename(fr.filename), fr.lineno, fr.name)
+        return '?'
 
     def _wrap(self, owner, name, pred):
         orig = getattr(owner, name)
@@ -503,6 +512,9 @@ class ReadbackCensus:
         def f(*a, **k):
             if pred(*a, **k):
                 census.count += 1
+                if census.sites is not None:
+                    key = census._site()
+                    census.sites[key] = census.sites.get(key, 0) + 1
             return orig(*a, **k)
         self._saved.append((owner, name, orig))
         setattr(owner, name, f)
@@ -610,6 +622,9 @@ def main():
             with ReadbackCensus() as census:
                 step()
             readbacks = census.count
+            if census.sites is not None and rank == 0:
+                for k, v in sorted(census.sites.items(), key=lambda kv: -kv[1]):
+                    print('readback site %3d  %s' % (v, k), file=sys.stderr)
         else:
             step()
 

@@ -481,7 +481,7 @@ def describe(df, bins=10, corr_reject=0.9, **kwargs):
         dbounds = bounds + [(p1['imin'], p1['imax']) if p1['count'] else None for p1 in date_p1]
         dknown = known + [None] * len(date_cols)
         dist = engine.distinct_batch(dcols, dhints, dbounds, dknown) if not sharded else \
-            engine.distinct_batch_sharded(dcols, dhints, dbounds, dknown)
+            engine.distinct_batch_sharded(dcols, dhints, dbounds, dknown, n_all=n)
         for col, d in zip(dcols, dist):
             bundles[col.name]['distinct_pre'] = d
         # every string/binary/decimal column's value counts with shared

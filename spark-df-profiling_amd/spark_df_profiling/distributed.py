@@ -194,6 +194,20 @@ def merge_topk(comm, pairs, k):
     return merged[:k]
 
 
+def merge_topk_batch(comm, pairs_list, k):
+    """merge_topk of several columns with ONE all-gather (each all_gather_object
+    is two host round trips)."""
+    if not comm.sharded:
+        return [pairs[:k] for pairs in pairs_list]
+    allp = comm.allgather_object(list(pairs_list))
+    out = []
+    for j in range(len(pairs_list)):
+        merged = [p for part in allp for p in part[j]]
+        merged.sort(key=lambda vc: (-vc[1], _sortable(vc[0])))
+        out.append(merged[:k])
+    return out
+
+
 def _sortable(v):
     if isinstance(v, (bytes, bytearray)):
         return bytes(v)

@@ -1754,7 +1754,7 @@ class Engine:
         """group_sharded_batch of one column."""
         return self.group_sharded_batch([col])[0]
 
-    def group_sharded_batch(self, cols):
+    def group_sharded_batch(self, cols, n_all=None):
         """countDistinct (describe.py:143) of fixed-width columns of a
         row-sharded table, on the partitioning kernels: level-1 buckets (top
         B1 hash bits) are owned by contiguous rank ranges, so after the local
@@ -1775,8 +1775,9 @@ class Engine:
         s = self._s()
         B1 = self.SHARDED_B1
         nb1 = 1 << B1
-        n_all = int(comm.allreduce_sum(torch.tensor([cols[0].length], dtype=torch.int64,
-                                                     device=self.device)).item())
+        if n_all is None:                                 # (the caller usually knows the table's rows)
+            n_all = int(comm.allreduce_sum(torch.tensor([cols[0].length], dtype=torch.int64,
+                                                         device=self.device)).item())
         target = sdp.sdp_part_bucket_target(0, 0)
         b2 = min(10, max(1, math.ceil(math.log2(max(2.0, n_all / nb1 / target)))))
         nb2 = 1 << b2
@@ -1935,14 +1936,15 @@ class Engine:
                 out.append('group')
         return out
 
-    def distinct_batch_sharded(self, cols, hints, bounds, known=None):
+    def distinct_batch_sharded(self, cols, hints, bounds, known=None, n_all=None):
         """distinct_batch on a row-sharded table (every rank calls it with the
         same columns; hints/bounds come from the merged pass 1): bitmaps for
         small integral ranges, the global-table exchange for small key ranges,
         group_sharded_batch for the rest (shared round trips)."""
         comm = self.comm
-        n_all = int(comm.allreduce_sum(torch.tensor([cols[0].length if cols else 0], dtype=torch.int64,
-                                                    device=self.device)).item()) if cols else 0
+        if n_all is None:                                 # (describe() passes the table's global rows)
+            n_all = int(comm.allreduce_sum(torch.tensor([cols[0].length if cols else 0], dtype=torch.int64,
+                                                        device=self.device)).item()) if cols else 0
         out = list(known) if known is not None else [None] * len(cols)     # sorted columns: counted
         grp = []
         for i, (col, pth) in enumerate(zip(cols, self.distinct_paths_sharded(cols, hints, bounds, n_all))):
@@ -1955,7 +1957,7 @@ class Engine:
                 out[i] = self._distinct_fixed_table(col, False, hints[i])['groups']
             else:
                 grp.append(i)
-        for i, tab in zip(grp, self.group_sharded_batch([cols[i] for i in grp])):
+        for i, tab in zip(grp, self.group_sharded_batch([cols[i] for i in grp], n_all=n_all)):
             out[i] = tab['groups'] if tab is not None else \
                 self._distinct_fixed_table(cols[i], False, hints[i])['groups']
         return out
@@ -2316,12 +2318,9 @@ class Engine:
                 values[j] = self.group_values(tab, slots, col)
         for (j, _, _, _), vals in zip(byte_req, self.row_bytes_values_batch([r[1:] for r in byte_req])):
             values[j] = vals
-        from .distributed import merge_topk
-        out = []
-        for (tab, col), top, vals in zip(items, tops, values):
-            pairs = [(v, int(c)) for v, (_, c) in zip(vals, top)]
-            out.append(merge_topk(self.comm, pairs, k))
-        return out
+        from .distributed import merge_topk_batch
+        return merge_topk_batch(self.comm, [[(v, int(c)) for v, (_, c) in zip(vals, top)]
+                                            for top, vals in zip(tops, values)], k)
 
     def _smallest_keys_among(self, sel_pack, r, tab, sort_take):
         """The r groups with the smallest keys among a large set of equal counts."""
