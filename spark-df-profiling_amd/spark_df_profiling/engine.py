@@ -771,10 +771,13 @@ class Engine:
                 off += hb
             return result
         # sharded: counts and bins summed exactly; abs-dev partials gathered, summed in rank order
-        parts = [torch.cat([res[:rsz].view(torch.int64)[1:4], hist]) for res, hist, _, _ in outs]
-        summed = self.comm.allreduce_sum(torch.cat(parts)).cpu().numpy()
+        # (one all-gather and one readback: the int64 counts are summed over
+        # ranks on the host, exactly, the fp64 partials in rank order)
+        parts = torch.cat([torch.cat([res[:rsz].view(torch.int64)[1:4], hist]) for res, hist, _, _ in outs])
         mads = torch.stack([res[:8].view(torch.float64)[0] for res, _, _, _ in outs])
-        allm = torch.stack(self.comm.allgather(mads)).cpu().numpy()        # [world, ncols]
+        allp = torch.stack(self.comm.allgather(torch.cat([parts, mads.view(torch.int64)]))).cpu().numpy()
+        summed = allp[:, :parts.numel()].sum(axis=0)
+        allm = np.ascontiguousarray(allp[:, parts.numel():]).view(np.float64)   # [world, ncols]
         result, off = [], 0
         for i, (res, hist, _, _) in enumerate(outs):
             v = summed[off:off + 3 + hist.numel()]
@@ -1795,10 +1798,12 @@ class Engine:
             ctx['o1'] = self._scan(ctx.pop('h1'))
             ctx['bsn_dev'] = torch.cat([ctx['o1'][0:nb1 * grid:grid], ctx['o1'][-1:]])
             ctxs.append(ctx)
-        flat = torch.cat([c['bsn_dev'] for c in ctxs]).cpu().numpy().astype(np.int64)
-        bss = [flat[i * (nb1 + 1):(i + 1) * (nb1 + 1)] for i in range(len(ctxs))]
-        sizes = torch.from_numpy(np.stack([np.diff(bs) for bs in bss]).reshape(-1)).to(self.device)
-        all_sizes = torch.stack(comm.allgather(sizes)).cpu().numpy().reshape(world, len(ctxs), nb1)
+        # every rank's level-1 bucket sizes in one all-gather and ONE readback
+        # (the local bucket starts are the prefix sums of this rank's row; the
+        # exclusive scan starts at 0)
+        sizes = torch.cat([c['bsn_dev'][1:] - c['bsn_dev'][:-1] for c in ctxs])
+        all_sizes = torch.stack(comm.allgather(sizes)).cpu().numpy().astype(np.int64).reshape(world, len(ctxs), nb1)
+        bss = [np.concatenate([[0], np.cumsum(all_sizes[rank, i])]).astype(np.int64) for i in range(len(ctxs))]
         my0, my1 = lo[rank], lo[rank + 1]
         nmy = my1 - my0
 
@@ -1946,13 +1951,13 @@ class Engine:
             n_all = int(comm.allreduce_sum(torch.tensor([cols[0].length if cols else 0], dtype=torch.int64,
                                                         device=self.device)).item()) if cols else 0
         out = list(known) if known is not None else [None] * len(cols)     # sorted columns: counted
-        grp = []
+        grp, bitmaps = [], []
         for i, (col, pth) in enumerate(zip(cols, self.distinct_paths_sharded(cols, hints, bounds, n_all))):
             bd = bounds[i]
             if out[i] is not None:
                 continue
             if pth == 'bitmap':
-                out[i] = self.distinct_bitmap(col, bd[0], bd[1] - bd[0] + 1)
+                bitmaps.append((i, self._distinct_bitmap_dev(col, bd[0], bd[1] - bd[0] + 1)))
             elif pth == 'table':
                 out[i] = self._distinct_fixed_table(col, False, hints[i])['groups']
             else:
@@ -1960,6 +1965,9 @@ class Engine:
         for i, tab in zip(grp, self.group_sharded_batch([cols[i] for i in grp], n_all=n_all)):
             out[i] = tab['groups'] if tab is not None else \
                 self._distinct_fixed_table(cols[i], False, hints[i])['groups']
+        if bitmaps:                                       # every bitmap count in one readback
+            for (i, _), v in zip(bitmaps, self._host_u64(torch.cat([d for _, d in bitmaps]))):
+                out[i] = v
         return out
 
     def _scan(self, counts_i32):
@@ -1987,12 +1995,16 @@ class Engine:
         """countDistinct (describe.py:143) of an integral column whose values lie
         in [lo, lo + range_), range_ <= 2^20: LDS bitmaps (sdp_bitmap.hip).  Ranks
         all-gather their OR-ed bitmaps and re-reduce them."""
+        return int(self._distinct_bitmap_dev(col, lo, range_).item())
+
+    def _distinct_bitmap_dev(self, col, lo, range_):
+        """distinct_bitmap's count as a one-element device tensor (no readback)."""
         out, bm, nw = self._distinct_bitmap_launch(col, lo, range_, keep_bitmap=True)
         if self.comm.sharded:
             allb = torch.cat(self.comm.allgather(bm))
             out.zero_()
             sdp.sdp_bitmap_reduce(ptr(allb), self.comm.world, nw, None, ptr(out), self._s())
-        return int(out.item())
+        return out
 
     def distinct_fixed(self, col, with_counts=False, capacity_hint=None):
         """countDistinct over a fixed-width column (describe.py:143).
