@@ -683,17 +683,19 @@ struct Chunk {
 // part_scatter_recs_kernel<true> (b1 = 0, b2 = level-1 bits) then moves the
 // records -- 24 B each, sequential reads -- into their buckets.  Heavy keys are
 // counted in LDS and never become records, as in the other row kernels.
-constexpr int BR_T = 256;                   // 4 waves, one strip each (<= 128 VGPRs: the
-                                            // 1024-block grid is resident in one round)
+constexpr int BR_T = 1024;                  // 16 waves, one strip each, one workgroup per CU
+                                            // (<= 128 VGPRs; the 256-block grid is resident in
+                                            // one round) -- the LDS holds 1024 heavy keys
 constexpr int BR_W = BR_T / WAVE;
 constexpr int BR_RPT = 4;                   // rows per lane per tile
 
 struct BRecLds {
-    HeavyLdsT<true> heavy;
+    HeavyLdsT<true, HEAVY_MAX_REC> heavy;
     uint32_t hist[BR_W][MAXB];
 };
+static_assert(sizeof(BRecLds) <= 120 * 1024, "records kernel LDS");
 
-constexpr int BR_MINB = 4;
+constexpr int BR_MINB = 1;
 template <int OW>
 __global__ void __launch_bounds__(BR_T, BR_MINB) part_records_rows_bytes_kernel(sdp_bytes_column col, HeavyArg heavy, int b1,
                                                                        int64_t rows_per_block, uint32_t *hist,
@@ -2090,8 +2092,8 @@ int sdp_part_rows_records(const sdp_bytes_column *bcol, const sdp_heavy *heavy, 
     if (bcol->length >= (int64_t)RMASK40) return set_error(SDP_EINVAL, "part_rows_records: more than 2^40 rows");
     HeavyArg hv{nullptr, nullptr, nullptr, nullptr, 0};
     if (heavy && heavy->n > 0) {
-        if (heavy->n > HEAVY_MAX)
-            return set_error(SDP_EINVAL, "part_rows_records: %d heavy keys > %d", heavy->n, HEAVY_MAX);
+        if (heavy->n > HEAVY_MAX_REC)
+            return set_error(SDP_EINVAL, "part_rows_records: %d heavy keys > %d", heavy->n, HEAVY_MAX_REC);
         hv = HeavyArg{heavy->d_h, heavy->d_k0, heavy->d_k1, heavy->d_meta, heavy->n};
         if (hv.k0 == nullptr || hv.k1 == nullptr || hv.meta == nullptr || d_heavy_counts == nullptr)
             return set_error(SDP_EINVAL, "part_rows_records: byte heavy keys need k0/k1/meta and counts");

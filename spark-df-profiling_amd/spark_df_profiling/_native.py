@@ -24,6 +24,7 @@ MAX_WINDOWS = 5
 PASS1_WAVES = 4          # SDP_PASS1_WAVES
 PART_MAX_GRID = 1024     # SDP_PART_MAX_GRID
 HEAVY_MAX = 256
+HEAVY_MAX_REC = 1024         # byte keys on the records kernel (sdp_heavy.h HEAVY_MAX_REC)
 BITMAP_MAX_BITS = 1 << 20        # SDP_BITMAP_MAX_BITS
 
 # enum sdp_dtype

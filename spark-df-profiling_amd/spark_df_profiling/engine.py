@@ -47,6 +47,9 @@ TOPK = 50                                       # describe.py:259
 EMPTY64 = 0xFFFFFFFFFFFFFFFF
 U64 = (1 << 64) - 1
 PART_SAMPLE = 16384          # rows sampled for heavy keys (sdp_part_sample)
+# byte columns: up to HEAVY_MAX_REC heavy keys need a larger sample to be seen
+# HEAVY_MIN times (zipf(1.1) over 1e8 labels: the 1024th key holds ~6e-5 of the rows)
+PART_SAMPLE_BYTES = 65536
 HEAVY_MIN = 3                # sample occurrences that make a key heavy
 # level-2 records per workgroup chunk: each chunk pays its header and bucket
 # offsets before its first tile (131072 vs 65536: f64 level-2 scatter 4.4-4.7
@@ -1194,7 +1197,7 @@ class Engine:
 
     def _heavy_sample_launch(self, col, isb, gather=False):
         """Queue the heavy-key sample of `col` (no readback)."""
-        ns = min(PART_SAMPLE, max(col.length, 1))
+        ns = min(PART_SAMPLE_BYTES if isb else PART_SAMPLE, max(col.length, 1))
         if gather and self.comm.sharded:
             ns = max(1, min(PART_SAMPLE // self.comm.world, col.length))   # pooled: PART_SAMPLE in all
         s = self._s()
@@ -1245,6 +1248,7 @@ class Engine:
         hv = self._heavy_struct(u, cnt, first, pos, keep, isb, meta)
         if hv is not None:        # sampled share of rows that become partition records
             hv['rec_frac'] = (n_valid - hv['heavy_rows']) / float(len(hn))
+            hv['ns'] = len(hn)
         return hv
 
     def _heavy_struct(self, u, cnt, first=None, pos=None, keep=None, isb=False, meta=None):
@@ -1255,10 +1259,14 @@ class Engine:
         sel = np.nonzero(cnt >= HEAVY_MIN)[0]
         if sel.size == 0:
             return None
-        if sel.size > nat.HEAVY_MAX:
-            sel = sel[np.argsort(-cnt[sel], kind='stable')[:nat.HEAVY_MAX]]
+        # at most HEAVY_MAX keys (HEAVY_MAX_REC for byte keys: the records kernel
+        # holds them; the other byte kernels take the first HEAVY_MAX, _hv_cap),
+        # the most frequent first
+        cap = nat.HEAVY_MAX_REC if isb else nat.HEAVY_MAX
+        sel = sel[np.argsort(-cnt[sel], kind='stable')[:cap]]
         hv = {'h': self._h2d(u[sel].view(np.int64).copy()), 'n': int(sel.size),
-              'h_host': [int(x) for x in u[sel].tolist()], 'heavy_rows': int(cnt[sel].sum())}
+              'h_host': [int(x) for x in u[sel].tolist()], 'heavy_rows': int(cnt[sel].sum()),
+              'cnt_host': [int(x) for x in cnt[sel].tolist()]}
         if isb:
             rows = pos[first[sel]]
             hv['meta_host'] = [int(x) for x in meta[rows].tolist()]
@@ -1344,26 +1352,34 @@ class Engine:
         target = sdp.sdp_part_bucket_target(int(isb), int(with_counts))
         if hv is Engine._NO_HV:
             hv = self._heavy_keys(col, isb)
-        n_rec = n
-        if isb and hv is not None and 'rec_frac' in hv:
-            # byte columns: size the buckets for the records the sample predicts
-            # (heavy keys never become records), with margin; fewer hash bits
-            # mean longer runs per bucket in both scatters
-            n_rec = min(n, int(n * (1.25 * hv['rec_frac'] + 0.02)) + 1)
-        total_bits = max(0, math.ceil(math.log2(max(1.0, n_rec / target))))
+        if isb and not BYTES_ONE_READ:
+            hv = self._hv_cap(hv, nat.HEAVY_MAX)       # the row kernels' LDS tables hold fewer
+        while True:
+            n_rec = n
+            if isb and hv is not None and 'rec_frac' in hv:
+                # byte columns: size the buckets for the records the sample predicts
+                # (heavy keys never become records), with margin; fewer hash bits
+                # mean longer runs per bucket in both scatters
+                n_rec = min(n, int(n * (1.25 * hv['rec_frac'] + 0.02)) + 1)
+            total_bits = max(0, math.ceil(math.log2(max(1.0, n_rec / target))))
+            b1 = min(10, (total_bits + 1) // 2)
+            one_read = isb and BYTES_ONE_READ and b1 > 0
+            if not isb or one_read or hv is None or hv['n'] <= nat.HEAVY_MAX:
+                break
+            hv = self._hv_cap(hv, nat.HEAVY_MAX)       # b1 == 0: the row kernels take the bytes
         large = False
         if total_bits > 20 and not isb and not with_counts:
             # > 2^30 rows: 4x larger final buckets on the workgroup-table kernel
             total_bits = max(20, math.ceil(math.log2(max(1.0, n / (4 * target)))))
             large = True
-        b1 = min(10, (total_bits + 1) // 2)
+            b1 = min(10, (total_bits + 1) // 2)
         b2 = total_bits - b1
         if b2 > 10:
             return None
         nb1, nb2 = 1 << b1, 1 << b2
         rpb = sdp.sdp_part_rows_per_block(n, int(isb))
         grid = max(1, -(-n // rpb))
-        if isb and BYTES_ONE_READ and b1 > 0:
+        if one_read:
             grid = sdp.sdp_part_records_chunks(n)           # one level-1 histogram per wave strip
         return {'col': col, 'isb': isb, 'with_counts': with_counts, 'large': large, 'b1': b1, 'b2': b2,
                 'nb1': nb1, 'nb2': nb2, 'stats': self._u64(68, zero=True), 'cs': None if isb else col.sdp(),
@@ -1371,7 +1387,28 @@ class Engine:
                 'hcnt': self._u64(max(hv['n'] if hv else 1, 1), zero=True), 'grid': grid,
                 'h1': torch.empty(nb1 * grid, dtype=torch.int32, device=self.device),
                 'rb': col_read_bytes(col), 'recw': 24 if isb else 8,
-                'one_read': isb and BYTES_ONE_READ and b1 > 0}
+                'one_read': one_read}
+
+    @staticmethod
+    def _hv_cap(hv, cap):
+        """The first `cap` heavy keys of hv (the most frequent: _heavy_struct
+        orders them by sample count).  Rows of the dropped keys simply become
+        partition records; the groups come out the same."""
+        if hv is None or hv['n'] <= cap:
+            return hv
+        out = dict(hv)
+        out['n'] = cap
+        out['h_host'] = hv['h_host'][:cap]
+        if 'meta_host' in hv:
+            out['meta_host'] = hv['meta_host'][:cap]
+        if 'cnt_host' in hv:
+            out['cnt_host'] = hv['cnt_host'][:cap]
+            out['heavy_rows'] = int(sum(out['cnt_host']))
+            if 'rec_frac' in hv:
+                out['rec_frac'] = hv['rec_frac'] + (hv['heavy_rows'] - out['heavy_rows']) / float(hv['ns'])
+        st = hv['struct']
+        out['struct'] = nat.SdpHeavy(st.d_h, st.d_k0, st.d_k1, st.d_meta, cap, 0)
+        return out
 
     def _group_count(self, ctx):
         """Level-1 bucket counts (sdp_part_rows phase 0).  Byte columns

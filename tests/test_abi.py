@@ -93,13 +93,13 @@ def test_part_argument_checks_without_gpu():
     assert _native.sdp.sdp_part_bucket_target(1, 1) == 2048
     with pytest.raises(_native.NativeError, match='part_rows_records'):
         _native.sdp.sdp_part_rows_records(None, None, 4, None, None, None, None, None, None)
-    # one chunk per wave strip: 4 per workgroup of the records grid (whole
-    # 4 K-row tiles, at most SDP_PART_MAX_GRID workgroups)
+    # one chunk per wave strip: 16 per workgroup of the records grid (whole
+    # 4 K-row tiles, one workgroup per CU: at most 256 workgroups)
     n = 10 ** 9
     rpb = _native.sdp.sdp_part_rows_per_block(n, 1)
     ch = _native.sdp.sdp_part_records_chunks(n)
-    assert ch % 4 == 0 and 4 <= ch <= 4 * 1024 and (ch // 4) * 4096 * (-(-n // 4096 // (ch // 4))) >= n
-    assert _native.sdp.sdp_part_records_chunks(0) == 4 and _native.sdp.sdp_part_records_chunks(5000) == 8
+    assert ch % 16 == 0 and 16 <= ch <= 16 * 256 and (ch // 16) * 4096 * (-(-n // 4096 // (ch // 16))) >= n
+    assert _native.sdp.sdp_part_records_chunks(0) == 16 and _native.sdp.sdp_part_records_chunks(5000) == 32
     assert rpb % 1024 == 0
 
 
