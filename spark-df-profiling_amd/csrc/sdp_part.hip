@@ -293,6 +293,105 @@ __global__ void __launch_bounds__(CT) part_count_rows_u64_kernel(sdp_column col,
     block_add_u64(special, &stats[1]);
 }
 
+// ---- write-combined bucket output ------------------------------------------------
+// A scatter appends each bucket's records at that bucket's cursor.  Written
+// straight from a tile sorted in LDS, a bucket's run per 16 K-record tile (~16
+// records) starts and ends inside 128-byte lines, and the two half-filled lines
+// of every run reach HBM separately: 6.1 ms per 1e9 records against 3.8 ms when
+// every write is one whole aligned line (1024 streams per workgroup, 256
+// workgroups; tools/ubench/scatter_bench.hip, profiles/r04sb_scatter_bench.txt).
+// So each bucket's current line is assembled in LDS and leaves whole once it
+// fills; lines a tile fills entirely go out directly (their records are written
+// together, the L2 merges them), and only a segment's first and last lines are
+// written in part.  Used by the level-2 scatter of fixed keys (f64_norm 1e9
+// records: 4.1-4.7 -> 3.1-3.2 ms); the row scatter gained nothing from it (its
+// time is not in the write stream), byte records (24 bytes) would need 384 KB.
+constexpr int WC_LINE = 16;                     // 8-byte records per 128-byte line
+struct WcLds {
+    uint64_t line[MAXB][WC_LINE];               // bucket b's current line (slots lo[b] .. cur[b] % 16 filled)
+    uint64_t cur[MAXB];                         // bucket b's next output position
+    uint32_t cnt[MAXB];                         // this tile's records of bucket b
+    uint16_t list[MAXB];                        // buckets whose current line this tile completes
+    uint8_t lo[MAXB];                           // first slot of the current line that is this segment's
+    uint32_t nlist;
+};
+// (owner thread of bucket b) the records of the current line not yet written
+__device__ __forceinline__ void wc_flush_partial(WcLds &s, int b, uint64_t *out) {
+    const uint64_t c = s.cur[b];
+    const uint64_t base = c & ~(uint64_t)(WC_LINE - 1);
+    const int e = (int)(c & (WC_LINE - 1));
+    for (int j = s.lo[b]; j < e; ++j) out[base + j] = s.line[b][j];
+}
+__device__ __forceinline__ void wc_start(WcLds &s, int b, uint64_t pos) {
+    s.cur[b] = pos;
+    s.lo[b] = (uint8_t)(pos & (WC_LINE - 1));
+    s.cnt[b] = 0;
+}
+// (owner) continue bucket b at pos: a jump flushes the partial line first
+__device__ __forceinline__ void wc_seek(WcLds &s, int b, uint64_t pos, uint64_t *out) {
+    if (pos != s.cur[b]) {
+        wc_flush_partial(s, b, out);
+        wc_start(s, b, pos);
+    }
+}
+// One tile: record q of this thread (bit q of `have`) goes to bucket
+// (h[q] >> shift) & (nb - 1).  Every thread of the workgroup calls it.
+template <int NT, int RPT>
+__device__ __forceinline__ void wc_tile(WcLds &s, const uint64_t (&h)[RPT], uint32_t have, int shift, int nb,
+                                        uint64_t *out) {
+    const int t = threadIdx.x;
+    const uint64_t mask = (uint64_t)(nb - 1);
+    static_assert(NT * RPT <= 65536, "ranks are packed 16 bits per record");
+    uint32_t r[(RPT + 1) / 2] = {};             // rank of record q in its bucket: 16 bits each
+#pragma unroll
+    for (int q = 0; q < RPT; ++q)
+        if ((have >> q) & 1u) r[q / 2] |= atomicAdd(&s.cnt[(int)((h[q] >> shift) & mask)], 1u) << (16 * (q & 1));
+    lds_barrier();
+    // records of the current line into LDS, of lines this tile fills entirely
+    // straight out, of the new partial line held until the current one is out
+    static_assert(RPT <= 16, "pending slots are packed 4 bits per record");
+    uint32_t pend = 0;
+    uint64_t slots = 0;                         // slot of pending record q: bits 4q .. 4q+3
+#pragma unroll
+    for (int q = 0; q < RPT; ++q) {
+        if ((have >> q) & 1u) {
+            const int b = (int)((h[q] >> shift) & mask);
+            const uint64_t c = s.cur[b];
+            const uint64_t p = c + ((r[q / 2] >> (16 * (q & 1))) & 0xFFFFu), e = c + s.cnt[b];
+            if ((p >> 4) == (c >> 4)) s.line[b][p & (WC_LINE - 1)] = h[q];
+            else if ((p >> 4) != (e >> 4)) out[p] = h[q];
+            else {
+                pend |= 1u << q;
+                slots |= (p & (WC_LINE - 1)) << (4 * q);
+            }
+        }
+    }
+    for (int b = t; b < nb; b += NT) {
+        const uint64_t c = s.cur[b];
+        if (((c + s.cnt[b]) >> 4) != (c >> 4)) s.list[atomicAdd(&s.nlist, 1u)] = (uint16_t)b;
+    }
+    lds_barrier();
+    // completed lines: 16 lanes per line, one aligned 128-byte write
+    const uint32_t nl = s.nlist;
+    for (uint32_t i = t / WC_LINE; i < nl; i += NT / WC_LINE) {
+        const int b = s.list[i], l = t & (WC_LINE - 1);
+        if (l >= s.lo[b]) out[(s.cur[b] & ~(uint64_t)(WC_LINE - 1)) + l] = s.line[b][l];
+    }
+    lds_barrier();
+#pragma unroll
+    for (int q = 0; q < RPT; ++q)
+        if ((pend >> q) & 1u) s.line[(int)((h[q] >> shift) & mask)][(slots >> (4 * q)) & 15] = h[q];
+    for (int b = t; b < nb; b += NT) {
+        const uint64_t c = s.cur[b], e = c + s.cnt[b];
+        if ((e >> 4) != (c >> 4)) s.lo[b] = 0;
+        s.cur[b] = e;
+        s.cnt[b] = 0;
+    }
+    if (t == 0) s.nlist = 0;
+    lds_barrier();
+}
+
+constexpr int WC_RPT = 8;                       // records per thread per tile (16 spills registers, no faster)
 // block bx of a G-block grid (the batched launch runs several columns' grids
 // side by side, blockIdx.y = column)
 template <typename T>
@@ -964,6 +1063,78 @@ __global__ void __launch_bounds__(ST) part_scatter_recs_kernel(const uint64_t *i
         }
         ch = chn;
     }
+}
+
+// Write-combined level-2 scatter of fixed-key records (WcLds): workgroup g
+// takes one contiguous range of chunks, so consecutive chunks of one level-1
+// bucket continue every sub-bucket's cursor (the chunk-major order of the
+// level-2 offsets), and a sub-bucket's partial line is flushed only where the
+// next chunk's offset jumps.
+__global__ void __launch_bounds__(ST) part_scatter_recs_wc_kernel(const uint64_t *in_k0, const Chunk *chunks,
+                                                                  int64_t nchunks, int b1, int b2,
+                                                                  const uint64_t *offs, uint64_t *out_k0,
+                                                                  int xcd_map) {
+    constexpr int RPT = WC_RPT;
+    constexpr int TILE = ST * RPT;
+    __shared__ WcLds s;
+    const int t = threadIdx.x;
+    const int nb = 1 << b2;
+    const int shift = 64 - b1 - b2;
+    const int G = gridDim.x, bx = blockIdx.x;
+    const int g = (xcd_map && G % 8 == 0) ? (int)((bx % 8) * (G / 8) + bx / 8) : bx;
+    const int64_t c0 = nchunks * g / G, c1 = nchunks * (g + 1) / G;
+    auto load_tile = [&](int64_t base, int64_t end, uint64_t (&a)[RPT]) {
+#pragma unroll
+        for (int q = 0; q < RPT; ++q) {
+            const int64_t r = base + (int64_t)q * ST + t;
+            if (r < end) a[q] = in_k0[r];
+        }
+    };
+    auto uniform_chunk = [](const Chunk &x) {
+        auto u = [](int64_t v) {
+            const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v);
+            const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)((uint64_t)v >> 32));
+            return (int64_t)(((uint64_t)hi << 32) | lo);
+        };
+        return Chunk{u(x.start), u(x.end), u(x.hbase), u(x.hstride)};
+    };
+    if (c0 >= c1) return;                       // (workgroup-uniform: no barrier is skipped by a part)
+    uint64_t k0[RPT];
+    Chunk ch = uniform_chunk(chunks[c0]);
+    uint64_t pos = t < nb ? offs[ch.hbase + (int64_t)t * ch.hstride] : 0;
+    load_tile(ch.start, ch.end, k0);
+    if (t < nb) wc_start(s, t, pos);
+    if (t == 0) s.nlist = 0;
+    for (int64_t c = c0; c < c1; ++c) {
+        if (c > c0 && t < nb) wc_seek(s, t, pos, out_k0);
+        const int64_t cn = c + 1;
+        const Chunk chn = cn < c1 ? uniform_chunk(chunks[cn]) : Chunk{0, 0, 0, 0};
+        lds_barrier();
+        for (int64_t base = ch.start; base < ch.end; base += TILE) {
+            uint64_t x[RPT];
+            uint32_t have = 0;
+#pragma unroll
+            for (int q = 0; q < RPT; ++q) {
+                x[q] = k0[q];
+                if (base + (int64_t)q * ST + t < ch.end) have |= 1u << q;
+            }
+            const int64_t nbase = base + TILE;
+            const bool last = nbase >= ch.end;                 // wave-uniform
+            // the next tile (of this chunk, or the next chunk's first with its offsets) in flight
+            auto next = [&] {
+                if (last && cn < c1 && t < nb) pos = offs[chn.hbase + (int64_t)t * chn.hstride];
+                load_tile(last ? chn.start : nbase, last ? chn.end : ch.end, k0);
+            };
+            next();             // (issued before the placement: 3.10 vs 3.21-3.38 ms per 1e9 records after it)
+            wc_tile<ST, RPT>(s, x, have, shift, nb, out_k0);
+        }
+        if (ch.start >= ch.end && cn < c1) {                   // (an empty chunk prefetched nothing)
+            if (t < nb) pos = offs[chn.hbase + (int64_t)t * chn.hstride];
+            load_tile(chn.start, chn.end, k0);
+        }
+        ch = chn;
+    }
+    if (t < nb) wc_flush_partial(s, t, out_k0);
 }
 
 // ---- final buckets: LDS grouping -------------------------------------------------
@@ -2133,9 +2304,9 @@ int sdp_part_recs(const sdp_records *in, int32_t is_bytes, const sdp_chunk *d_ch
         if (phase == 0)
             hipLaunchKernelGGL(part_count_recs_u64_kernel, dim3(grid), dim3(CT), 0, s, in->d_k0, ch, nchunks, b1, b2,
                                d_hist);
-        else
-            hipLaunchKernelGGL(part_scatter_recs_kernel<false>, dim3(grid), dim3(ST), 0, s, in->d_k0, nullptr, nullptr,
-                               ch, nchunks, b1, b2, d_offsets, o0, nullptr, nullptr, xcd_map_enabled());
+        else                             // one resident workgroup per CU, a contiguous range of chunks each
+            hipLaunchKernelGGL(part_scatter_recs_wc_kernel, dim3(grid_of(nchunks, 256)), dim3(ST), 0, s, in->d_k0,
+                               ch, nchunks, b1, b2, d_offsets, o0, xcd_map_enabled());
     }
     return check_launch("part_recs_kernel");
 }
