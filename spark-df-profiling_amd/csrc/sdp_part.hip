@@ -303,49 +303,59 @@ __global__ void __launch_bounds__(CT) part_count_rows_u64_kernel(sdp_column col,
 // So each bucket's current line is assembled in LDS and leaves whole once it
 // fills; lines a tile fills entirely go out directly (their records are written
 // together, the L2 merges them), and only a segment's first and last lines are
-// written in part.  Used by the level-2 scatter of fixed keys (f64_norm 1e9
-// records: 4.1-4.7 -> 3.1-3.2 ms); the row scatter gained nothing from it (its
-// time is not in the write stream), byte records (24 bytes) would need 384 KB.
-constexpr int WC_LINE = 16;                     // 8-byte records per 128-byte line
-struct WcLds {
-    uint64_t line[MAXB][WC_LINE];               // bucket b's current line (slots lo[b] .. cur[b] % 16 filled)
-    uint64_t cur[MAXB];                         // bucket b's next output position
-    uint32_t cnt[MAXB];                         // this tile's records of bucket b
-    uint16_t list[MAXB];                        // buckets whose current line this tile completes
-    uint8_t lo[MAXB];                           // first slot of the current line that is this segment's
+// written in part.  Used by the record scatters: fixed keys (f64_norm 1e9
+// records: 4.1-5.1 -> 3.1 ms) and byte keys' level-1 / level-2 (64-byte lines;
+// C3 step 11.5 -> 9.4 and 9.2 -> 7.1 ms); the row scatter gained nothing from it
+// (its time is not in the write stream).
+// (WcLdsT<NA, L, NBM>: NA parallel record arrays (1 for fixed keys, 3 for the
+// k0 / k1 / meta of byte keys), lines of L records, at most NBM buckets.)
+template <int NA, int L, int NBM>
+struct WcLdsT {
+    uint64_t line[NA][NBM][L];                  // bucket b's current line (slots lo[b] .. cur[b] % L filled)
+    uint64_t cur[NBM];                          // bucket b's next output position
+    uint32_t cnt[NBM];                          // this tile's records of bucket b
+    uint16_t list[NBM];                         // buckets whose current line this tile completes
+    uint8_t lo[NBM];                            // first slot of the current line that is this segment's
     uint32_t nlist;
 };
+using WcLds = WcLdsT<1, 16, MAXB>;              // fixed keys: 128-byte lines, 1024 buckets (146 KB)
+template <int NA> struct WcOut { uint64_t *a[NA]; };
 // (owner thread of bucket b) the records of the current line not yet written
-__device__ __forceinline__ void wc_flush_partial(WcLds &s, int b, uint64_t *out) {
+template <int NA, int L, int NBM>
+__device__ __forceinline__ void wc_flush_partial(WcLdsT<NA, L, NBM> &s, int b, const WcOut<NA> &out) {
     const uint64_t c = s.cur[b];
-    const uint64_t base = c & ~(uint64_t)(WC_LINE - 1);
-    const int e = (int)(c & (WC_LINE - 1));
-    for (int j = s.lo[b]; j < e; ++j) out[base + j] = s.line[b][j];
+    const uint64_t base = c & ~(uint64_t)(L - 1);
+    const int e = (int)(c & (L - 1));
+    for (int j = s.lo[b]; j < e; ++j)
+#pragma unroll
+        for (int a = 0; a < NA; ++a) out.a[a][base + j] = s.line[a][b][j];
 }
-__device__ __forceinline__ void wc_start(WcLds &s, int b, uint64_t pos) {
+template <int NA, int L, int NBM>
+__device__ __forceinline__ void wc_start(WcLdsT<NA, L, NBM> &s, int b, uint64_t pos) {
     s.cur[b] = pos;
-    s.lo[b] = (uint8_t)(pos & (WC_LINE - 1));
+    s.lo[b] = (uint8_t)(pos & (L - 1));
     s.cnt[b] = 0;
 }
 // (owner) continue bucket b at pos: a jump flushes the partial line first
-__device__ __forceinline__ void wc_seek(WcLds &s, int b, uint64_t pos, uint64_t *out) {
+template <int NA, int L, int NBM>
+__device__ __forceinline__ void wc_seek(WcLdsT<NA, L, NBM> &s, int b, uint64_t pos, const WcOut<NA> &out) {
     if (pos != s.cur[b]) {
         wc_flush_partial(s, b, out);
         wc_start(s, b, pos);
     }
 }
-// One tile: record q of this thread (bit q of `have`) goes to bucket
-// (h[q] >> shift) & (nb - 1).  Every thread of the workgroup calls it.
-template <int NT, int RPT>
-__device__ __forceinline__ void wc_tile(WcLds &s, const uint64_t (&h)[RPT], uint32_t have, int shift, int nb,
-                                        uint64_t *out) {
+// One tile: record q of this thread (bit q of `have`; values v[.][q]) goes to
+// bucket bk(q).  Every thread of the workgroup calls it.
+template <int NT, int RPT, int NA, int L, int NBM, typename BK>
+__device__ __forceinline__ void wc_tile(WcLdsT<NA, L, NBM> &s, const uint64_t (&v)[NA][RPT], uint32_t have, int nb,
+                                        const WcOut<NA> &out, BK &&bk) {
+    static_assert(L <= 16 && (L & (L - 1)) == 0, "lines of 2^k <= 16 records");
     const int t = threadIdx.x;
-    const uint64_t mask = (uint64_t)(nb - 1);
     static_assert(NT * RPT <= 65536, "ranks are packed 16 bits per record");
     uint32_t r[(RPT + 1) / 2] = {};             // rank of record q in its bucket: 16 bits each
 #pragma unroll
     for (int q = 0; q < RPT; ++q)
-        if ((have >> q) & 1u) r[q / 2] |= atomicAdd(&s.cnt[(int)((h[q] >> shift) & mask)], 1u) << (16 * (q & 1));
+        if ((have >> q) & 1u) r[q / 2] |= atomicAdd(&s.cnt[bk(q)], 1u) << (16 * (q & 1));
     lds_barrier();
     // records of the current line into LDS, of lines this tile fills entirely
     // straight out, of the new partial line held until the current one is out
@@ -355,35 +365,47 @@ __device__ __forceinline__ void wc_tile(WcLds &s, const uint64_t (&h)[RPT], uint
 #pragma unroll
     for (int q = 0; q < RPT; ++q) {
         if ((have >> q) & 1u) {
-            const int b = (int)((h[q] >> shift) & mask);
+            const int b = bk(q);
             const uint64_t c = s.cur[b];
             const uint64_t p = c + ((r[q / 2] >> (16 * (q & 1))) & 0xFFFFu), e = c + s.cnt[b];
-            if ((p >> 4) == (c >> 4)) s.line[b][p & (WC_LINE - 1)] = h[q];
-            else if ((p >> 4) != (e >> 4)) out[p] = h[q];
-            else {
+            if (p / L == c / L) {
+#pragma unroll
+                for (int a = 0; a < NA; ++a) s.line[a][b][p & (L - 1)] = v[a][q];
+            } else if (p / L != e / L) {
+#pragma unroll
+                for (int a = 0; a < NA; ++a) out.a[a][p] = v[a][q];
+            } else {
                 pend |= 1u << q;
-                slots |= (p & (WC_LINE - 1)) << (4 * q);
+                slots |= (p & (L - 1)) << (4 * q);
             }
         }
     }
     for (int b = t; b < nb; b += NT) {
         const uint64_t c = s.cur[b];
-        if (((c + s.cnt[b]) >> 4) != (c >> 4)) s.list[atomicAdd(&s.nlist, 1u)] = (uint16_t)b;
+        if ((c + s.cnt[b]) / L != c / L) s.list[atomicAdd(&s.nlist, 1u)] = (uint16_t)b;
     }
     lds_barrier();
-    // completed lines: 16 lanes per line, one aligned 128-byte write
+    // completed lines: L lanes per line, one aligned write per array
     const uint32_t nl = s.nlist;
-    for (uint32_t i = t / WC_LINE; i < nl; i += NT / WC_LINE) {
-        const int b = s.list[i], l = t & (WC_LINE - 1);
-        if (l >= s.lo[b]) out[(s.cur[b] & ~(uint64_t)(WC_LINE - 1)) + l] = s.line[b][l];
+    for (uint32_t i = t / L; i < nl; i += NT / L) {
+        const int b = s.list[i], l = t & (L - 1);
+        if (l >= s.lo[b]) {
+            const uint64_t o = (s.cur[b] & ~(uint64_t)(L - 1)) + l;
+#pragma unroll
+            for (int a = 0; a < NA; ++a) out.a[a][o] = s.line[a][b][l];
+        }
     }
     lds_barrier();
 #pragma unroll
     for (int q = 0; q < RPT; ++q)
-        if ((pend >> q) & 1u) s.line[(int)((h[q] >> shift) & mask)][(slots >> (4 * q)) & 15] = h[q];
+        if ((pend >> q) & 1u) {
+            const int b = bk(q), sl = (int)((slots >> (4 * q)) & 15);
+#pragma unroll
+            for (int a = 0; a < NA; ++a) s.line[a][b][sl] = v[a][q];
+        }
     for (int b = t; b < nb; b += NT) {
         const uint64_t c = s.cur[b], e = c + s.cnt[b];
-        if ((e >> 4) != (c >> 4)) s.lo[b] = 0;
+        if (e / L != c / L) s.lo[b] = 0;
         s.cur[b] = e;
         s.cnt[b] = 0;
     }
@@ -1065,29 +1087,45 @@ __global__ void __launch_bounds__(ST) part_scatter_recs_kernel(const uint64_t *i
     }
 }
 
-// Write-combined level-2 scatter of fixed-key records (WcLds): workgroup g
-// takes one contiguous range of chunks, so consecutive chunks of one level-1
-// bucket continue every sub-bucket's cursor (the chunk-major order of the
-// level-2 offsets), and a sub-bucket's partial line is flushed only where the
-// next chunk's offset jumps.
-__global__ void __launch_bounds__(ST) part_scatter_recs_wc_kernel(const uint64_t *in_k0, const Chunk *chunks,
+// Write-combined scatter of partition records (WcLdsT): workgroup g takes one
+// contiguous range of chunks, so consecutive chunks of one level-1 bucket
+// continue every sub-bucket's cursor (the chunk-major order of the level-2
+// offsets), and a sub-bucket's partial line is flushed only where the next
+// chunk's offset jumps.  Fixed keys: 128-byte lines of 1024 sub-buckets.  Byte
+// keys (k0 / k1 / meta, three arrays): 64-byte lines of <= 512 buckets, so the
+// three line buffers fit in 96 KB.
+template <bool BYTES> struct WcRecs {
+    static constexpr int NA = BYTES ? 3 : 1;
+    static constexpr int L = BYTES ? 8 : 16;
+    static constexpr int NBM = BYTES ? 512 : MAXB;
+    static constexpr int RPT = BYTES ? 4 : WC_RPT;
+    using Lds = WcLdsT<NA, L, NBM>;
+};
+template <bool BYTES>
+__global__ void __launch_bounds__(ST) part_scatter_recs_wc_kernel(const uint64_t *in_k0, const uint64_t *in_k1,
+                                                                  const uint64_t *in_meta, const Chunk *chunks,
                                                                   int64_t nchunks, int b1, int b2,
                                                                   const uint64_t *offs, uint64_t *out_k0,
-                                                                  int xcd_map) {
-    constexpr int RPT = WC_RPT;
+                                                                  uint64_t *out_k1, uint64_t *out_meta, int xcd_map) {
+    using W = WcRecs<BYTES>;
+    constexpr int RPT = W::RPT, NA = W::NA;
     constexpr int TILE = ST * RPT;
-    __shared__ WcLds s;
+    __shared__ typename W::Lds s;
     const int t = threadIdx.x;
     const int nb = 1 << b2;
     const int shift = 64 - b1 - b2;
+    const uint64_t mask = (uint64_t)(nb - 1);
     const int G = gridDim.x, bx = blockIdx.x;
     const int g = (xcd_map && G % 8 == 0) ? (int)((bx % 8) * (G / 8) + bx / 8) : bx;
     const int64_t c0 = nchunks * g / G, c1 = nchunks * (g + 1) / G;
-    auto load_tile = [&](int64_t base, int64_t end, uint64_t (&a)[RPT]) {
+    auto load_tile = [&](int64_t base, int64_t end, uint64_t (&a)[NA][RPT]) {
 #pragma unroll
         for (int q = 0; q < RPT; ++q) {
             const int64_t r = base + (int64_t)q * ST + t;
-            if (r < end) a[q] = in_k0[r];
+            if (r < end) {
+                a[0][q] = in_k0[r];
+                if constexpr (BYTES) { a[1][q] = in_k1[r]; a[2][q] = in_meta[r]; }
+            }
         }
     };
     auto uniform_chunk = [](const Chunk &x) {
@@ -1099,42 +1137,54 @@ __global__ void __launch_bounds__(ST) part_scatter_recs_wc_kernel(const uint64_t
         return Chunk{u(x.start), u(x.end), u(x.hbase), u(x.hstride)};
     };
     if (c0 >= c1) return;                       // (workgroup-uniform: no barrier is skipped by a part)
-    uint64_t k0[RPT];
+    uint64_t k[NA][RPT];
     Chunk ch = uniform_chunk(chunks[c0]);
     uint64_t pos = t < nb ? offs[ch.hbase + (int64_t)t * ch.hstride] : 0;
-    load_tile(ch.start, ch.end, k0);
+    load_tile(ch.start, ch.end, k);
+    WcOut<NA> out;
+    out.a[0] = out_k0;
+    if constexpr (BYTES) { out.a[1] = out_k1; out.a[2] = out_meta; }
     if (t < nb) wc_start(s, t, pos);
     if (t == 0) s.nlist = 0;
     for (int64_t c = c0; c < c1; ++c) {
-        if (c > c0 && t < nb) wc_seek(s, t, pos, out_k0);
+        if (c > c0 && t < nb) wc_seek(s, t, pos, out);
         const int64_t cn = c + 1;
         const Chunk chn = cn < c1 ? uniform_chunk(chunks[cn]) : Chunk{0, 0, 0, 0};
         lds_barrier();
         for (int64_t base = ch.start; base < ch.end; base += TILE) {
-            uint64_t x[RPT];
+            uint64_t x[NA][RPT];
             uint32_t have = 0;
+            uint32_t bkp[(RPT + 1) / 2] = {};              // byte keys: bucket of record q, 16 bits each
 #pragma unroll
             for (int q = 0; q < RPT; ++q) {
-                x[q] = k0[q];
-                if (base + (int64_t)q * ST + t < ch.end) have |= 1u << q;
+#pragma unroll
+                for (int a = 0; a < NA; ++a) x[a][q] = k[a][q];
+                if (base + (int64_t)q * ST + t < ch.end) {
+                    have |= 1u << q;
+                    if constexpr (BYTES)
+                        bkp[q / 2] |= (uint32_t)((rec_hash(x[0][q], x[1][q], x[2][q]) >> shift) & mask)
+                                      << (16 * (q & 1));
+                }
             }
             const int64_t nbase = base + TILE;
             const bool last = nbase >= ch.end;                 // wave-uniform
-            // the next tile (of this chunk, or the next chunk's first with its offsets) in flight
-            auto next = [&] {
-                if (last && cn < c1 && t < nb) pos = offs[chn.hbase + (int64_t)t * chn.hstride];
-                load_tile(last ? chn.start : nbase, last ? chn.end : ch.end, k0);
-            };
-            next();             // (issued before the placement: 3.10 vs 3.21-3.38 ms per 1e9 records after it)
-            wc_tile<ST, RPT>(s, x, have, shift, nb, out_k0);
+            // the next tile (of this chunk, or the next chunk's first with its
+            // offsets) in flight; issued before the placement: 3.10 vs 3.21-3.38 ms
+            // per 1e9 fixed-key records after it
+            if (last && cn < c1 && t < nb) pos = offs[chn.hbase + (int64_t)t * chn.hstride];
+            load_tile(last ? chn.start : nbase, last ? chn.end : ch.end, k);
+            wc_tile<ST, RPT>(s, x, have, nb, out, [&](int q) {
+                if constexpr (BYTES) return (int)((bkp[q / 2] >> (16 * (q & 1))) & 0xFFFFu);
+                else return (int)((x[0][q] >> shift) & mask);
+            });
         }
         if (ch.start >= ch.end && cn < c1) {                   // (an empty chunk prefetched nothing)
             if (t < nb) pos = offs[chn.hbase + (int64_t)t * chn.hstride];
-            load_tile(chn.start, chn.end, k0);
+            load_tile(chn.start, chn.end, k);
         }
         ch = chn;
     }
-    if (t < nb) wc_flush_partial(s, t, out_k0);
+    if (t < nb) wc_flush_partial(s, t, out);
 }
 
 // ---- final buckets: LDS grouping -------------------------------------------------
@@ -2297,6 +2347,10 @@ int sdp_part_recs(const sdp_records *in, int32_t is_bytes, const sdp_chunk *d_ch
         if (phase == 0)
             hipLaunchKernelGGL(part_count_recs_kernel<true>, dim3(grid), dim3(CT), 0, s, in->d_k0, in->d_k1, in->d_meta,
                                ch, nchunks, b1, b2, d_hist);
+        else if ((1 << b2) <= WcRecs<true>::NBM)       // (more buckets: the tile-sorted scatter)
+            hipLaunchKernelGGL(part_scatter_recs_wc_kernel<true>, dim3(grid_of(nchunks, 256)), dim3(ST), 0, s,
+                               in->d_k0, in->d_k1, in->d_meta, ch, nchunks, b1, b2, d_offsets, o0, o1, o2,
+                               xcd_map_enabled());
         else
             hipLaunchKernelGGL(part_scatter_recs_kernel<true>, dim3(grid), dim3(ST), 0, s, in->d_k0, in->d_k1,
                                in->d_meta, ch, nchunks, b1, b2, d_offsets, o0, o1, o2, xcd_map_enabled());
@@ -2305,8 +2359,9 @@ int sdp_part_recs(const sdp_records *in, int32_t is_bytes, const sdp_chunk *d_ch
             hipLaunchKernelGGL(part_count_recs_u64_kernel, dim3(grid), dim3(CT), 0, s, in->d_k0, ch, nchunks, b1, b2,
                                d_hist);
         else                             // one resident workgroup per CU, a contiguous range of chunks each
-            hipLaunchKernelGGL(part_scatter_recs_wc_kernel, dim3(grid_of(nchunks, 256)), dim3(ST), 0, s, in->d_k0,
-                               ch, nchunks, b1, b2, d_offsets, o0, xcd_map_enabled());
+            hipLaunchKernelGGL(part_scatter_recs_wc_kernel<false>, dim3(grid_of(nchunks, 256)), dim3(ST), 0, s,
+                               in->d_k0, nullptr, nullptr, ch, nchunks, b1, b2, d_offsets, o0, nullptr, nullptr,
+                               xcd_map_enabled());
     }
     return check_launch("part_recs_kernel");
 }
