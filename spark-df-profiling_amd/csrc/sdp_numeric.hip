@@ -1497,7 +1497,11 @@ __device__ __forceinline__ void pass2_count_body(const sdp_column &col, double m
     const int64_t r1 = min(n, r0 + rows_per_block);
     const int64_t v0 = r0 / VPT, v1 = r1 / VPT;        // whole vectors of this block's rows
     const Vec16<T> *vals = (const Vec16<T> *)col.d_values;
-    constexpr int U = sizeof(T) >= 8 ? P2_UNROLL : (std::is_same<T, float>::value ? P2_UNROLL / 2 : 1);
+    // (doubles: two vectors per tile -- at four the fp64 moments, the hash and
+    // the bin search spill 18 VGPRs: 18.1 -> 17.1 ms for six 1e9-row columns;
+    // int64 measured flat, profiles/r04p2c_pass2_count_unroll_ab.log)
+    constexpr int U = std::is_same<T, double>::value ? 2
+                      : sizeof(T) >= 8 ? P2_UNROLL : (std::is_same<T, float>::value ? P2_UNROLL / 2 : 1);
     constexpr int64_t TV = (int64_t)P2_BLOCK * U;
     // ping-pong tiles of this block's whole vectors [v0, v1)
     const VBits vbm = vbits_init(col.d_validity, col.validity_bit_offset, col.d_values);

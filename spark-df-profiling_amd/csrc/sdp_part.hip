@@ -446,7 +446,7 @@ __device__ __forceinline__ void scatter_rows_u64_body(const sdp_column &col, con
         uint32_t vmask;
         tile.hash(col, vbm, base, r1, h, vmask);
         if (base + S_TILE < r1) tile.load(col, vbm, base + S_TILE, r1);      // next tile in flight
-        uint32_t rank[S_RPT];
+        uint32_t rank[S_RPT / 2] = {};          // 16 bits per row (< S_TILE): no VGPR spills
         uint32_t keep = 0;
 #pragma unroll
         for (int q = 0; q < S_RPT; ++q) {
@@ -454,7 +454,7 @@ __device__ __forceinline__ void scatter_rows_u64_body(const sdp_column &col, con
                 const int hv = any_heavy ? heavy_find_u64(s.heavy, heavy.n, h[q]) : -1;
                 if (hv < 0 && h[q] != EMPTY64) {
                     keep |= 1u << q;
-                    rank[q] = atomicAdd(&s.hist[b1 ? (int)(h[q] >> shift) : 0], 1u);
+                    rank[q / 2] |= atomicAdd(&s.hist[b1 ? (int)(h[q] >> shift) : 0], 1u) << (16 * (q & 1));
                 }
             }
         }
@@ -462,7 +462,8 @@ __device__ __forceinline__ void scatter_rows_u64_body(const sdp_column &col, con
         block_excl_scan<ST>(s.hist, s.off, nb, s.wsum);
 #pragma unroll
         for (int q = 0; q < S_RPT; ++q)
-            if ((keep >> q) & 1u) s.stage[s.off[b1 ? (int)(h[q] >> shift) : 0] + rank[q]] = h[q];
+            if ((keep >> q) & 1u)
+                s.stage[s.off[b1 ? (int)(h[q] >> shift) : 0] + ((rank[q / 2] >> (16 * (q & 1))) & 0xFFFFu)] = h[q];
         lds_barrier();
         const uint32_t total = s.off[nb - 1] + s.hist[nb - 1];
         for (uint32_t j = t; j < total; j += ST) {
