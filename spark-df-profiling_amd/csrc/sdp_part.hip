@@ -2067,13 +2067,13 @@ __global__ void __launch_bounds__(ST) d32_scatter1_kernel(sdp_column col, int64_
     const VBits vbm = vbits_init(col.d_validity, col.validity_bit_offset, col.d_values);
     if (r0 < r1) tile.load(col, vbm, r0, r1);
     for (int64_t base = r0; base < r1; base += S_TILE) {
-        uint32_t h[S_RPT], vmask, rank[S_RPT];
+        uint32_t h[S_RPT], vmask, rank[S_RPT / 2] = {};  // ranks 16 bits each (< S_TILE): no VGPR spills
         tile.hash(col, vbm, base, r1, lo, h, vmask);
         if (base + S_TILE < r1) tile.load(col, vbm, base + S_TILE, r1);      // next tile in flight
 #pragma unroll
         for (int q = 0; q < S_RPT; ++q) {
             if ((vmask >> q) & 1u) {
-                rank[q] = atomicAdd(&s.hist[h[q] >> (32 - D32_B1)], 1u);
+                rank[q / 2] |= atomicAdd(&s.hist[h[q] >> (32 - D32_B1)], 1u) << (16 * (q & 1));
                 atomicAdd(&s.h2[h[q] >> (32 - D32_B1 - D32_B2)], 1u);
             }
         }
@@ -2081,7 +2081,8 @@ __global__ void __launch_bounds__(ST) d32_scatter1_kernel(sdp_column col, int64_
         block_excl_scan<ST>(s.hist, s.off, D32_NB1, s.wsum);
 #pragma unroll
         for (int q = 0; q < S_RPT; ++q)
-            if ((vmask >> q) & 1u) s.stage[s.off[h[q] >> (32 - D32_B1)] + rank[q]] = h[q];
+            if ((vmask >> q) & 1u)
+                s.stage[s.off[h[q] >> (32 - D32_B1)] + ((rank[q / 2] >> (16 * (q & 1))) & 0xFFFFu)] = h[q];
         lds_barrier();
         const uint32_t total = s.off[D32_NB1 - 1] + s.hist[D32_NB1 - 1];
         for (uint32_t j = t; j < total; j += ST) {
