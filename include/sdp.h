@@ -422,7 +422,8 @@ typedef struct sdp_records {
     uint64_t *d_k1;     /* byte keys only */
     uint64_t *d_meta;   /* byte keys only */
 } sdp_records;
-/* Keys counted outside the partitions (n <= 256): hashes, and for byte keys
+/* Keys counted outside the partitions (n <= 256; n <= 1024 for
+ * sdp_part_rows_records): hashes, and for byte keys
  * the (k0, k1, meta) of one representative row; counts go to d_heavy_counts. */
 typedef struct sdp_heavy {
     const uint64_t *d_h;
@@ -522,7 +523,8 @@ int sdp_part_rows_batch(const sdp_rows_task *d_tasks, int32_t ntasks, int32_t dt
  * rows to d_out at the strip's first row position (d_out holds length records),
  * counts the strip's level-1 buckets into d_hist[b * nchunks + chunk] and
  * writes d_chunks[chunk] = {strip start, start + records, chunk, nchunks};
- * heavy counts and d_stats[0] as sdp_part_rows phase 0.  The level-1 scatter
+ * heavy counts (up to 1024 heavy keys) and d_stats[0] as sdp_part_rows
+ * phase 0.  The level-1 scatter
  * is then sdp_part_recs(d_out, 1, d_chunks, nchunks, 0, b1, 1, ...) with the
  * exclusive scan of d_hist.  nchunks = sdp_part_records_chunks(length). */
 int64_t sdp_part_records_chunks(int64_t length);
