@@ -19,6 +19,11 @@ HBM when the timed region starts; H2D is not timed.
     python bench.py [--gpus N --steps K --warmup W --rows R]
     torchrun --nproc-per-node N bench.py --gpus N ...     (one rank per GPU, RCCL)
 
+With --gpus N > 1 and no launcher (no WORLD_SIZE in the environment) bench.py
+starts the N rank processes itself as children (torch.distributed.run on
+127.0.0.1) and re-prints rank 0's line; a rank whose process group is not N
+ranks wide exits non-zero.
+
 Rank 0 prints one JSON line.  `roofline` is for the dominant kernel, timed with
 HIP events on the launch stream; `cpu_baseline` is the oracle (CPU restatement)
 on a bounded sample of the same workload, rank 0 at N=1 only.
@@ -537,6 +542,46 @@ class ReadbackCensus:
         return False
 
 
+def launch_cmd(argv, gpus, env):
+    """The child command that runs `gpus` rank processes of this bench, or None
+    when this process should run the step itself: --gpus 1, or a launcher
+    (torchrun / the driver) already set WORLD_SIZE.  One rank per GPU,
+    rendezvous on 127.0.0.1 at a free port."""
+    if gpus <= 1 or 'WORLD_SIZE' in env:
+        return None
+    import socket
+    with socket.socket() as sk:
+        sk.bind(('127.0.0.1', 0))
+        port = sk.getsockname()[1]
+    return [sys.executable, '-m', 'torch.distributed.run', '--nnodes=1', '--nproc-per-node', str(gpus),
+            '--master-addr', '127.0.0.1', '--master-port', str(port), os.path.abspath(__file__)] + list(argv)
+
+
+def check_world(gpus, world, ranks_seen):
+    """A rank's world must be what --gpus asked for (a silent one-GPU run of an
+    N-GPU metric point is the failure this guards)."""
+    if world != gpus or ranks_seen != gpus:
+        raise SystemExit('bench.py: --gpus %d but the process group has world_size %d (%d ranks answered)'
+                         % (gpus, world, ranks_seen))
+
+
+def run_ranks(cmd):
+    """Start the rank processes as children (this process never touches the
+    GPU), stream their stderr, re-print rank 0's JSON line, return their rc."""
+    import subprocess
+    p = subprocess.run(cmd, stdout=subprocess.PIPE, text=True)
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith('{')]
+    other = [ln for ln in p.stdout.splitlines() if not ln.startswith('{')]
+    if other:
+        print('\n'.join(other), file=sys.stderr)
+    if p.returncode == 0 and not lines:
+        print('bench.py: the rank processes printed no JSON line', file=sys.stderr)
+        return 1
+    if lines:
+        print(lines[-1])
+    return p.returncode
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('--gpus', type=int, default=1)
@@ -553,6 +598,11 @@ def main():
     ap.add_argument('--workers', type=int, default=None,
                     help='columns profiled concurrently per GPU (default: SDP_COLUMN_WORKERS or 1)')
     args = ap.parse_args()
+    # --gpus N without a launcher: N rank processes as children, started
+    # before anything here touches the GPU or starts a worker pool
+    cmd = launch_cmd(sys.argv[1:], args.gpus, os.environ)
+    if cmd is not None:
+        sys.exit(run_ranks(cmd))
     if args.rows is None:
         args.rows = 10 ** 7 if args.workload == 'c5' else 10 ** 9
     traffic_path = args.traffic if args.traffic is not None else TRAFFIC_SUMMARY.get(args.workload)
@@ -596,6 +646,13 @@ def main():
             dist.init_process_group(backend)
         from spark_df_profiling.comm import TorchComm
         comm = TorchComm()
+    ranks_seen = 1
+    if world > 1:
+        # count the ranks through the backend itself (a one-element all-reduce)
+        one = torch.ones(1, dtype=torch.float32, device=device)
+        ranks_seen = int(comm.allreduce_sum(one).item())
+    if world > 1 or args.gpus > 1:
+        check_world(args.gpus, world, ranks_seen)
 
     from spark_df_profiling import describe
     from spark_df_profiling import _native as nat
@@ -687,7 +744,7 @@ def main():
                     'with the Pearson matrix on fp64 MFMA' % (args.rows, ncols))
     out = {
         'metric': METRIC, 'value': round(args.rows * args.steps / elapsed, 1), 'unit': 'rows/s',
-        'n_gpus': world, 'steps': args.steps, 'warmup': args.warmup,
+        'n_gpus': world, 'ranks_seen': ranks_seen, 'steps': args.steps, 'warmup': args.warmup,
         'ms_per_step': round(1e3 * elapsed / args.steps, 2), 'higher_is_better': True, 'scaling': 'strong',
         'vs_baseline': None, 'dtype': 'f64', 'data': 'synthetic (torch, seeded, generated in HBM)',
         'config': {'workload': workload, 'rows': args.rows, 'columns': ncols,
