@@ -41,6 +41,45 @@ enum sdp_status {
 
 #define SDP_MAX_WINDOWS 5     /* quantile windows per pass-1 launch */
 
+/* ---- grouping policy (describe.py:143 countDistinct, :251 groupBy count) ---
+ * One set of constants for every orchestrator: the library's coarse entries
+ * (sdp_api.cpp) and the Python engine (engine.py reads them from _native.py,
+ * which checks them against sdp_layout_info() at load). */
+#define SDP_HEAVY_MAX         256      /* heavy keys the row kernels' LDS tables hold       */
+#define SDP_HEAVY_MAX_REC     1024     /* heavy byte keys the records kernel holds          */
+#define SDP_HEAVY_MIN         3        /* sample occurrences that make a key heavy          */
+#define SDP_PART_SAMPLE       16384    /* heavy-key sample rows, fixed-width keys           */
+#define SDP_PART_SAMPLE_BYTES 65536    /* heavy-key sample rows, byte keys                  */
+#define SDP_PART_CHUNK        131072   /* level-2 records per chunk                         */
+#define SDP_GSORT_MAX         8192     /* groups one sdp_sort_groups launch orders          */
+
+/* ---- layout handshake ------------------------------------------------------
+ * SDP_ABI_VERSION changes whenever a struct below, a record layout or a policy
+ * constant above changes.  A host binding compares sdp_layout_info() with its
+ * own view and refuses a library that disagrees (a record-layout mismatch
+ * between the engine and the library once turned garbage metas into row
+ * indices on the GPU). */
+#define SDP_ABI_VERSION 5
+#define SDP_LAYOUT_NSIZES 17
+typedef struct sdp_layout {
+    int32_t abi_version;
+    int32_t n_sizes;                   /* SDP_LAYOUT_NSIZES                           */
+    /* byte-key records: byte_record_arrays parallel uint64 arrays (k0, k1, meta),
+     * one record every byte_record_stride bytes in each */
+    int32_t byte_record_arrays;
+    int32_t byte_record_stride;
+    int32_t fixed_record_bytes;        /* fixed-key level-1 / level-2 records (mix64 h) */
+    int32_t heavy_max, heavy_max_rec, heavy_min;
+    int32_t part_sample, part_sample_bytes, gsort_max, _pad;
+    int64_t part_chunk;
+    /* sizeof: sdp_column, sdp_bytes_column, sdp_records, sdp_heavy, sdp_chunk,
+     * sdp_qplan, sdp_pass1_result, sdp_select_task, sdp_compact_task,
+     * sdp_pass1_task, sdp_pass2_task, sdp_rows_task, sdp_pass2_result,
+     * sdp_minmax_result, sdp_distinct_result, sdp_topk_entry, sdp_topk_result */
+    int64_t sizes[SDP_LAYOUT_NSIZES];
+} sdp_layout;
+int sdp_layout_info(sdp_layout *out);      /* host only; always 0 */
+
 /* One Arrow column slice resident in HBM. */
 typedef struct sdp_column {
     const void    *d_values;           /* element 0 of the slice; 16-B aligned      */
@@ -468,7 +507,9 @@ typedef struct sdp_pass2_task {
     int32_t            bins, edges_monotone, b1, grid;
     /* b1 = -1: the count is sdp_distinct32's level-1 count instead (64
      * buckets of mix32(key - key32_lo) into d_part_hist [64][grid], non-null
-     * rows added to d_stats[1]; heavy keys unused) -- its pre-count argument */
+     * rows added to d_stats[1]; heavy keys unused) -- its pre-count argument.
+     * Only for SDP_F32 and integral dtypes (32-bit key spaces); an SDP_F64
+     * task with b1 = -1 counts nothing. */
     int64_t            key32_lo;
 } sdp_pass2_task;
 
@@ -476,6 +517,25 @@ typedef struct sdp_pass2_task {
  * in two launches (wide tables); d_tasks lives in device memory. */
 int sdp_pass2_count_batch(const sdp_pass2_task *d_tasks, int32_t ntasks, int32_t dtype, int32_t bins,
                           int32_t edges_monotone, int32_t max_grid, void *stream);
+
+/* Pass 2 of every NUM column of a table (<= 16 columns of SDP_F64 / SDP_F32 /
+ * SDP_I64 / SDP_I32, one length, 2..10 monotone bins) AND the Pearson Gram of
+ * the columns in gram_mask (utils.py:27-31: listwise deletion over those
+ * columns, shift = each task's mean) in ONE read of the table.  Per column the
+ * outputs are sdp_pass2_count_batch's (d_result, d_hist, and -- b1 >= 0 or
+ * b1 = -1 -- the level-1 count outputs; b1 = -2: no count); the Gram's are
+ * sdp_gram's (d_gram ntasks x ntasks, d_colsum, *d_n: kept rows; entries of
+ * columns outside gram_mask are 0).  Every task: rows_per_block and grid of
+ * sdp_part_rows_per_block(length, 0), its d_work of
+ * sdp_pass2_count_workspace_bytes.  h_tasks and d_tasks hold the same tasks
+ * (host copy: argument checks and LDS layout; device copy: the kernel).  At
+ * most two columns may carry heavy keys (SDP_ECAP otherwise).
+ * Stream-ordered.  Replaces describe.py:215-223 + :49 of every NUM column and
+ * utils.py:29-31. */
+int64_t sdp_pass2_gram_workspace_bytes(int64_t length, int32_t ncols);
+int sdp_pass2_gram(const sdp_pass2_task *h_tasks, const sdp_pass2_task *d_tasks, int32_t ntasks,
+                   uint32_t gram_mask, void *d_work, int64_t work_bytes, double *d_gram, double *d_colsum,
+                   double *d_n, void *stream);
 
 /* Packs the key bytes of n groups -- bytes [d_starts[i], d_starts[i] + d_lens[i])
  * of d_data -- at d_out + d_offs[i] (the sharded string exchange's payload). */
@@ -655,7 +715,8 @@ int sdp_hash_distinct_count(const sdp_column *col, const sdp_bytes_column *bcol,
  * order-preserving 64-bit key (key_f64 / key_i64 inverses: sign-flip for
  * integers; sign-flip / invert for floats), byte columns the 0-based row index
  * of one row holding the value.  ***Other Values*** = rows - sum(counts);
- * ***Other Values Distinct Count*** = groups - n_top. */
+ * ***Other Values Distinct Count*** = groups - n_top.  0 <= k <= SDP_GSORT_MAX
+ * (SDP_EINVAL otherwise: the candidates are ordered by one sort launch). */
 typedef struct sdp_topk_entry {
     uint64_t key;
     uint64_t count;

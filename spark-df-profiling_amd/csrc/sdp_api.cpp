@@ -23,11 +23,12 @@ namespace sdp {
 namespace {
 
 constexpr int64_t ARENA_ALIGN = 256;
-constexpr int PART_SAMPLE = 16384;          // heavy-key sample rows (engine.PART_SAMPLE)
-constexpr int HEAVY_MIN = 3;                // sample occurrences that make a key heavy
-constexpr int HEAVY_N = 256;                // SDP heavy-key capacity (sdp_heavy.h HEAVY_MAX)
-constexpr int64_t PART_CHUNK = 131072;      // level-2 records per chunk (engine.PART_CHUNK)
-constexpr int64_t GSORT_MAX = 8192;         // groups one sort_groups launch orders
+// the grouping policy is sdp.h's, shared with the Python engine
+constexpr int PART_SAMPLE = SDP_PART_SAMPLE;
+constexpr int PART_SAMPLE_BYTES = SDP_PART_SAMPLE_BYTES;
+constexpr int HEAVY_MIN = SDP_HEAVY_MIN;
+constexpr int64_t PART_CHUNK = SDP_PART_CHUNK;
+constexpr int64_t GSORT_MAX = SDP_GSORT_MAX;
 constexpr int64_t SMALL_BYTES = 64ll << 20; // headroom for tables, histograms, chunk lists
 
 struct Arena {
@@ -245,16 +246,32 @@ struct Groups {
 
 struct Heavy {
     int n = 0;
-    std::vector<uint64_t> h, meta;  // host copies
+    std::vector<uint64_t> h, meta;  // host copies, the most frequent key first
+    std::vector<int64_t> cnt;       // sample occurrences of each
     uint64_t *d_h = nullptr, *d_k0 = nullptr, *d_k1 = nullptr, *d_meta = nullptr;
     double rec_frac = 1.0;
+    int ns = 1;                     // sample rows
     bool near_unique = false;
+    // the first `cap` keys only (engine._hv_cap): the row kernels' LDS tables
+    // hold SDP_HEAVY_MAX, the byte records kernel SDP_HEAVY_MAX_REC; rows of
+    // the dropped keys become partition records, the groups are the same
+    void cap_to(int cap) {
+        if (n <= cap) return;
+        int64_t dropped = 0;
+        for (int i = cap; i < n; ++i) dropped += cnt[i];
+        rec_frac += (double)dropped / (double)ns;
+        n = cap;
+        h.resize(cap);
+        cnt.resize(cap);
+        if (!meta.empty()) meta.resize(cap);
+    }
 };
 
 // keys seen >= HEAVY_MIN times in an evenly spaced sample (engine._heavy_keys):
 // counted outside the partitions, so skew never piles into one bucket
 int heavy_keys(Arena &A, const sdp_column *col, const sdp_bytes_column *bcol, int64_t n, Heavy &hv, hipStream_t s) {
-    const int ns = (int)std::min<int64_t>(PART_SAMPLE, std::max<int64_t>(n, 1));
+    const int ns = (int)std::min<int64_t>(bcol ? PART_SAMPLE_BYTES : PART_SAMPLE, std::max<int64_t>(n, 1));
+    hv.ns = ns;
     uint64_t *dh = A.take<uint64_t>(ns);
     SDP_NEED(dh, A);
     sdp_records rec{nullptr, nullptr, nullptr};
@@ -296,16 +313,18 @@ int heavy_keys(Arena &A, const sdp_column *col, const sdp_bytes_column *bcol, in
     for (const U &x : u)
         if (x.cnt >= HEAVY_MIN) sel.push_back(x);
     if (sel.empty()) return 0;
-    if ((int)sel.size() > HEAVY_N) {
-        std::stable_sort(sel.begin(), sel.end(), [](const U &a, const U &b) { return a.cnt > b.cnt; });
-        sel.resize(HEAVY_N);
-        std::sort(sel.begin(), sel.end(), [](const U &a, const U &b) { return a.h < b.h; });
-    }
+    // the most frequent first (engine._heavy_struct), at most SDP_HEAVY_MAX_REC
+    // byte keys / SDP_HEAVY_MAX fixed keys; group_partitioned caps byte keys
+    // to SDP_HEAVY_MAX when the row kernels, not the records kernel, take them
+    std::stable_sort(sel.begin(), sel.end(), [](const U &a, const U &b) { return a.cnt > b.cnt; });
+    const int cap = bcol ? SDP_HEAVY_MAX_REC : SDP_HEAVY_MAX;
+    if ((int)sel.size() > cap) sel.resize(cap);
     hv.n = (int)sel.size();
     int64_t heavy_rows = 0;
     std::vector<uint64_t> hk0, hk1;
     for (const U &x : sel) {
         hv.h.push_back(x.h);
+        hv.cnt.push_back(x.cnt);
         heavy_rows += x.cnt;
         if (bcol) {
             hk0.push_back(k0[x.first]);
@@ -341,19 +360,27 @@ int group_partitioned(Arena &A, const sdp_column *col, const sdp_bytes_column *b
     Heavy hv;
     SDP_TRY(heavy_keys(A, col, bcol, n, hv, s));
     const int64_t target = sdp_part_bucket_target(isb, with_counts);
-    int64_t n_rec = n;
-    if (isb && hv.n > 0) n_rec = std::min<int64_t>(n, (int64_t)((double)n * (1.25 * hv.rec_frac + 0.02)) + 1);
     auto bits_for = [](double x) { return x <= 1.0 ? 0 : (int)std::ceil(std::log2(x)); };
-    int total_bits = bits_for((double)n_rec / (double)target);
+    int total_bits, b1;
+    bool one_read;
+    while (true) {                                 // (engine._group_prepare)
+        int64_t n_rec = n;
+        if (isb && hv.n > 0) n_rec = std::min<int64_t>(n, (int64_t)((double)n * (1.25 * hv.rec_frac + 0.02)) + 1);
+        total_bits = bits_for((double)n_rec / (double)target);
+        b1 = std::min(10, (total_bits + 1) / 2);
+        one_read = isb && b1 > 0;
+        if (!isb || one_read || hv.n <= SDP_HEAVY_MAX) break;
+        hv.cap_to(SDP_HEAVY_MAX);                  // b1 == 0: the row kernels take the bytes
+    }
     bool large = false;
     if (total_bits > 20 && !isb && !with_counts) {
         total_bits = std::max(20, bits_for((double)n / (4.0 * (double)target)));
         large = true;
+        b1 = std::min(10, (total_bits + 1) / 2);
     }
-    const int b1 = std::min(10, (total_bits + 1) / 2), b2 = total_bits - b1;
+    const int b2 = total_bits - b1;
     if (b2 > 10) return 0;
     const int64_t nb1 = 1ll << b1, nb2 = 1ll << b2;
-    const bool one_read = isb && b1 > 0;
     int64_t grid;
     if (one_read) grid = sdp_part_records_chunks(n);
     else {
@@ -629,21 +656,33 @@ struct TopK {
             SDP_TRY(sdp_select_by_value(sel, keys, on, 0, kh, o, nullptr, on2, s));
             return sort_take(o, on2, r, r);
         }
-        int offset = 0;
+        // buffers taken once for the first (largest) n and reused by every
+        // prefix round: the tie set of round i is the selection of round i+1
+        // (two tie buffers, alternating); sort_take's small packs are released
+        // at the start of each round
+        uint64_t *pre = A.take<uint64_t>(n), *kth = A.take<uint64_t>(1);
+        const int64_t ws_bytes = sdp_select_kth_workspace_bytes(n);
+        void *ws = A.take<char>(ws_bytes);
+        uint64_t *below = A.take<uint64_t>(n), *bn = A.take<uint64_t>(1);
+        uint64_t *eqb[2] = {A.take<uint64_t>(n), A.take<uint64_t>(n)};
+        uint64_t *enb[2] = {A.take<uint64_t>(1), A.take<uint64_t>(1)};
+        SDP_NEED(enb[1], A);
+        SDP_NEED(enb[0], A);
+        SDP_NEED(eqb[1], A);
+        SDP_NEED(eqb[0], A);
+        SDP_NEED(below, A);
+        SDP_NEED(ws, A);
+        SDP_NEED(kth, A);
+        SDP_NEED(pre, A);
+        const int64_t mark = A.used;
+        int offset = 0, flip = 0;
         int64_t need = r;
         while (true) {
-            uint64_t *pre = A.take<uint64_t>(n), *kth = A.take<uint64_t>(1);
-            void *ws = A.take<char>(sdp_select_kth_workspace_bytes(n));
-            uint64_t *below = A.take<uint64_t>(n), *bn = A.take<uint64_t>(1);
-            uint64_t *eq = A.take<uint64_t>(n), *en = A.take<uint64_t>(1);
-            SDP_NEED(en, A);
-            SDP_NEED(eq, A);
-            SDP_NEED(below, A);
-            SDP_NEED(ws, A);
-            SDP_NEED(kth, A);
-            SDP_NEED(pre, A);
+            A.used = mark;
+            uint64_t *eq = eqb[flip], *en = enb[flip];
+            flip ^= 1;
             SDP_TRY(sdp_group_prefix(sel, on, g.slots, bcol, offset, pre, s));
-            SDP_TRY(sdp_select_kth(pre, on, n, need - 1, 0, EMPTY64, ws, sdp_select_kth_workspace_bytes(n), kth, s));
+            SDP_TRY(sdp_select_kth(pre, on, n, need - 1, 0, EMPTY64, ws, ws_bytes, kth, s));
             uint64_t kh;
             SDP_TRY(d2h(&kh, kth, 8, s));
             SDP_TRY(zero(bn, 8, s));
@@ -872,6 +911,7 @@ extern "C" int sdp_value_counts_topk(const sdp_column *col, const sdp_bytes_colu
     SDP_TRY(check_inputs(col, bcol, "sdp_value_counts_topk"));
     if (h_out == nullptr || (k > 0 && h_top == nullptr) || k < 0 || d_work == nullptr)
         return set_error(SDP_EINVAL, "sdp_value_counts_topk: args");
+    if (k > SDP_GSORT_MAX) return set_error(SDP_EINVAL, "sdp_value_counts_topk: k = %d > %d", k, SDP_GSORT_MAX);
     hipStream_t s = (hipStream_t)stream;
     Arena A(d_work, work_bytes);
     memset(h_out, 0, sizeof(*h_out));

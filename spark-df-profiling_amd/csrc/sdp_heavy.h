@@ -10,12 +10,12 @@
 namespace sdp {
 
 constexpr int MAXB = 1024;              // buckets per level (b <= 10)
-constexpr int HEAVY_MAX = 256;
+constexpr int HEAVY_MAX = SDP_HEAVY_MAX;
 // the byte records kernel (one workgroup per CU, 110 KB of LDS) holds more:
 // on a zipf(1.1) string column over 1e8 labels the top 1024 keys cover ~62 %
 // of the rows against ~54 % for the top 256, and every heavy row is one
 // 24-byte record fewer through both scatters and the de-duplication
-constexpr int HEAVY_MAX_REC = 1024;
+constexpr int HEAVY_MAX_REC = SDP_HEAVY_MAX_REC;
 // open-addressing slots: load <= 1/4 at 256 keys, <= 1/2 at 1024
 template <int MAXK>
 constexpr int heavy_slots() { return MAXK <= 256 ? 1024 : 2 * MAXK; }

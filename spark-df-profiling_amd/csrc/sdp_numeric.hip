@@ -1484,6 +1484,8 @@ __device__ __forceinline__ void pass2_count_body(const sdp_column &col, double m
                 atomicAdd(&cl.hist[mix32(key32_rel<T>(x, lo32)) >> (32 - D32_B1)], 1u);
                 return;
             }
+        } else {
+            if (d32) return;        // no 32-bit key space for doubles (sdp.h: b1 = -1 is F32 / integral only)
         }
         const uint64_t h = mix64(key_of<T>(x));
         const int hv = any_heavy ? heavy_find_u64(cl.heavy, heavy.n, h) : -1;
@@ -2303,6 +2305,11 @@ extern "C" int sdp_pass2_count_batch(const sdp_pass2_task *d_tasks, int32_t ntas
     int rc = check_launch("pass2_count_batch_kernel");
     if (rc) return rc;
     hipLaunchKernelGGL(pass2_merge_batch_kernel, dim3(ntasks), dim3(MERGE_T), 0, s, d_tasks);
+    return check_launch("pass2_merge_batch_kernel");
+}
+
+int launch_pass2_merge_batch(const sdp_pass2_task *d_tasks, int ntasks, void *stream) {
+    hipLaunchKernelGGL(pass2_merge_batch_kernel, dim3(ntasks), dim3(MERGE_T), 0, (hipStream_t)stream, d_tasks);
     return check_launch("pass2_merge_batch_kernel");
 }
 

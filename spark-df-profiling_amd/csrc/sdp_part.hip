@@ -1326,22 +1326,15 @@ __global__ void __launch_bounds__(DTU) part_dedup_u64_kernel(const uint64_t *in_
     }
 }
 
-// DIRECT (near-unique columns, chosen from the heavy-key sample): every probe
-// is one CAS -- a new key is claimed in one LDS round trip instead of a read
-// and a CAS (f64 N(0,1) at 1e9 rows: 4.91 -> 4.37 ms); with repeated keys the
-// read-first form wins (zipf int64: 3.51 vs 4.18 ms), as same-slot CASes of a
-// wave serialise where reads broadcast.
 // Distinct-only fixed keys: one WAVE per final bucket (~1 K records), a
-// wave-private 2048-slot LDS table, no workgroup barriers.  Each lane walks its
-// own queue of records (a long probe sequence delays only that lane); a slot is
-// read before it is claimed, so repeated keys resolve with broadcast reads.
-// A bucket of fewer records than slots always terminates and takes the lean
-// loop (no probe counter: it costs 2.5x, tools/ubench/dedup_bench.hip); larger
-// buckets run in batches with a probe limit, and more than WV_SLOTS/2 distinct
-// keys in one bucket raises stats[3] (the caller recounts on the global-table
-// path).  The key whose hash is UINT64_MAX never reaches here (the row kernels
-// count it in stats[1]).  Measured on MI355X: 4.3 ms for 943 M distinct
-// records in 1 M buckets vs 13.2 ms for a workgroup-per-bucket table.
+// wave-private 2048-slot LDS table, no workgroup barriers.  DIRECT (near-unique
+// columns, chosen from the heavy-key sample): every probe is one CAS -- a new
+// key is claimed in one LDS round trip instead of a read and a CAS (f64 N(0,1)
+// at 1e9 rows: 4.91 -> 4.37 ms); with repeated keys the read-first form wins
+// (zipf int64: 3.51 vs 4.18 ms), as same-slot CASes of a wave serialise where
+// reads broadcast.  More than WV_SLOTS/2 distinct keys in one bucket raises
+// stats[3] (the caller recounts on the global-table path).  The key whose hash
+// is UINT64_MAX never reaches here (the row kernels count it in stats[1]).
 constexpr int WV_W = 4;                 // waves per workgroup
 constexpr int WV_SLOTS = 2048;          // table slots per wave (16 KB)
 constexpr int WV_Q = 20;                // records per lane per batch
@@ -1354,110 +1347,8 @@ __device__ __forceinline__ void wave_load_batch(uint64_t (&hq)[WV_Q], const uint
         hq[q] = r < hi ? in_h[r] : EMPTY64;
     }
 }
-// inserts this lane's records of the batch starting at rb (loaded by wave_load_batch)
-template <bool LIMIT, bool DIRECT>
-__device__ __forceinline__ uint32_t wave_insert_regs(uint64_t *T, uint64_t (&hq)[WV_Q], int64_t rb, int64_t hi,
-                                                     int lane, bool &full) {
-    const int64_t rem = hi - rb - lane;
-    int left = rem <= 0 ? 0 : (int)min((int64_t)WV_Q, (rem + WAVE - 1) / WAVE);
-    uint64_t x = 0;
-    uint32_t pos = 0, fresh = 0;
-    int probes = 0;
-    bool have = false;
-    while (true) {
-        if (!have) {
-            if (left == 0) break;
-            x = hq[0];
-#pragma unroll
-            for (int k = 0; k < WV_Q - 1; ++k) hq[k] = hq[k + 1];
-            --left;
-            pos = (uint32_t)x & (WV_SLOTS - 1);
-            if (LIMIT) probes = 0;
-            have = true;
-        }
-        uint64_t cur;
-        if (DIRECT) {
-            cur = atomicCAS((unsigned long long *)&T[pos], (unsigned long long)EMPTY64, (unsigned long long)x);
-            if (cur == EMPTY64) ++fresh;
-        } else {
-            cur = T[pos];
-            if (cur == EMPTY64) {
-                cur = atomicCAS((unsigned long long *)&T[pos], (unsigned long long)EMPTY64, (unsigned long long)x);
-                if (cur == EMPTY64) ++fresh;
-            }
-        }
-        if (cur == EMPTY64 || cur == x) { have = false; continue; }
-        pos = (pos + 1) & (WV_SLOTS - 1);
-        if (LIMIT && ++probes >= WV_SLOTS / 2) { full = true; have = false; }
-    }
-    return fresh;
-}
-
-// The first batch of the wave's next bucket is loaded before the current bucket
-// is inserted, so its memory latency overlaps the LDS probing.
-template <bool DIRECT>
-__global__ void __launch_bounds__(WV_W * WAVE) part_dedup_u64_wave_kernel(const uint64_t *in_h,
-                                                                          const uint64_t *starts,
-                                                                          int64_t nbuckets, uint64_t *stats) {
-    __shared__ uint64_t tab[WV_W][WV_SLOTS];
-    const int lane = lane_id(), w = threadIdx.x / WAVE;
-    uint64_t *T = tab[w];
-    uint64_t groups = 0;
-    bool full = false;
-    const int64_t stride = (int64_t)gridDim.x * WV_W;
-    int64_t f = (int64_t)blockIdx.x * WV_W + w;
-    int64_t lo = 0, hi = 0;
-    uint64_t hq[WV_Q];
-    if (f < nbuckets) {
-        lo = starts[f];
-        hi = starts[f + 1];
-        wave_load_batch(hq, in_h, lo, hi, lane);
-    }
-    uint64_t hn[WV_Q];
-    // one step: prefetch bucket fn into `nxt`, insert bucket f from `cur`
-    auto step = [&](uint64_t (&cur)[WV_Q], uint64_t (&nxt)[WV_Q]) {
-        const int64_t fn = f + stride;
-        int64_t lo_n = 0, hi_n = 0;
-        if (fn < nbuckets) {
-            lo_n = starts[fn];
-            hi_n = starts[fn + 1];
-            wave_load_batch(nxt, in_h, lo_n, hi_n, lane);
-        }
-        if (lo != hi) {
-#pragma unroll
-            for (int k = 0; k < WV_SLOTS / WAVE; ++k) T[k * WAVE + lane] = EMPTY64;
-            __builtin_amdgcn_wave_barrier();
-            uint32_t fresh = 0;
-            if (hi - lo <= WV_BATCH) {
-                fresh = wave_insert_regs<false, DIRECT>(T, cur, lo, hi, lane, full);
-            } else {
-                for (int64_t rb = lo; rb < hi; rb += WV_BATCH) {
-                    if (rb != lo) wave_load_batch(cur, in_h, rb, hi, lane);
-                    fresh += wave_insert_regs<true, DIRECT>(T, cur, rb, hi, lane, full);
-                }
-            }
-            groups += fresh;
-            __builtin_amdgcn_wave_barrier();
-        }
-        lo = lo_n;
-        hi = hi_n;
-        f = fn;
-    };
-    while (f < nbuckets) {
-        step(hq, hn);
-        if (f >= nbuckets) break;
-        step(hn, hq);
-    }
-    groups = wave_sum_u64(groups);
-    const bool any_full = __any(full);
-    if (lane == 0) {
-        if (groups) atomicAdd((unsigned long long *)&stats[4 + (blockIdx.x & 63)], (unsigned long long)groups);
-        if (any_full) atomicOr((unsigned long long *)&stats[3], 1ull);
-    }
-}
-
-// Two-phase wave dedup (round 3; SDP_DEDUP_V2=0 selects the kernel above).
-// The register-queue loop above pays a dependent LDS round trip plus a shift of
+// Two-phase wave dedup (round 3).  The round-2 register-queue loop (each lane
+// walking its own queue of records, deleted in round 5) paid a dependent LDS round trip plus a shift of
 // its 20-record queue (40 VGPR moves) for every probe: PMC showed ~1300 VALU and
 // ~700 SALU instructions per ~1 K-record bucket against ~80 LDS instructions
 // (profiles/r03h_pmc_group_f64_norm.csv).
@@ -1745,6 +1636,11 @@ __global__ void __launch_bounds__(DT) part_dedup_bytes_kernel(const uint64_t *in
                 for (int q = 0; q < D_RPT; ++q) {
                     if (pos[q] < 0) continue;
                     const int p = pos[q];
+                    // a meta whose row lies outside the column (records that are
+                    // not what the caller described) is a collision: the caller
+                    // recounts exactly, and no representative row leaves here
+                    const int64_t row = (int64_t)(cur.meta[q] & RMASK40) - 1;
+                    if (row < 0 || row >= col.length) s_coll = 1;
                     bool eq;
                     if ((mine >> q) & 1u) {
                         eq = true;
@@ -2393,20 +2289,12 @@ int sdp_part_dedup(const sdp_records *in, int32_t is_bytes, const sdp_bytes_colu
                            nullptr, nullptr, nullptr, d_stats);
     } else {
         const int wgrid = grid_of((nbuckets + WV_W - 1) / WV_W, 256 * 16);
-        const char *e = getenv("SDP_DEDUP_V2");
-        const bool v2 = e == nullptr || e[0] != '0';          // SDP_DEDUP_V2=0: the register-queue kernel
-        if (v2 && (with_counts & 4))
+        if (with_counts & 4)            // near-unique keys: claim with one CAS, no read first
             hipLaunchKernelGGL(part_dedup_u64_wave2_kernel<1>, dim3(wgrid), dim3(WV_W * WAVE), 0, s, in->d_k0,
                                d_starts, nbuckets, d_ngroups, d_stats);
-        else if (v2)
+        else
             hipLaunchKernelGGL(part_dedup_u64_wave2_kernel<0>, dim3(wgrid), dim3(WV_W * WAVE), 0, s, in->d_k0,
                                d_starts, nbuckets, d_ngroups, d_stats);
-        else if (with_counts & 4)       // near-unique keys: claim with one CAS, no read first
-            hipLaunchKernelGGL(part_dedup_u64_wave_kernel<true>, dim3(wgrid), dim3(WV_W * WAVE), 0, s, in->d_k0,
-                               d_starts, nbuckets, d_stats);
-        else
-            hipLaunchKernelGGL(part_dedup_u64_wave_kernel<false>, dim3(wgrid), dim3(WV_W * WAVE), 0, s, in->d_k0,
-                               d_starts, nbuckets, d_stats);
     }
     return check_launch("part_dedup");
 }

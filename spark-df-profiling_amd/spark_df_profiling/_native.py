@@ -23,9 +23,20 @@ LIB_PATH = os.environ.get('SDP_LIBRARY', os.path.join(_HERE, 'lib', 'libsdp.so')
 MAX_WINDOWS = 5
 PASS1_WAVES = 4          # SDP_PASS1_WAVES
 PART_MAX_GRID = 1024     # SDP_PART_MAX_GRID
-HEAVY_MAX = 256
-HEAVY_MAX_REC = 1024         # byte keys on the records kernel (sdp_heavy.h HEAVY_MAX_REC)
 BITMAP_MAX_BITS = 1 << 20        # SDP_BITMAP_MAX_BITS
+
+# the grouping policy (include/sdp.h SDP_*), shared with the library's coarse
+# entries; _load() refuses a library built with other values
+ABI_VERSION = 5              # SDP_ABI_VERSION
+HEAVY_MAX = 256              # SDP_HEAVY_MAX: the row kernels' heavy-key tables
+HEAVY_MAX_REC = 1024         # SDP_HEAVY_MAX_REC: byte keys on the records kernel
+HEAVY_MIN = 3                # SDP_HEAVY_MIN
+PART_SAMPLE = 16384          # SDP_PART_SAMPLE
+PART_SAMPLE_BYTES = 65536    # SDP_PART_SAMPLE_BYTES
+PART_CHUNK = 131072          # SDP_PART_CHUNK
+GSORT_MAX = 8192             # SDP_GSORT_MAX
+BYTE_RECORD_ARRAYS = 3       # byte-key records: k0[], k1[], meta[] (sdp_records)
+RECORD_WORD = 8              # bytes between one record's words in each array
 
 # enum sdp_dtype
 I8, I16, I32, I64, F32, F64, U8, U16, U32, U64, BOOL = 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11
@@ -140,6 +151,45 @@ class SdpTopkResult(ctypes.Structure):             # sdp_topk_result (sdp_value_
 
 QUANTILES_MAX = 16       # SDP_QUANTILES_MAX
 
+LAYOUT_NSIZES = 17           # SDP_LAYOUT_NSIZES
+
+
+class SdpLayout(ctypes.Structure):                 # sdp_layout (sdp_layout_info)
+    _fields_ = [('abi_version', ctypes.c_int32), ('n_sizes', ctypes.c_int32),
+                ('byte_record_arrays', ctypes.c_int32), ('byte_record_stride', ctypes.c_int32),
+                ('fixed_record_bytes', ctypes.c_int32), ('heavy_max', ctypes.c_int32),
+                ('heavy_max_rec', ctypes.c_int32), ('heavy_min', ctypes.c_int32),
+                ('part_sample', ctypes.c_int32), ('part_sample_bytes', ctypes.c_int32),
+                ('gsort_max', ctypes.c_int32), ('_pad', ctypes.c_int32), ('part_chunk', ctypes.c_int64),
+                ('sizes', ctypes.c_int64 * LAYOUT_NSIZES)]
+
+
+# the structs in sdp_layout.sizes order
+_LAYOUT_STRUCTS = [SdpColumn, SdpBytesColumn, SdpRecords, SdpHeavy, SdpChunk, SdpQPlan, SdpPass1Result,
+                   SdpSelectTask, SdpCompactTask, SdpPass1Task, SdpPass2Task, SdpRowsTask, SdpPass2Result,
+                   SdpMinmaxResult, SdpDistinctResult, SdpTopkEntry, SdpTopkResult]
+
+
+def expected_layout():
+    """This binding's view of the library layout, as sdp_layout_info reports it."""
+    return {'abi_version': ABI_VERSION, 'n_sizes': LAYOUT_NSIZES, 'byte_record_arrays': BYTE_RECORD_ARRAYS,
+            'byte_record_stride': RECORD_WORD, 'fixed_record_bytes': RECORD_WORD, 'heavy_max': HEAVY_MAX,
+            'heavy_max_rec': HEAVY_MAX_REC, 'heavy_min': HEAVY_MIN, 'part_sample': PART_SAMPLE,
+            'part_sample_bytes': PART_SAMPLE_BYTES, 'gsort_max': GSORT_MAX, 'part_chunk': PART_CHUNK,
+            'sizes': [ctypes.sizeof(t) for t in _LAYOUT_STRUCTS]}
+
+
+def layout_mismatches(lib_layout):
+    """[(field, binding, library)] where a library's sdp_layout differs from this binding."""
+    want = expected_layout()
+    got = {k: getattr(lib_layout, k) for k in want if k != 'sizes'}
+    got['sizes'] = list(lib_layout.sizes)[:LAYOUT_NSIZES]
+    bad = [(k, want[k], got[k]) for k in want if k != 'sizes' and want[k] != got[k]]
+    for t, a, b in zip(_LAYOUT_STRUCTS, want['sizes'], got['sizes']):
+        if a != b:
+            bad.append(('sizeof(%s)' % t.__name__, a, b))
+    return bad
+
 _P = ctypes.c_void_p
 _I32 = ctypes.c_int32
 _I64 = ctypes.c_int64
@@ -154,6 +204,7 @@ _HVY = ctypes.POINTER(SdpHeavy)
 _SIGNATURES = {
     'sdp_last_error': (ctypes.c_char_p, []),
     'sdp_version': (ctypes.c_char_p, []),
+    'sdp_layout_info': (ctypes.c_int, [ctypes.POINTER(SdpLayout)]),
     'sdp_pass1_workspace_bytes': (_I64, [_I64, _I32]),
     'sdp_pass2_workspace_bytes': (_I64, [_I64, _I32, _I32]),
     'sdp_pass1_grid': (_I32, [_I64, _I32]),
@@ -166,6 +217,8 @@ _SIGNATURES = {
     'sdp_pass1_batch': (ctypes.c_int, [_P, _I32, _I32, _I32, _I32, _I32, _P]),
     'sdp_part_sample_batch': (ctypes.c_int, [_P, _I32, _I32, _P, _P]),
     'sdp_pass2_count_batch': (ctypes.c_int, [_P, _I32, _I32, _I32, _I32, _I32, _P]),
+    'sdp_pass2_gram_workspace_bytes': (_I64, [_I64, _I32]),
+    'sdp_pass2_gram': (ctypes.c_int, [_P, _P, _I32, ctypes.c_uint32, _P, _I64, _P, _P, _P, _P]),
     'sdp_part_rows_batch': (ctypes.c_int, [_P, _I32, _I32, _I32, _P]),
     'sdp_compact_candidates': (ctypes.c_int, [_P, _P, _I32, _I64, _P, _P, _P, _P]),
     'sdp_radix_hist': (ctypes.c_int, [_P, _P, _U64, _I32, _P, _P]),
@@ -245,7 +298,7 @@ _VALUE_FUNCS = {'sdp_last_error', 'sdp_version', 'sdp_pass1_workspace_bytes', 's
                 'sdp_scan_workspace_bytes', 'sdp_bitmap_workspace_bytes', 'sdp_select_kth_workspace_bytes',
                 'sdp_select_rounds', 'sdp_pass2_count_workspace_bytes', 'sdp_minmax_workspace_bytes',
                 'sdp_quantiles_workspace_bytes', 'sdp_distinct_workspace_bytes', 'sdp_value_counts_workspace_bytes',
-                'sdp_pearson_workspace_bytes', 'sdp_distinct32_workspace_bytes'}
+                'sdp_pearson_workspace_bytes', 'sdp_distinct32_workspace_bytes', 'sdp_pass2_gram_workspace_bytes'}
 _STATUS_FUNCS = set(_SIGNATURES) - _VALUE_FUNCS
 
 _lib = None
@@ -259,10 +312,23 @@ def _load():
         raise NativeError('libsdp.so not found at %s -- build it with `make -C spark-df-profiling_amd/csrc` '
                           '(or __graft_entry__.build()); there is no CPU fallback' % LIB_PATH)
     lib = ctypes.CDLL(LIB_PATH)
+    if not hasattr(lib, 'sdp_layout_info'):
+        raise NativeError('%s exports no sdp_layout_info: a library older than ABI %d -- rebuild it'
+                          % (LIB_PATH, ABI_VERSION))
     for name, (res, args) in _SIGNATURES.items():
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
+    # layout handshake: the structs, record layout and grouping policy the
+    # library was built with must be this binding's (a mismatched record layout
+    # once sent garbage row indices into a kernel)
+    lay = SdpLayout()
+    lib.sdp_layout_info(ctypes.byref(lay))
+    bad = layout_mismatches(lay)
+    if bad:
+        raise NativeError('%s was built for another layout (%s) -- rebuild it with '
+                          '`make -C spark-df-profiling_amd/csrc`' % (
+                              LIB_PATH, '; '.join('%s: binding %s, library %s' % b for b in bad)))
     _lib = lib
     return lib
 

@@ -454,14 +454,25 @@ def describe(df, bins=10, corr_reject=0.9, **kwargs):
         # their level-1 buckets (one column read fewer)
         # (a column found sorted in pass 1 already has its count: sdp_sorted_distinct)
         known = [p1.get('sorted_distinct') for p1 in p1s]
-        paths = engine.distinct_paths_sharded(num_cols, hints, bounds, n) if sharded else \
-            engine.distinct_paths(num_cols, hints, bounds)
+        # (date columns join the distinct batch: their distinct hint is the day range)
+        dcols = num_cols + date_cols
+        dhints = hints + [min(p1['n_valid'], p1['imax'] - p1['imin'] + 1) if p1['count'] else p1['n_valid']
+                          for p1 in date_p1]
+        dbounds = bounds + [(p1['imin'], p1['imax']) if p1['count'] else None for p1 in date_p1]
+        dknown = known + [None] * len(date_cols)
+        # every column's distinct path is chosen ONCE, here, before pass 2 and
+        # the grouping consume the pass-1 heavy-key samples it depends on; pass 2's
+        # pre-counts and the distinct batch both follow it
+        dpaths = engine.distinct_paths_sharded(dcols, dhints, dbounds, n) if sharded else \
+            engine.distinct_paths(dcols, dhints, dbounds)
+        paths = dpaths[:len(num_cols)]
         group_cols = {i for i, pth in enumerate(paths) if pth == 'group' and known[i] is None}
         # 32-bit key spaces (sdp_distinct32): pass 2 takes their level-1 count too
         count32_cols = {i: (bounds[i][0] if bounds[i] is not None else 0)
                         for i, pth in enumerate(paths) if pth == 'bits32' and known[i] is None}
         stats = engine.numeric_stats_batch(num_cols, packs, bins, [k_vals.get(c.name, 2) for c in num_cols],
-                                           group_cols=group_cols, gk=gk, count32_cols=count32_cols)
+                                           group_cols=group_cols, gk=gk, count32_cols=count32_cols,
+                                           corr=corr_reject is not None)
         to_plot = []
         for col, pack, st in zip(num_cols, packs, stats):
             bundles[col.name]['p1_pack'] = pack
@@ -473,15 +484,9 @@ def describe(df, bins=10, corr_reject=0.9, **kwargs):
                     to_plot.append((col.name, st))
         early_plots.update(zip([name for name, _ in to_plot], _submit_plots([st for _, st in to_plot])))
         # every NUM column's countDistinct with shared readbacks (and, sharded,
-        # shared collectives)
-        # (date columns join the batch: their distinct hint is the day range)
-        dcols = num_cols + date_cols
-        dhints = hints + [min(p1['n_valid'], p1['imax'] - p1['imin'] + 1) if p1['count'] else p1['n_valid']
-                          for p1 in date_p1]
-        dbounds = bounds + [(p1['imin'], p1['imax']) if p1['count'] else None for p1 in date_p1]
-        dknown = known + [None] * len(date_cols)
-        dist = engine.distinct_batch(dcols, dhints, dbounds, dknown) if not sharded else \
-            engine.distinct_batch_sharded(dcols, dhints, dbounds, dknown, n_all=n)
+        # shared collectives), on the paths chosen above
+        dist = engine.distinct_batch(dcols, dhints, dbounds, dknown, paths=dpaths) if not sharded else \
+            engine.distinct_batch_sharded(dcols, dhints, dbounds, dknown, n_all=n, paths=dpaths)
         for col, d in zip(dcols, dist):
             bundles[col.name]['distinct_pre'] = d
         # every string/binary/decimal column's value counts with shared

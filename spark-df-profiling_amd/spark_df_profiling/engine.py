@@ -42,23 +42,23 @@ SAMPLE2_TOTAL = 131072        # second sample narrowing the quantile windows (sd
 # the refine kernel's 16 K-key LDS sort; 0 disables)
 SAMPLE3_TOTAL = int(os.environ.get('SDP_SAMPLE3', 360448))
 SORT_MAX = 16384
-GSORT_MAX = 8192
+GSORT_MAX = nat.GSORT_MAX          # (sdp.h SDP_GSORT_MAX, checked at load)
 TOPK = 50                                       # describe.py:259
 EMPTY64 = 0xFFFFFFFFFFFFFFFF
 U64 = (1 << 64) - 1
-PART_SAMPLE = 16384          # rows sampled for heavy keys (sdp_part_sample)
+PART_SAMPLE = nat.PART_SAMPLE      # rows sampled for heavy keys (sdp_part_sample; SDP_PART_SAMPLE)
 # byte columns: up to HEAVY_MAX_REC heavy keys need a larger sample to be seen
 # HEAVY_MIN times (zipf(1.1) over 1e8 labels: the 1024th key holds ~6e-5 of the rows)
-PART_SAMPLE_BYTES = 65536
-HEAVY_MIN = 3                # sample occurrences that make a key heavy
+PART_SAMPLE_BYTES = nat.PART_SAMPLE_BYTES
+HEAVY_MIN = nat.HEAVY_MIN          # sample occurrences that make a key heavy
 # level-2 records per workgroup chunk: each chunk pays its header and bucket
 # offsets before its first tile (131072 vs 65536: f64 level-2 scatter 4.4-4.7
 # -> 4.1-4.3 ms per 1e9 records; 262144 loses on skewed columns,
 # profiles/r04z_part_chunk_ab.log)
-PART_CHUNK = 131072
+PART_CHUNK = nat.PART_CHUNK
 # byte columns: strings read once into compacted records, then a record scatter
-# (SDP_BYTES_TWO_READS=1: the count + re-read scatter of round 1, for A/B runs)
-BYTES_ONE_READ = os.environ.get('SDP_BYTES_TWO_READS', '0') != '1'
+# (columns too short for two levels, b1 = 0, take the count + scatter row kernels)
+BYTES_ONE_READ = True
 # pass 1 with inclusive quantile windows where the plan allows (SDP_PASS1_EXCL=1: never, for A/B runs)
 PASS1_INCLUSIVE = os.environ.get('SDP_PASS1_EXCL', '0') != '1'
 # SDP_PASS1_BATCH=0: one sdp_pass1 launch per column instead of one sdp_pass1_batch per dtype
@@ -198,6 +198,7 @@ class Engine:
         self._heavy_pre = None          # id(col) -> heavy keys sampled with pass 1
         self._near_unique = set()       # id(col) of columns >= 90 % distinct in that sample
         self._counted = {}              # id(col) -> group context whose level-1 count pass 2 did
+        self._fused_gram = None         # the Gram sdp_pass2_gram formed with pass 2 (gram() takes it)
         self._heavy_bytes_pre = {}      # id(col) -> byte column's heavy keys, sampled with pass 1
 
     # -- small helpers ----------------------------------------------------------
@@ -692,18 +693,106 @@ class Engine:
                 out[p] = key_to_float(values[lo_r])
         return out, st['fallback']
 
-    def pass2_batch(self, items, count_ctx=None):
+    # pass 2 of a table's NUM columns and their Pearson Gram in one read
+    # (sdp_pass2_gram; SDP_P2GRAM=0 keeps them apart, for A/B runs)
+    P2GRAM = os.environ.get('SDP_P2GRAM', '1') != '0'
+    P2GRAM_MAX_COLS = 16
+    P2GRAM_MAX_BINS = 10
+    P2GRAM_HEAVY_COLS = 2
+
+    @staticmethod
+    def _edges_monotone(edges):
+        return all(math.isfinite(float(x)) for x in edges) and all(
+            float(edges[j]) <= float(edges[j + 1]) for j in range(len(edges) - 1))
+
+    def _p2gram_ok(self, items, count_ctx):
+        """sdp_pass2_gram takes this table: <= 16 columns of f64/f32/i64/i32
+        of one length, 2..10 monotone finite bins, <= 2 heavy-key columns."""
+        if not self.P2GRAM or not 1 <= len(items) <= self.P2GRAM_MAX_COLS:
+            return False
+        n = items[0][0].length
+        heavy = 0
+        for i, (col, mean, edges, hi_t, lo_t) in enumerate(items):
+            if (col.kind != 'fixed' or col.dtype not in (nat.F64, nat.F32, nat.I64, nat.I32) or col.length != n
+                    or col.values.data_ptr() % 16 or not 2 <= len(edges) <= self.P2GRAM_MAX_BINS
+                    or not self._edges_monotone(edges)):
+                return False
+            ctx = count_ctx.get(i)
+            if ctx is not None and not ctx.get('d32'):
+                if not 0 <= ctx['b1'] <= 10:
+                    return False
+                if ctx['hv'] is not None and ctx['hv']['n'] > 0:
+                    if ctx['hv']['n'] > nat.HEAVY_MAX:
+                        return False
+                    heavy += 1
+            if ctx is not None and ctx.get('d32') and col.dtype == nat.F64:
+                return False
+        return heavy <= self.P2GRAM_HEAVY_COLS
+
+    def _pass2_gram(self, items, count_ctx, gram_mask):
+        """pass2_batch through sdp_pass2_gram: one launch reads every column
+        once for pass 2, the level-1 counts of count_ctx and the Pearson Gram
+        of the columns gram_mask marks (kept for gram())."""
+        s = self._s()
+        rsz = ctypes.sizeof(nat.SdpPass2Result)
+        n = items[0][0].length
+        rpb = sdp.sdp_part_rows_per_block(max(n, 1), 0)
+        grid = max(1, -(-n // rpb))
+        none = nat.SdpHeavy(None, None, None, None, 0, 0)
+        outs, tasks = [], []
+        for i, (col, mean, edges, hi_t, lo_t) in enumerate(items):
+            bins = len(edges)
+            e = self._h2d(np.array([float(x) for x in edges], dtype=np.float64))
+            res, hist = self._bytes(rsz), self._u64(bins)
+            work = self._bytes(sdp.sdp_pass2_count_workspace_bytes(col.length, bins))
+            ctx = count_ctx.get(i)
+            if ctx is None:
+                b1, ph, hc, st, hv, lo = -2, None, None, None, none, 0
+            else:
+                hvd = ctx['hv']
+                b1, ph, hc, st = ctx['b1'], ctx['h1'], ctx['hcnt'], ctx['stats']
+                hv = hvd['struct'] if hvd else none
+                lo = int(ctx.get('lo', 0))
+                self._counted[id(col)] = ctx
+            tasks.append(nat.SdpPass2Task(col.sdp(), e.data_ptr(), float(mean), float(hi_t), float(lo_t),
+                                          work.data_ptr(), res.data_ptr(), hist.data_ptr(), hv,
+                                          ph.data_ptr() if ph is not None else None,
+                                          hc.data_ptr() if hc is not None else None,
+                                          st.data_ptr() if st is not None else None,
+                                          rpb, bins, 1, b1, grid, lo))
+            outs.append((res, hist, e, work))
+        C = len(items)
+        arr = (nat.SdpPass2Task * C)(*tasks)
+        d_tasks = self._h2d(np.frombuffer(bytearray(bytes(arr)), dtype=np.uint8))
+        gw = self._bytes(sdp.sdp_pass2_gram_workspace_bytes(n, C))
+        G = torch.empty(C * C, dtype=torch.float64, device=self.device)
+        cs = torch.empty(C, dtype=torch.float64, device=self.device)
+        nn = torch.empty(1, dtype=torch.float64, device=self.device)
+        mask = sum(1 << i for i, g in enumerate(gram_mask) if g)
+        nat.annotate('table', sum(col_read_bytes(c) for c, _, _, _, _ in items))
+        sdp.sdp_pass2_gram(arr, ptr(d_tasks), C, mask, ptr(gw), gw.numel(), ptr(G), ptr(cs), ptr(nn), s)
+        idx = [i for i, g in enumerate(gram_mask) if g]
+        self._fused_gram = {'ids': [id(items[i][0]) for i in idx], 'shifts': [float(items[i][1]) for i in idx],
+                            'idx': idx, 'C': C, 'G': G, 's': cs, 'n': nn, 'keep': (d_tasks, gw, arr)}
+        return self._pass2_results(outs)
+
+    def pass2_batch(self, items, count_ctx=None, gram_mask=None):
         """[(col, mean, edges, hi_t, lo_t)] -> [pass-2 dict] (see pass2), all
         launched back to back and read back once (sharded: one all-reduce of
         every column's counts and bins, one all-gather of the mad partials).
         count_ctx[i] (a _group_prepare context) makes column i's launch also do
         the level-1 count of its distinct-count partitioning (sdp_pass2_count);
-        the context is then kept for group_batch."""
+        the context is then kept for group_batch.  gram_mask[i]: column i is in
+        the Pearson matrix (utils.py:27-31) -- when the table fits
+        sdp_pass2_gram, that one launch also forms the Gram gram() returns."""
         if not items:
             return []
+        count_ctx = count_ctx or {}
+        self._fused_gram = None
+        if gram_mask is not None and any(gram_mask) and self._p2gram_ok(items, count_ctx):
+            return self._pass2_gram(items, count_ctx, gram_mask)
         s = self._s()
         rsz = ctypes.sizeof(nat.SdpPass2Result)
-        count_ctx = count_ctx or {}
         outs = []
         batched = []               # (kind, SdpPass2Task, col): counted columns launched together below
         for i, (col, mean, edges, hi_t, lo_t) in enumerate(items):
@@ -754,6 +843,7 @@ class Engine:
                 mg = max(t.grid for t, _ in grp)
                 for t, c in grp:      # sdp_pass2_count's own argument checks (the table is device memory)
                     if (c.values.data_ptr() % 16 or not -1 <= t.b1 <= 10 or t.heavy.n > nat.HEAVY_MAX
+                            or (t.b1 == -1 and c.dtype not in (nat.F32,) + self.BITS32_DTYPES)
                             or t.grid > mg or mg > nat.PART_MAX_GRID):
                         raise nat.NativeError('pass2_count_batch: a task fails the sdp_pass2_count checks')
                 arr = (nat.SdpPass2Task * len(grp))(*[t for t, _ in grp])
@@ -761,6 +851,12 @@ class Engine:
                 nat.annotate(_label(grp[0][1], 'batch'), sum(col_read_bytes(c) for _, c in grp))
                 sdp.sdp_pass2_count_batch(ptr(d_tasks), len(grp), dtype, bins, mono, mg, s)
                 keep_tasks.append(d_tasks)
+        return self._pass2_results(outs)
+
+    def _pass2_results(self, outs):
+        """The pass-2 dicts of launched columns [(res, hist, edges, work)]: one
+        readback (sharded: one all-gather)."""
+        rsz = ctypes.sizeof(nat.SdpPass2Result)
         if not self.comm.sharded:
             raw = torch.cat([t for res, hist, _, _ in outs for t in (res[:rsz], hist.view(torch.uint8))]).cpu().numpy()
             result, off = [], 0
@@ -890,7 +986,7 @@ class Engine:
         return {p: float(v) for p, v in zip(probs, out.cpu().numpy())}
 
     def numeric_stats_batch(self, cols, packs, bins=10, ks=None, probs=PROBS, group_cols=(), gk=None,
-                            count32_cols=None):
+                            count32_cols=None, corr=False):
         """numeric_stats of every column (None for a column with no non-null
         value) with two host readbacks in all.  A bins value the reference
         rejects (describe.py:46 with bins=1) is recorded per column and raised
@@ -956,7 +1052,12 @@ class Engine:
                     self._group_prepare(cols[i], False)
                 if ctx is not None:
                     count_ctx[j] = ctx
-        for i, r2 in zip(p2_idx, self.pass2_batch(p2_items, count_ctx)):
+        # corr=True: the Pearson matrix will be asked for the NUM columns,
+        # i.e. those with more than one distinct value (describe.py:156), which
+        # pass 1 already tells: no value, or one value and no NaN, is CONST
+        gram_mask = [not (stats[i].count == 0 or (stats[i].min == stats[i].max and stats[i].n_nan == 0))
+                     for i in p2_idx] if corr else None
+        for i, r2 in zip(p2_idx, self.pass2_batch(p2_items, count_ctx, gram_mask)):
             st = stats[i]
             st.mad = r2['abs_dev_sum']
             st.hist_counts = r2['hist']
@@ -1301,6 +1402,8 @@ class Engine:
         ctxs = []
         for c in cols:
             pre = self._counted.pop(id(c), None)           # counted by pass 2 (sdp_pass2_count)
+            if pre is not None and pre.get('d32'):         # a 32-bit-path count: not this path's
+                pre = None
             if pre is None:
                 pre = self._group_prepare(c, False)
                 if pre is not None:
@@ -1750,7 +1853,7 @@ class Engine:
         count32_cols), the column is read once here instead of twice."""
         pre = self._counted.pop(id(col), None)
         h1 = None
-        if pre is not None and pre.get('d32'):
+        if pre is not None and pre.get('d32'):              # (a partitioning-path count is dropped)
             h1, out = pre['h1'], pre['stats']
         else:
             out = self._u64(2, zero=True)
@@ -1760,15 +1863,19 @@ class Engine:
         sdp.sdp_distinct32(ctypes.byref(cs), int(lo), ptr(h1), ptr(work), work.numel(), ptr(out), self._s())
         return out
 
-    def distinct_batch(self, cols, hints, bounds, known=None):
+    def distinct_batch(self, cols, hints, bounds, known=None, paths=None):
         """countDistinct of several NUM/DATE columns (describe.py:143) with
         the path choice of describe._distinct_count / distinct_fixed per column
         and the host readbacks shared: LDS bitmaps for small integral ranges
         (one readback for all), hash partitioning for the rest (group_batch).
         `bounds[i]` = (imin, imax) for integral columns with values, else None.
-        Single rank only; returns [distinct count]."""
+        `paths`: the caller's distinct_paths of these columns, taken before
+        pass 2 consumed the heavy-key samples the choice reads (describe()
+        passes them, so pass 2's pre-counts and this batch agree); computed
+        here when absent.  Single rank only; returns [distinct count]."""
         out = list(known) if known is not None else [None] * len(cols)     # sorted columns: counted
-        paths = self.distinct_paths(cols, hints, bounds)
+        if paths is None:
+            paths = self.distinct_paths(cols, hints, bounds)
         bm = [i for i, pth in enumerate(paths) if pth == 'bitmap' and out[i] is None]
         b32 = [i for i, pth in enumerate(paths) if pth == 'bits32' and out[i] is None]
         grp = [i for i, pth in enumerate(paths) if pth == 'group' and out[i] is None]
@@ -1825,6 +1932,8 @@ class Engine:
         ctxs = []
         for col in cols:                                  # level 1 counts of every column, no readback
             ctx = self._counted.pop(id(col), None)        # counted by pass 2 (sdp_pass2_count)
+            if ctx is not None and (ctx.get('d32') or not ctx.get('sharded')):
+                ctx = None                                # another path's count: recount
             if ctx is None:
                 ctx = self._group_prepare_sharded(col)
                 if ctx['n']:
@@ -1978,7 +2087,7 @@ class Engine:
                 out.append('group')
         return out
 
-    def distinct_batch_sharded(self, cols, hints, bounds, known=None, n_all=None):
+    def distinct_batch_sharded(self, cols, hints, bounds, known=None, n_all=None, paths=None):
         """distinct_batch on a row-sharded table (every rank calls it with the
         same columns; hints/bounds come from the merged pass 1): bitmaps for
         small integral ranges, the global-table exchange for small key ranges,
@@ -1989,7 +2098,9 @@ class Engine:
                                                         device=self.device)).item()) if cols else 0
         out = list(known) if known is not None else [None] * len(cols)     # sorted columns: counted
         grp, bitmaps = [], []
-        for i, (col, pth) in enumerate(zip(cols, self.distinct_paths_sharded(cols, hints, bounds, n_all))):
+        if paths is None:
+            paths = self.distinct_paths_sharded(cols, hints, bounds, n_all)
+        for i, (col, pth) in enumerate(zip(cols, paths)):
             bd = bounds[i]
             if out[i] is not None:
                 continue
@@ -2489,6 +2600,13 @@ class Engine:
             return out
         bounds = []
         for j, src, rows, col in live:
+            # representative rows come from record metas the kernels wrote: one
+            # outside the column means the records were not what the library
+            # was told (sdp_part_dedup flags those as collisions); never gather it
+            if min(rows) < 0 or max(rows) >= src.length:
+                raise nat.NativeError('representative row %d outside the %d-row column %r (record layout '
+                                      'mismatch?)' % (min(rows) if min(rows) < 0 else max(rows), src.length,
+                                                      src.name))
             if src.fixed_width:
                 w = src.fixed_width
                 st = torch.tensor([r * w for r in rows], dtype=torch.int64)
@@ -2543,6 +2661,15 @@ class Engine:
     # Pearson (utils.py:20-36)
     # ==========================================================================
     def gram(self, cols: List[DeviceColumn], shifts, check_nan):
+        fg, self._fused_gram = getattr(self, '_fused_gram', None), None
+        if fg is not None and fg['ids'] == [id(c) for c in cols] and fg['shifts'] == [float(x) for x in shifts]:
+            # formed by pass 2's read (sdp_pass2_gram) for exactly these columns
+            C, idx = fg['C'], torch.tensor(fg['idx'], dtype=torch.int64, device=self.device)
+            G = fg['G'].view(C, C).index_select(0, idx).index_select(1, idx).reshape(-1)
+            packed = self.comm.allreduce_sum(torch.cat([G, fg['s'].index_select(0, idx), fg['n']]))
+            host = packed.cpu().numpy()
+            k = len(cols)
+            return host[:k * k].reshape(k, k), host[k * k:k * k + k], float(host[-1])
         n = cols[0].length
         C = len(cols)
         arr = (nat.SdpColumn * C)(*[c.sdp() for c in cols])

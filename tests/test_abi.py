@@ -136,3 +136,39 @@ def test_c_caller_compiles_against_header():
     src = os.path.join(ROOT, 'examples', 'c_caller', 'sdp_profile.c')
     subprocess.run(['gcc', '-std=c11', '-Wall', '-Werror', '-fsyntax-only', '-D__HIP_PLATFORM_AMD__',
                     '-I/opt/rocm/include', '-I' + os.path.join(ROOT, 'include'), src], check=True)
+
+
+def test_layout_handshake():
+    """The loaded library reports the binding's layout and grouping policy
+    (SDP_ABI_VERSION, record layout, struct sizes); a library that differs
+    would be refused at load."""
+    from spark_df_profiling import _native
+    _native._load()                       # (raises on a mismatch)
+    lay = _native.SdpLayout()
+    assert _native.sdp.sdp_layout_info(ctypes.byref(lay)) == 0
+    assert _native.layout_mismatches(lay) == []
+    assert lay.abi_version == _native.ABI_VERSION and lay.heavy_max_rec == 1024
+    # a library built with another record layout / policy / struct size is named
+    lay.byte_record_stride = 24
+    lay.heavy_max = 128
+    lay.sizes[1] += 8
+    bad = {b[0] for b in _native.layout_mismatches(lay)}
+    assert bad == {'byte_record_stride', 'heavy_max', 'sizeof(SdpBytesColumn)'}
+
+
+def test_policy_constants_come_from_the_header():
+    """One grouping policy: engine.py's constants are _native's, which are
+    sdp.h's SDP_* values (checked against the library at load)."""
+    from spark_df_profiling import _native, engine
+    text = open(HEADER).read()
+    for c, v in (('SDP_HEAVY_MAX', _native.HEAVY_MAX), ('SDP_HEAVY_MAX_REC', _native.HEAVY_MAX_REC),
+                 ('SDP_HEAVY_MIN', _native.HEAVY_MIN), ('SDP_PART_SAMPLE', _native.PART_SAMPLE),
+                 ('SDP_PART_SAMPLE_BYTES', _native.PART_SAMPLE_BYTES), ('SDP_PART_CHUNK', _native.PART_CHUNK),
+                 ('SDP_GSORT_MAX', _native.GSORT_MAX), ('SDP_ABI_VERSION', _native.ABI_VERSION)):
+        m = re.search(r'#define %s\s+(\d+)' % c, text)
+        assert m and int(m.group(1)) == v, c
+    assert (engine.PART_SAMPLE, engine.PART_SAMPLE_BYTES, engine.HEAVY_MIN, engine.PART_CHUNK, engine.GSORT_MAX) == \
+        (_native.PART_SAMPLE, _native.PART_SAMPLE_BYTES, _native.HEAVY_MIN, _native.PART_CHUNK, _native.GSORT_MAX)
+    # sdp_api.cpp keeps no copies of its own
+    api = open(os.path.join(ROOT, 'spark-df-profiling_amd', 'csrc', 'sdp_api.cpp')).read()
+    assert not re.search(r'constexpr\s+\w+\s+(HEAVY_N|HEAVY_MIN|PART_SAMPLE\w*|PART_CHUNK|GSORT_MAX)\s*=\s*\d', api)

@@ -165,13 +165,12 @@ def _dedup_buckets(buckets, flags):
     return int(st[4:68].sum()), int(st[3])
 
 
-@pytest.mark.parametrize('v2', ['0', '1'])
 @pytest.mark.parametrize('direct', [0, 4])
-def test_wave_dedup_kernels(v2, direct, monkeypatch):
-    """Both wave dedup kernels (SDP_DEDUP_V2) on crafted final buckets: single and
-    multi-batch buckets, duplicates, keys sharing one home slot (collision list
-    and its overflow past 448 entries), empty buckets."""
-    monkeypatch.setenv('SDP_DEDUP_V2', v2)
+def test_wave_dedup_kernels(direct):
+    """The two-phase wave dedup (read-first and direct-CAS modes) on crafted
+    final buckets: single and multi-batch buckets, duplicates, keys sharing
+    one home slot (collision list and its overflow past 448 entries), empty
+    buckets."""
     g = datagen.rng(7)
     b = []
     for _ in range(300):                                   # ordinary buckets with repeats
@@ -297,3 +296,60 @@ def test_wide_short_tables_keep_fused_partitioning():
     paths = e.distinct_paths(dt.columns, [n] * 9, [None] * 9)
     assert paths == ['group'] * 9
     assert e.distinct_paths(dt.columns[:3], [n] * 3, [None] * 3) == ['bits32'] * 3
+
+
+def test_byte_dedup_out_of_range_metas():
+    """Byte records whose metas point outside the column (records that are not
+    what the library was told, e.g. a layout mismatch between engine and
+    library) are flagged as a collision by sdp_part_dedup -- never read -- and
+    the exact recount on the global table gives the right groups."""
+    import ctypes
+    import torch
+    from collections import Counter
+    from spark_df_profiling import _native as nat
+    from spark_df_profiling._native import sdp, ptr
+    g = datagen.rng(11)
+    base = ['k%03d' % i for i in range(300)] + ['a long string of more than sixteen bytes #%03d' % i
+                                               for i in range(200)]
+    vals = [base[i] for i in g.integers(0, len(base), 6000)]
+    e, col = _engine_groups(pa.array(vals, type=pa.large_string()))
+    bc = col.sdp_bytes()
+    dev, s = e.device, nat.stream_handle()
+    n = col.length
+    rpb = sdp.sdp_part_rows_per_block(n, 1)
+    grid = max(1, -(-n // rpb))
+    h1 = torch.zeros(grid, dtype=torch.int32, device=dev)
+    st0 = torch.zeros(68, dtype=torch.int64, device=dev)
+    sdp.sdp_part_rows(None, ctypes.byref(bc), None, 0, 0, ptr(h1), None, None, None, ptr(st0), s)
+    offs = e._scan(h1)
+    nrec = int(offs[-1].item())
+    assert nrec == n
+    k0, k1, meta = (torch.empty(nrec, dtype=torch.int64, device=dev) for _ in range(3))
+    rec = nat.SdpRecords(k0.data_ptr(), k1.data_ptr(), meta.data_ptr())
+    sdp.sdp_part_rows(None, ctypes.byref(bc), None, 0, 1, None, ptr(offs), ctypes.byref(rec), None, ptr(st0), s)
+    starts = torch.tensor([0, nrec], dtype=torch.int64, device=dev)
+
+    def dedup():
+        st = torch.zeros(68, dtype=torch.int64, device=dev)
+        ok, oc = (torch.empty(nrec, dtype=torch.int64, device=dev) for _ in range(2))
+        ng = torch.zeros(1, dtype=torch.int32, device=dev)
+        sdp.sdp_part_dedup(ctypes.byref(rec), 1, ctypes.byref(bc), ptr(starts), 1, 1, ptr(ok), ptr(oc), ptr(ng),
+                           ptr(st), s)
+        return st.cpu().numpy()
+
+    good = dedup()
+    assert good[2] == 0 and good[3] == 0 and int(good[4:].sum()) == len(set(vals))
+    # metas with row indices past the column (and one below it) on long and short keys
+    bad_rows = torch.arange(0, nrec, 7, device=dev)
+    meta[bad_rows] += 1 << 39
+    meta[3] = meta[3] & ~((1 << 40) - 1)                 # row index -1
+    bad = dedup()
+    torch.cuda.synchronize()
+    assert bad[2] != 0                                    # collision: the caller recounts exactly
+    tab = e.value_counts_bytes_table(col)                 # the exact recount
+    m = tab['groups']
+    assert m == len(set(vals))
+    assert int(tab['rows']) == n
+    want = Counter(vals)
+    assert sorted(want.values()) == sorted(int(c) for c in
+                                           tab['counts'][:tab['capacity']].cpu().numpy() if c > 0)

@@ -102,6 +102,17 @@ def spark_int_percentile(sorted_at, n, p):
     return (hi - pos) * float(xl) + (pos - lo) * float(xh)
 
 
+def accumulated_edges(vmin, vmax, bins):
+    """describe.py:38-45: bin_width = (max - min) / float(bins); left edges by
+    repeated addition from min, the last one popped."""
+    width = (vmax - vmin) / float(bins)
+    edges = [vmin]
+    for _ in range(bins):
+        edges.append(edges[-1] + width)
+    edges.pop()
+    return edges
+
+
 def float_rank(n, p):
     if p <= 1e-4:
         return 1
@@ -156,8 +167,17 @@ def check_numeric(name, col, st, row, nrows, uniq=None, counts=None, problems=No
     nz = int(((x.double() == 0.0) & valid).sum().item())
     if int(row['n_zeros']) != nz:
         bad('n_zeros', int(row['n_zeros']), nz)
-    # histogram: CASE-WHEN bins from the host-accumulated edges
-    ge = [int((xs >= float(e)).sum().item()) for e in st.edges]
+    # histogram: CASE-WHEN bins from edges accumulated here from the checked
+    # min / max (describe.py:40-45: integral columns subtract as int64), not
+    # from the engine's own edges
+    if col.is_float:
+        vmin, vmax = float(xs.min().item()), float(xs.max().item())
+    else:
+        vmin, vmax = int(x[valid].min().item()), int(x[valid].max().item())
+    edges = accumulated_edges(vmin, vmax, len(st.hist_counts))
+    if [float(e) for e in st.edges] != [float(e) for e in edges]:
+        bad('histogram edges', [float(e) for e in st.edges], [float(e) for e in edges])
+    ge = [int((xs >= float(e)).sum().item()) for e in edges]
     want = [ge[j] - ge[j + 1] for j in range(len(ge) - 1)] + [ge[-1]]
     if list(map(int, st.hist_counts)) != want:
         bad('histogram', list(map(int, st.hist_counts)), want)
