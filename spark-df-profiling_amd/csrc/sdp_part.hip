@@ -1525,6 +1525,167 @@ __global__ void __launch_bounds__(WV_W * WAVE) part_dedup_u64_wave2_kernel(const
     }
 }
 
+// Half-space wave dedup (round 5).  The two-phase kernel above is latency
+// bound at two waves per SIMD (its 16 KB table per wave caps a CU at 8 waves;
+// SQ counters: wait 0.51 of wave cycles, VALU busy 0.15).  Here a wave takes
+// its bucket's records once into registers and groups them in two passes,
+// one per value of hash bit 10, each in a 1024-slot (8 KB) table indexed by
+// bits 0..9: the same records, keys and linear probing (a key lives in exactly
+// one half, so the halves' group counts add), but 4 KB of list and 8 KB of
+// table per wave -- four 4-wave workgroups, 16 waves per CU.  Same-box A/B per
+// 1e9-row column (profiles/r05f_dedup_half_ab.log): f64 N(0,1) (direct CAS)
+// 4.59 -> 3.94 ms; repeated keys lose (i64 zipf 3.73 -> 4.94, f32 2.55 -> 2.71:
+// the second pass's loop overhead outweighs the occupancy), so the read-first
+// mode keeps the 2048-slot kernel.
+constexpr int WH_SLOTS = 1024;
+constexpr int WH_Q = 16;                        // records per lane per batch (1024 per wave)
+constexpr int WH_BATCH = WH_Q * WAVE;
+constexpr int WH_OVF = 256;                     // collision-list entries per wave (2 KB)
+__device__ __forceinline__ void wave_load_batch16(uint64_t (&hq)[WH_Q], const uint64_t *in_h, int64_t rb, int64_t hi,
+                                                  int lane) {
+#pragma unroll
+    for (int q = 0; q < WH_Q; ++q) {
+        const int64_t r = rb + (int64_t)q * WAVE + lane;
+        hq[q] = r < hi ? in_h[r] : EMPTY64;
+    }
+}
+template <int MODE, bool LIMIT>
+__device__ __forceinline__ uint32_t wh_probe(uint64_t *T, uint64_t x, bool &full) {
+    uint32_t pos = ((uint32_t)x + 1u) & (WH_SLOTS - 1);
+    for (int probes = 1;; ++probes) {
+        uint64_t cur;
+        if (MODE == 1) {
+            cur = atomicCAS((unsigned long long *)&T[pos], (unsigned long long)EMPTY64, (unsigned long long)x);
+        } else {
+            cur = T[pos];
+            if (cur == EMPTY64)
+                cur = atomicCAS((unsigned long long *)&T[pos], (unsigned long long)EMPTY64, (unsigned long long)x);
+        }
+        if (cur == EMPTY64) return 1u;
+        if (cur == x) return 0u;
+        pos = (pos + 1) & (WH_SLOTS - 1);
+        if (LIMIT && probes >= WH_SLOTS / 2) { full = true; return 0u; }
+    }
+}
+// the records of half `hb` (hash bit 10) among this lane's batch -> new groups
+template <int MODE, bool LIMIT>
+__device__ __forceinline__ uint32_t wh_insert(uint64_t *T, uint64_t *O, const uint64_t (&hq)[WH_Q],
+                                              const uint64_t *in_h, int64_t rb, int64_t hi, int lane, uint32_t hb,
+                                              bool &full) {
+    const int64_t rem = hi - rb - lane;
+    const int left = rem <= 0 ? 0 : (int)min((int64_t)WH_Q, (rem + WAVE - 1) / WAVE);
+    uint64_t cur[WH_Q];
+    uint32_t mine = 0;
+#pragma unroll
+    for (int q = 0; q < WH_Q; ++q) {
+        const uint64_t x = hq[q];
+        const bool v = q < left && (((uint32_t)(x >> 10)) & 1u) == hb;
+        mine |= (v ? 1u : 0u) << q;
+        uint64_t c = 0;
+        if (v) {
+            uint64_t *p = &T[(uint32_t)x & (WH_SLOTS - 1)];
+            c = MODE == 1 ? (uint64_t)atomicCAS((unsigned long long *)p, (unsigned long long)EMPTY64,
+                                                (unsigned long long)x)
+                          : *p;
+        }
+        cur[q] = c;
+    }
+    if (MODE == 0) {
+#pragma unroll
+        for (int q = 0; q < WH_Q; ++q)
+            if (((mine >> q) & 1u) && cur[q] == EMPTY64)
+                cur[q] = atomicCAS((unsigned long long *)&T[(uint32_t)hq[q] & (WH_SLOTS - 1)],
+                                   (unsigned long long)EMPTY64, (unsigned long long)hq[q]);
+    }
+    uint32_t fresh = 0, late = 0, nov = 0;
+#pragma unroll
+    for (int q = 0; q < WH_Q; ++q) {
+        const bool v = (mine >> q) & 1u;
+        fresh += (v && cur[q] == EMPTY64) ? 1u : 0u;
+        const bool coll = v && cur[q] != EMPTY64 && cur[q] != hq[q];
+        const uint64_t m = __ballot(coll);
+        if (m) {
+            const uint32_t slot = nov + (uint32_t)lane_rank(m);
+            if (coll) {
+                if (slot < (uint32_t)WH_OVF) O[slot] = hq[q];
+                else late |= 1u << q;
+            }
+            nov += (uint32_t)__popcll(m);
+        }
+    }
+    if (nov == 0) return fresh;
+    nov = min(nov, (uint32_t)WH_OVF);
+    __builtin_amdgcn_wave_barrier();
+    uint32_t j = lane;
+    uint64_t nx = j < nov ? O[j] : 0;
+    while (j < nov) {
+        const uint64_t x = nx;
+        j += WAVE;
+        nx = j < nov ? O[j] : 0;
+        fresh += wh_probe<MODE, LIMIT>(T, x, full);
+    }
+    while (late) {
+        const int q = __builtin_ctz(late);
+        late &= late - 1;
+        fresh += wh_probe<MODE, LIMIT>(T, in_h[rb + (int64_t)q * WAVE + lane], full);
+    }
+    __builtin_amdgcn_wave_barrier();
+    return fresh;
+}
+template <int MODE>
+__global__ void __launch_bounds__(WV_W * WAVE, 4) part_dedup_u64_half_kernel(const uint64_t *in_h,
+                                                                             const uint64_t *starts,
+                                                                             int64_t nbuckets, uint32_t *ngroups,
+                                                                             uint64_t *stats) {
+    // (no next-bucket prefetch in registers: 16 waves per CU hide the loads)
+    __shared__ uint64_t tab[WV_W][WH_SLOTS];
+    __shared__ uint64_t lst[WV_W][WH_OVF];
+    const int lane = lane_id(), w = threadIdx.x / WAVE;
+    uint64_t *T = tab[w];
+    uint64_t *O = lst[w];
+    uint64_t groups = 0;
+    bool full = false;
+    const int64_t stride = (int64_t)gridDim.x * WV_W;
+    for (int64_t f = (int64_t)blockIdx.x * WV_W + w; f < nbuckets; f += stride) {
+        const int64_t lo = starts[f], hi = starts[f + 1];
+        uint32_t fresh = 0;
+        if (lo != hi) {
+            uint64_t hq[WH_Q];
+            wave_load_batch16(hq, in_h, lo, hi, lane);
+            const bool one = hi - lo <= WH_BATCH;
+#pragma unroll 1
+            for (uint32_t hb = 0; hb < 2; ++hb) {
+                ulonglong2 *T2 = (ulonglong2 *)T;
+#pragma unroll
+                for (int k = 0; k < WH_SLOTS / (2 * WAVE); ++k) T2[k * WAVE + lane] = make_ulonglong2(EMPTY64, EMPTY64);
+                __builtin_amdgcn_wave_barrier();
+                if (one) {
+                    fresh += wh_insert<MODE, false>(T, O, hq, in_h, lo, hi, lane, hb, full);
+                } else {
+                    // (a bucket beyond one batch: its batches are re-read from L2 per half)
+#pragma unroll 1
+                    for (int64_t rb = lo; rb < hi; rb += WH_BATCH) {
+                        if (rb != lo || hb) wave_load_batch16(hq, in_h, rb, hi, lane);
+                        fresh += wh_insert<MODE, true>(T, O, hq, in_h, rb, hi, lane, hb, full);
+                    }
+                }
+                __builtin_amdgcn_wave_barrier();
+            }
+        }
+        groups += fresh;
+        if (ngroups != nullptr) {
+            const uint32_t bucket = (uint32_t)wave_sum_u64(fresh);
+            if (lane == 0) ngroups[f] = bucket;
+        }
+    }
+    groups = wave_sum_u64(groups);
+    const bool any_full = __any(full);
+    if (lane == 0) {
+        if (groups) atomicAdd((unsigned long long *)&stats[4 + (blockIdx.x & 63)], (unsigned long long)groups);
+        if (any_full) atomicOr((unsigned long long *)&stats[3], 1ull);
+    }
+}
+
 // Byte keys, in rounds of DT * 4 records held in registers:
 //   1. claim a slot per distinct hash (CAS on h)        2. the claimant writes
 //   its record into the slot    3. everyone compares bytes and counts.
@@ -2289,10 +2450,10 @@ int sdp_part_dedup(const sdp_records *in, int32_t is_bytes, const sdp_bytes_colu
                            nullptr, nullptr, nullptr, d_stats);
     } else {
         const int wgrid = grid_of((nbuckets + WV_W - 1) / WV_W, 256 * 16);
-        if (with_counts & 4)            // near-unique keys: claim with one CAS, no read first
-            hipLaunchKernelGGL(part_dedup_u64_wave2_kernel<1>, dim3(wgrid), dim3(WV_W * WAVE), 0, s, in->d_k0,
+        if (with_counts & 4)            // near-unique keys: one CAS per probe, half-space tables
+            hipLaunchKernelGGL(part_dedup_u64_half_kernel<1>, dim3(wgrid), dim3(WV_W * WAVE), 0, s, in->d_k0,
                                d_starts, nbuckets, d_ngroups, d_stats);
-        else
+        else                            // repeated keys: read-first probes, 2048-slot tables
             hipLaunchKernelGGL(part_dedup_u64_wave2_kernel<0>, dim3(wgrid), dim3(WV_W * WAVE), 0, s, in->d_k0,
                                d_starts, nbuckets, d_ngroups, d_stats);
     }
