@@ -491,16 +491,20 @@ def gram_roofline(rec, steps, ncols, n_rows, traffic_path=None, rows=None):
 
 
 class ReadbackCensus:
-    """Counts the device->host readbacks describe() makes while active (device
-    tensors read by .cpu() / .item() / .tolist() / .to('cpu')): each waits for
-    the stream, i.e. sits on the step's critical path.  (Host->device copies
-    are staged through pinned memory without a wait and are not counted.)
-    Run on the last warmup step, outside the timed region."""
+    """Counts the blocking host syncs describe() makes while active: device->host
+    readbacks (device tensors read by .cpu() / .item() / .tolist() / .to('cpu'))
+    and pageable host->device copies (torch.tensor(..., device=cuda), .to(cuda) /
+    .cuda() of a host tensor without non_blocking from pinned memory): PyTorch
+    synchronises the stream after either, so each sits on the step's critical
+    path.  (The engine's own uploads go through pinned memory with
+    non_blocking=True and are not counted.)  Run on the last warmup step,
+    outside the timed region."""
 
     def __init__(self):
         self.count = 0
+        self.h2d = 0
         self._saved = []
-        # SDP_READBACK_SITES=1: also tally the package line each readback comes from
+        # SDP_READBACK_SITES=1: also tally the package line each sync comes from
         self.sites = {} if os.environ.get('SDP_READBACK_SITES') == '1' else None
 
     def _site(self):
@@ -510,30 +514,54 @@ class ReadbackCensus:
                 return '%s:%d %s' % (os.path.basename(fr.filename), fr.lineno, fr.name)
         return '?'
 
+    def _note(self, kind):
+        if kind == 'h2d':
+            self.h2d += 1
+        else:
+            self.count += 1
+        if self.sites is not None:
+            key = '%s %s' % (kind, self._site())
+            self.sites[key] = self.sites.get(key, 0) + 1
+
     def _wrap(self, owner, name, pred):
         orig = getattr(owner, name)
         census = self
 
         def f(*a, **k):
-            if pred(*a, **k):
-                census.count += 1
-                if census.sites is not None:
-                    key = census._site()
-                    census.sites[key] = census.sites.get(key, 0) + 1
+            kind = pred(*a, **k)
+            if kind:
+                census._note(kind)
             return orig(*a, **k)
         self._saved.append((owner, name, orig))
         setattr(owner, name, f)
 
     def __enter__(self):
+        def is_cuda(dev):
+            return dev is not None and not isinstance(dev, torch.dtype) and str(dev).startswith('cuda')
+
         def to_pred(t, *a, **k):
             dev = k.get('device', a[0] if a else None)
+            if isinstance(dev, torch.Tensor):
+                dev = dev.device
             if isinstance(dev, torch.dtype) or dev is None:
-                return False
-            return t.is_cuda and str(dev).startswith('cpu')
-        self._wrap(torch.Tensor, 'cpu', lambda t, *a, **k: t.is_cuda)
-        self._wrap(torch.Tensor, 'item', lambda t, *a, **k: t.is_cuda)
-        self._wrap(torch.Tensor, 'tolist', lambda t, *a, **k: t.is_cuda)
+                return None
+            if t.is_cuda and str(dev).startswith('cpu'):
+                return 'readback'
+            if not t.is_cuda and is_cuda(dev) and not (k.get('non_blocking') and t.is_pinned()):
+                return 'h2d'
+            return None
+
+        def cuda_pred(t, *a, **k):
+            return 'h2d' if not t.is_cuda and not (k.get('non_blocking') and t.is_pinned()) else None
+
+        def tensor_pred(*a, **k):
+            return 'h2d' if is_cuda(k.get('device')) else None
+        self._wrap(torch.Tensor, 'cpu', lambda t, *a, **k: 'readback' if t.is_cuda else None)
+        self._wrap(torch.Tensor, 'item', lambda t, *a, **k: 'readback' if t.is_cuda else None)
+        self._wrap(torch.Tensor, 'tolist', lambda t, *a, **k: 'readback' if t.is_cuda else None)
         self._wrap(torch.Tensor, 'to', to_pred)
+        self._wrap(torch.Tensor, 'cuda', cuda_pred)
+        self._wrap(torch, 'tensor', tensor_pred)
         return self
 
     def __exit__(self, *exc):
@@ -673,15 +701,15 @@ def main():
     def step(raw=None):
         return describe(table, comm=comm, plots=not args.no_plots, raw=raw, workers=args.workers)
 
-    readbacks = None
+    readbacks = h2d_syncs = None
     for i in range(args.warmup):
         if i == args.warmup - 1:
             with ReadbackCensus() as census:
                 step()
-            readbacks = census.count
+            readbacks, h2d_syncs = census.count, census.h2d
             if census.sites is not None and rank == 0:
                 for k, v in sorted(census.sites.items(), key=lambda kv: -kv[1]):
-                    print('readback site %3d  %s' % (v, k), file=sys.stderr)
+                    print('sync site %3d  %s' % (v, k), file=sys.stderr)
         else:
             step()
 
@@ -754,6 +782,7 @@ def main():
         'roofline': rl,
         'whole_profile': rl.get('whole_profile'),
         'host_readbacks_per_step': readbacks,
+        'host_blocking_h2d_per_step': h2d_syncs,
         'per_kernel': per_kernel,
         'quantile_candidates_frac': {'max': max(cand.values()) if cand else None,
                                      'mean': round(sum(cand.values()) / len(cand), 4) if cand else None},

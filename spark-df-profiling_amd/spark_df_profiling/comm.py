@@ -25,6 +25,17 @@ from typing import List
 import torch
 
 
+def to_dev(data, dtype, device):
+    """A host list / array as a device tensor without a stream sync: staged in
+    pinned memory and copied with non_blocking=True (torch.tensor(...,
+    device=cuda) from pageable memory synchronises the stream after the copy,
+    i.e. waits for every kernel queued before it)."""
+    t = torch.as_tensor(data, dtype=dtype)
+    if torch.device(device).type != 'cuda':
+        return t.to(device)
+    return t.pin_memory().to(device, non_blocking=True)
+
+
 class LocalComm:
     rank = 0
     world = 1
@@ -107,7 +118,7 @@ class TorchComm:
     def allgatherv(self, t):
         """all_gather of 1-D tensors whose lengths differ per rank."""
         self.calls['allgatherv'] += 1
-        n = torch.tensor([t.numel()], dtype=torch.int64, device=t.device)
+        n = torch.full((1,), t.numel(), dtype=torch.int64, device=t.device)
         sizes = [int(s.item()) for s in self.allgather(n)]
         m = max(sizes) if sizes else 0
         pad = torch.zeros(m, dtype=t.dtype, device=t.device)
@@ -140,7 +151,7 @@ class TorchComm:
         # gloo runs the same all_to_all_single calls on host copies, so the
         # CPU tests exercise exactly the split logic RCCL sees
         dev = send.device
-        counts = self._io(torch.tensor(send_counts, dtype=torch.int64, device=dev))
+        counts = self._io(to_dev(send_counts, torch.int64, dev))
         recv_counts = torch.empty_like(counts)
         self.dist.all_to_all_single(recv_counts, counts, group=self.group)
         return self.alltoallv_known(send, send_counts, recv_counts.tolist())
@@ -176,17 +187,43 @@ class TorchComm:
         self.calls['alltoall_counts'] += 1
         k = len(rows)
         dev = torch.device('cpu') if self.cpu else torch.device('cuda', torch.cuda.current_device())
-        send = torch.tensor(rows, dtype=torch.int64).t().contiguous().to(dev)     # [world, k]
+        send = to_dev(torch.tensor(rows, dtype=torch.int64).t().contiguous(), torch.int64, dev)   # [world, k]
         recv = torch.empty_like(send)
         self.dist.all_to_all_single(recv, send, group=self.group)
         r = recv.cpu().tolist()
         return [[r[src][j] for src in range(self.world)] for j in range(k)]
 
+    # bytes of a pickled object that ride the first all-gather round; a larger
+    # object on any rank costs a second round sized by the largest
+    OBJECT_CAP = 1 << 16
+
     def allgather_object(self, obj):
+        """all_gather_object in one tensor collective and ONE readback in the
+        common case: every rank sends [size | pickled bytes padded to
+        OBJECT_CAP] from pinned memory (no stream sync on the way in); torch's
+        all_gather_object pays a pageable upload and two readbacks (sizes, then
+        data).  A rank whose payload exceeds the cap makes every rank run a
+        second round of the largest size."""
+        import pickle
+        import numpy as np
         self.calls['allgather_object'] += 1
-        out = [None] * self.world
-        self.dist.all_gather_object(out, obj, group=self.group)
-        return out
+        payload = pickle.dumps(obj, protocol=pickle.HIGHEST_PROTOCOL)
+        dev = torch.device('cpu') if self.cpu else torch.device('cuda', torch.cuda.current_device())
+
+        def round_(cap):
+            buf = np.zeros(8 + cap, dtype=np.uint8)
+            buf[:8] = np.frombuffer(np.int64(len(payload)).tobytes(), dtype=np.uint8)
+            m = min(cap, len(payload))
+            buf[8:8 + m] = np.frombuffer(payload[:m], dtype=np.uint8)
+            t = to_dev(buf, torch.uint8, dev)
+            outs = [torch.empty_like(t) for _ in range(self.world)]
+            self.dist.all_gather(outs, t, group=self.group)
+            return torch.stack(outs).cpu().numpy()
+        got = round_(self.OBJECT_CAP)
+        sizes = [int(np.frombuffer(r[:8].tobytes(), dtype=np.int64)[0]) for r in got]
+        if max(sizes) > self.OBJECT_CAP:
+            got = round_(max(sizes))
+        return [pickle.loads(r[8:8 + sz].tobytes()) for r, sz in zip(got, sizes)]
 
     def barrier(self):
         self.calls['barrier'] += 1

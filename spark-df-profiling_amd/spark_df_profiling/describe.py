@@ -404,7 +404,7 @@ def describe(df, bins=10, corr_reject=0.9, **kwargs):
         gk = {'partitions': partitions, 'accuracy': accuracy}
     import torch
     n_local = table.num_rows
-    n = int(engine.comm.allreduce_sum(torch.tensor([n_local], dtype=torch.int64, device=engine.device)).item())
+    n = int(engine.comm.allreduce_sum(torch.full((1,), n_local, dtype=torch.int64, device=engine.device)).item())
     table_stats = {'n': n}
     if n == 0:
         raise ValueError('df cannot be empty')

@@ -23,6 +23,7 @@ import torch
 
 from . import _native as nat
 from ._native import sdp, ptr
+from .comm import to_dev
 
 MASK40 = (1 << 40) - 1
 
@@ -69,8 +70,8 @@ def exchange_fixed_groups(engine, tab, with_counts):
     col = DeviceColumn('_exchange', 'bigint', int(rkeys.numel()), 'fixed', nat.U64)
     col.values = rkeys if rkeys.numel() else torch.zeros(2, dtype=torch.int64, device=engine.device)
     local = engine._distinct_fixed_table(col, with_counts=with_counts, row_counts=rcnt, exchanged=True)
-    side = torch.tensor([tab['max_key_rows'], tab['rows'], local['groups'] - (1 if local['max_key_rows'] else 0)],
-                        dtype=torch.int64, device=engine.device)
+    side = to_dev([tab['max_key_rows'], tab['rows'], local['groups'] - (1 if local['max_key_rows'] else 0)],
+                  torch.int64, engine.device)
     tot = comm.allreduce_sum(side).tolist()
     max_rows, rows, owner_groups = int(tot[0]), int(tot[1]), int(tot[2])
     local['groups_local'] = local['groups'] - (1 if local['max_key_rows'] else 0)
@@ -175,7 +176,7 @@ def exchange_bytes_groups_batch(engine, tabs):
         local['col'] = rc
         locals_.append(local)
         sides += [tab['rows'], local['groups']]
-    t = comm.allreduce_sum(torch.tensor(sides, dtype=torch.int64, device=engine.device)).tolist()
+    t = comm.allreduce_sum(to_dev(sides, torch.int64, engine.device)).tolist()
     for j, local in enumerate(locals_):
         local['groups_local'] = local['groups']
         local['groups'] = int(t[2 * j + 1])

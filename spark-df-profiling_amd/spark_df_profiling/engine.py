@@ -32,7 +32,7 @@ import torch
 
 from . import _native as nat
 from ._native import sdp, ptr
-from .comm import LocalComm
+from .comm import LocalComm, to_dev
 from .columns import DeviceColumn, decimal_from_key
 
 PROBS = (0.05, 0.25, 0.5, 0.75, 0.95)          # describe.py:207
@@ -220,8 +220,7 @@ class Engine:
 
     def _to_dev(self, struct):
         raw = bytes(struct)
-        t = torch.frombuffer(bytearray(raw), dtype=torch.uint8)
-        return t.to(self.device)
+        return to_dev(np.frombuffer(bytearray(raw), dtype=np.uint8), torch.uint8, self.device)
 
     def _h2d(self, arr):
         """Host numpy array -> device tensor without a host round trip: staged
@@ -352,7 +351,7 @@ class Engine:
         """All-gather the per-rank pass-1 states and merge them in rank order."""
         if not self.comm.sharded:
             return merge_pass1_results([local])
-        raw = torch.frombuffer(bytearray(bytes(local)), dtype=torch.uint8).to(self.device)
+        raw = to_dev(np.frombuffer(bytearray(bytes(local)), dtype=np.uint8), torch.uint8, self.device)
         parts = [nat.SdpPass1Result.from_buffer_copy(p.cpu().numpy().tobytes()) for p in self.comm.allgather(raw)]
         return merge_pass1_results(parts)
 
@@ -394,7 +393,7 @@ class Engine:
         mine = cur[:n_local]
         parts = self.comm.allgatherv(mine)
         allk = torch.cat(parts) if len(parts) > 1 else mine.clone()
-        nn = torch.tensor([allk.numel()], dtype=torch.int64, device=self.device)
+        nn = torch.full((1,), allk.numel(), dtype=torch.int64, device=self.device)
         buf = self._u64(max(allk.numel(), 1))
         buf[:allk.numel()] = allk
         sdp.sdp_sort_small(ptr(buf), ptr(nn), self._s())
@@ -453,9 +452,9 @@ class Engine:
                     'n_unbinned': int(r.n_unbinned), 'hist': raw[sz:].view(np.int64).astype(np.int64)}
         r = self._read(res, nat.SdpPass2Result)
         # merge ranks: counts sum exactly; abs-dev sums gathered and added in rank order
-        vec = torch.tensor([r.n_high, r.n_low, r.n_unbinned], dtype=torch.int64, device=self.device)
+        vec = to_dev([r.n_high, r.n_low, r.n_unbinned], torch.int64, self.device)
         vec = self.comm.allreduce_sum(torch.cat([vec, hist]))
-        mads = self.comm.allgather(torch.tensor([r.abs_dev_sum], dtype=torch.float64, device=self.device))
+        mads = self.comm.allgather(torch.full((1,), r.abs_dev_sum, dtype=torch.float64, device=self.device))
         v = vec.cpu().numpy()
         return {'abs_dev_sum': math.fsum(float(m.item()) for m in mads), 'n_high': int(v[0]), 'n_low': int(v[1]),
                 'n_unbinned': int(v[2]), 'hist': v[3:].astype(np.int64)}
@@ -1803,9 +1802,9 @@ class Engine:
                 extra_c.append(special)
             if extra_k:
                 m = len(extra_k)
-                keys[groups_local:groups_local + m] = torch.tensor(
-                    np.array(extra_k, dtype=np.uint64).view(np.int64), device=self.device)
-                counts[groups_local:groups_local + m] = torch.tensor(extra_c, dtype=torch.int64, device=self.device)
+                keys[groups_local:groups_local + m] = to_dev(np.array(extra_k, dtype=np.uint64).view(np.int64),
+                                                            torch.int64, self.device)
+                counts[groups_local:groups_local + m] = to_dev(extra_c, torch.int64, self.device)
             tab.update({'slots': keys, 'counts': counts, 'capacity': max(total, 1)})
         return tab
 
@@ -1925,7 +1924,7 @@ class Engine:
         B1 = self.SHARDED_B1
         nb1 = 1 << B1
         if n_all is None:                                 # (the caller usually knows the table's rows)
-            n_all = int(comm.allreduce_sum(torch.tensor([cols[0].length], dtype=torch.int64,
+            n_all = int(comm.allreduce_sum(torch.full((1,), cols[0].length, dtype=torch.int64,
                                                          device=self.device)).item())
         target = sdp.sdp_part_bucket_target(0, 0)
         b2 = min(10, max(1, math.ceil(math.log2(max(2.0, n_all / nb1 / target)))))
@@ -2096,7 +2095,7 @@ class Engine:
         group_sharded_batch for the rest (shared round trips)."""
         comm = self.comm
         if n_all is None:                                 # (describe() passes the table's global rows)
-            n_all = int(comm.allreduce_sum(torch.tensor([cols[0].length if cols else 0], dtype=torch.int64,
+            n_all = int(comm.allreduce_sum(torch.full((1,), cols[0].length if cols else 0, dtype=torch.int64,
                                                         device=self.device)).item()) if cols else 0
         out = list(known) if known is not None else [None] * len(cols)     # sorted columns: counted
         grp, bitmaps = [], []
@@ -2165,7 +2164,7 @@ class Engine:
         cache-resident and wins there (23 vs 44 ms)."""
         n = col.length
         if self.comm.sharded:         # the path choice must agree on every rank: decide on the global rows
-            n = int(self.comm.allreduce_sum(torch.tensor([n], dtype=torch.int64, device=self.device)).item())
+            n = int(self.comm.allreduce_sum(torch.full((1,), n, dtype=torch.int64, device=self.device)).item())
         small_range = capacity_hint is not None and capacity_hint * 4 <= max(n, 1)
         if not self.comm.sharded and not small_range and col.length >= (1 << 16):
             tab = self.group(col, with_counts, dense=with_counts)
@@ -2537,7 +2536,7 @@ class Engine:
         cache = tab.get('_slotval', {})
         need = [sl for sl in slot_list if sl is not None and sl not in cache]
         if need:
-            idx = torch.tensor(need, dtype=torch.int64, device=self.device)
+            idx = to_dev(need, torch.int64, self.device)
             cache = dict(cache)
             cache.update(zip(need, self._host_u64(tab['slots'][idx])))
         if not tab['bytes']:
@@ -2581,10 +2580,10 @@ class Engine:
             for r in rows:
                 b = col.bit_offset + r
                 bits.append(b)
-            byts = vb[torch.tensor([b // 8 for b in bits], dtype=torch.int64, device=self.device)].cpu().tolist()
+            byts = vb[to_dev([b // 8 for b in bits], torch.int64, self.device)].cpu().tolist()
             return [bool((x >> (b % 8)) & 1) for x, b in zip(byts, bits)]
         tv = typed_values(col)
-        v = tv[torch.tensor(rows, dtype=torch.int64, device=self.device)].cpu().numpy()
+        v = tv[to_dev(rows, torch.int64, self.device)].cpu().numpy()
         if col.dtype == nat.U64:
             v = v.view(np.uint64)
         elif col.dtype == nat.U32:
@@ -2612,9 +2611,9 @@ class Engine:
             if src.fixed_width:
                 w = src.fixed_width
                 st = torch.tensor([r * w for r in rows], dtype=torch.int64)
-                bounds.append(torch.cat([st, st + w]).to(self.device))
+                bounds.append(to_dev(torch.cat([st, st + w]), torch.int64, self.device))
             else:
-                ri = torch.tensor(rows, dtype=torch.int64, device=self.device)
+                ri = to_dev(rows, torch.int64, self.device)
                 o = src.offsets
                 bounds.append(torch.cat([o[ri], o[ri + 1]]).to(torch.int64))
         se = torch.cat(bounds).cpu().tolist()                    # one readback of every bound
@@ -2625,7 +2624,7 @@ class Engine:
             off += 2 * m
             pos = np.concatenate([np.arange(a, b, dtype=np.int64) for a, b in zip(starts, ends)])
             if pos.size:
-                gathers.append(src.data[torch.from_numpy(pos).to(self.device)])
+                gathers.append(src.data[to_dev(pos, torch.int64, self.device)])
             spans.append((j, col, starts, ends, int(pos.size)))
         flat = torch.cat(gathers).cpu().numpy().tobytes() if gathers else b''   # one readback of all bytes
         p = 0
@@ -2645,12 +2644,12 @@ class Engine:
             starts = [r * w for r in rows]
             ends = [s + w for s in starts]
         else:
-            ri = torch.tensor(rows, dtype=torch.int64, device=self.device)
+            ri = to_dev(rows, torch.int64, self.device)
             o = src.offsets
             se = torch.cat([o[ri], o[ri + 1]]).to(torch.int64).cpu().tolist()    # one readback
             starts, ends = se[:len(rows)], se[len(rows):]
         pos = np.concatenate([np.arange(a, b, dtype=np.int64) for a, b in zip(starts, ends)]) if rows else []
-        flat = src.data[torch.from_numpy(pos).to(self.device)].cpu().numpy().tobytes() if len(pos) else b''
+        flat = src.data[to_dev(pos, torch.int64, self.device)].cpu().numpy().tobytes() if len(pos) else b''
         out = []
         p = 0
         for a, b in zip(starts, ends):
@@ -2666,7 +2665,7 @@ class Engine:
         fg, self._fused_gram = getattr(self, '_fused_gram', None), None
         if fg is not None and fg['ids'] == [id(c) for c in cols] and fg['shifts'] == [float(x) for x in shifts]:
             # formed by pass 2's read (sdp_pass2_gram) for exactly these columns
-            C, idx = fg['C'], torch.tensor(fg['idx'], dtype=torch.int64, device=self.device)
+            C, idx = fg['C'], to_dev(fg['idx'], torch.int64, self.device)
             G = fg['G'].view(C, C).index_select(0, idx).index_select(1, idx).reshape(-1)
             packed = self.comm.allreduce_sum(torch.cat([G, fg['s'].index_select(0, idx), fg['n']]))
             host = packed.cpu().numpy()
@@ -2680,7 +2679,7 @@ class Engine:
         keep = torch.empty((n + 31) // 32 + 1, dtype=torch.int32, device=self.device)
         nat.annotate('', sum(n / 8.0 for c in cols if c.validity is not None))
         sdp.sdp_rowmask(arr, cn, C, ptr(work), work.numel(), ptr(keep), self._s())
-        sh = torch.tensor([float(x) for x in shifts], dtype=torch.float64, device=self.device)
+        sh = to_dev([float(x) for x in shifts], torch.float64, self.device)
         G = torch.empty(C * C, dtype=torch.float64, device=self.device)
         s = torch.empty(C, dtype=torch.float64, device=self.device)
         nn = torch.empty(1, dtype=torch.float64, device=self.device)

@@ -46,6 +46,9 @@ def _worker(rank, world, port, q):
         for part in comm.allgather_object(dict(imgs)):
             imgs.update(part)
         out['images'] = sorted(imgs.items())
+        # an object beyond the one-round cap on one rank: the second round
+        big = {'rank': rank, 'blob': bytes([rank]) * (comm.OBJECT_CAP * 2 if rank == 1 else 10)}
+        out['big'] = [(o['rank'], len(o['blob']), o['blob'][:1]) for o in comm.allgather_object(big)]
         # alltoallv (all_to_all_single, as on RCCL): rank r sends (r*10 + d) repeated d+1 times to rank d
         send = torch.cat([torch.full((d + 1,), rank * 10 + d, dtype=torch.int64) for d in range(world)])
         out['alltoallv'] = comm.alltoallv(send, [d + 1 for d in range(world)]).tolist()
@@ -90,6 +93,8 @@ def test_two_rank_merges():
         assert o['allreduce'] == [3]
         assert o['allreduce_'] == (True, 5, 5, 3, 13)
         assert o['images'] == [('c0', ('h0', 'm0')), ('c1', ('h1', 'm1'))]
+        from spark_df_profiling.comm import TorchComm
+        assert o['big'] == [(0, 10, b'\x00'), (1, 2 * TorchComm.OBJECT_CAP, b'\x01')]
         want = []
         for src in range(world):
             want += [src * 10 + r] * (r + 1)
