@@ -518,24 +518,6 @@ typedef struct sdp_pass2_task {
 int sdp_pass2_count_batch(const sdp_pass2_task *d_tasks, int32_t ntasks, int32_t dtype, int32_t bins,
                           int32_t edges_monotone, int32_t max_grid, void *stream);
 
-/* Pass 2 of every NUM column of a table (<= 16 columns of SDP_F64 / SDP_F32 /
- * SDP_I64 / SDP_I32, one length, 2..10 monotone bins) AND the Pearson Gram of
- * the columns in gram_mask (utils.py:27-31: listwise deletion over those
- * columns, shift = each task's mean) in ONE read of the table.  Per column the
- * outputs are sdp_pass2_count_batch's (d_result, d_hist, and -- b1 >= 0 or
- * b1 = -1 -- the level-1 count outputs; b1 = -2: no count); the Gram's are
- * sdp_gram's (d_gram ntasks x ntasks, d_colsum, *d_n: kept rows; entries of
- * columns outside gram_mask are 0).  Every task: rows_per_block and grid of
- * sdp_part_rows_per_block(length, 0), its d_work of
- * sdp_pass2_count_workspace_bytes.  h_tasks and d_tasks hold the same tasks
- * (host copy: argument checks and LDS layout; device copy: the kernel).  At
- * most two columns may carry heavy keys (SDP_ECAP otherwise).
- * Stream-ordered.  Replaces describe.py:215-223 + :49 of every NUM column and
- * utils.py:29-31. */
-int64_t sdp_pass2_gram_workspace_bytes(int64_t length, int32_t ncols);
-int sdp_pass2_gram(const sdp_pass2_task *h_tasks, const sdp_pass2_task *d_tasks, int32_t ntasks,
-                   uint32_t gram_mask, void *d_work, int64_t work_bytes, double *d_gram, double *d_colsum,
-                   double *d_n, void *stream);
 
 /* Packs the key bytes of n groups -- bytes [d_starts[i], d_starts[i] + d_lens[i])
  * of d_data -- at d_out + d_offs[i] (the sharded string exchange's payload). */

@@ -782,13 +782,6 @@ static int64_t align256(int64_t x) { return (x + 255) / 256 * 256; }
 
 using namespace sdp;
 
-int launch_gram_reduce16(const double *part_g, const double *part_cs, const double *part_n, int ncols, int S,
-                         double *d_gram, double *d_colsum, double *d_n, void *stream) {
-    hipLaunchKernelGGL(gram_reduce_kernel<16>, dim3(16 * 16 / R_EB), dim3(R_EB * R_P), 0, (hipStream_t)stream, part_g,
-                       part_cs, part_n, ncols, 1, 1, S, d_gram, d_colsum, d_n);
-    return check_launch("gram_reduce_kernel");
-}
-
 extern "C" int64_t sdp_gram_workspace_bytes(int64_t length, int32_t ncols) {
     if (ncols < 1 || length < 0) return -1;
     const GramGeom g = gram_geom(length, ncols);

@@ -2308,11 +2308,6 @@ extern "C" int sdp_pass2_count_batch(const sdp_pass2_task *d_tasks, int32_t ntas
     return check_launch("pass2_merge_batch_kernel");
 }
 
-int launch_pass2_merge_batch(const sdp_pass2_task *d_tasks, int ntasks, void *stream) {
-    hipLaunchKernelGGL(pass2_merge_batch_kernel, dim3(ntasks), dim3(MERGE_T), 0, (hipStream_t)stream, d_tasks);
-    return check_launch("pass2_merge_batch_kernel");
-}
-
 extern "C" int sdp_pass2(const sdp_column *col, double mean, const double *d_edges, int32_t bins,
                          int32_t edges_monotone, double hi_t, double lo_t, void *d_work, int64_t work_bytes,
                          sdp_pass2_result *d_result, uint64_t *d_hist, void *stream) {

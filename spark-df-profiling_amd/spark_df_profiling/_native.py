@@ -217,8 +217,6 @@ _SIGNATURES = {
     'sdp_pass1_batch': (ctypes.c_int, [_P, _I32, _I32, _I32, _I32, _I32, _P]),
     'sdp_part_sample_batch': (ctypes.c_int, [_P, _I32, _I32, _P, _P]),
     'sdp_pass2_count_batch': (ctypes.c_int, [_P, _I32, _I32, _I32, _I32, _I32, _P]),
-    'sdp_pass2_gram_workspace_bytes': (_I64, [_I64, _I32]),
-    'sdp_pass2_gram': (ctypes.c_int, [_P, _P, _I32, ctypes.c_uint32, _P, _I64, _P, _P, _P, _P]),
     'sdp_part_rows_batch': (ctypes.c_int, [_P, _I32, _I32, _I32, _P]),
     'sdp_compact_candidates': (ctypes.c_int, [_P, _P, _I32, _I64, _P, _P, _P, _P]),
     'sdp_radix_hist': (ctypes.c_int, [_P, _P, _U64, _I32, _P, _P]),
@@ -298,7 +296,7 @@ _VALUE_FUNCS = {'sdp_last_error', 'sdp_version', 'sdp_pass1_workspace_bytes', 's
                 'sdp_scan_workspace_bytes', 'sdp_bitmap_workspace_bytes', 'sdp_select_kth_workspace_bytes',
                 'sdp_select_rounds', 'sdp_pass2_count_workspace_bytes', 'sdp_minmax_workspace_bytes',
                 'sdp_quantiles_workspace_bytes', 'sdp_distinct_workspace_bytes', 'sdp_value_counts_workspace_bytes',
-                'sdp_pearson_workspace_bytes', 'sdp_distinct32_workspace_bytes', 'sdp_pass2_gram_workspace_bytes'}
+                'sdp_pearson_workspace_bytes', 'sdp_distinct32_workspace_bytes'}
 _STATUS_FUNCS = set(_SIGNATURES) - _VALUE_FUNCS
 
 _lib = None

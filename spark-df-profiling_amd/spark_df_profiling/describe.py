@@ -471,8 +471,7 @@ def describe(df, bins=10, corr_reject=0.9, **kwargs):
         count32_cols = {i: (bounds[i][0] if bounds[i] is not None else 0)
                         for i, pth in enumerate(paths) if pth == 'bits32' and known[i] is None}
         stats = engine.numeric_stats_batch(num_cols, packs, bins, [k_vals.get(c.name, 2) for c in num_cols],
-                                           group_cols=group_cols, gk=gk, count32_cols=count32_cols,
-                                           corr=corr_reject is not None)
+                                           group_cols=group_cols, gk=gk, count32_cols=count32_cols)
         to_plot = []
         for col, pack, st in zip(num_cols, packs, stats):
             bundles[col.name]['p1_pack'] = pack

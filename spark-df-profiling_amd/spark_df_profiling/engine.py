@@ -198,7 +198,6 @@ class Engine:
         self._heavy_pre = None          # id(col) -> heavy keys sampled with pass 1
         self._near_unique = set()       # id(col) of columns >= 90 % distinct in that sample
         self._counted = {}              # id(col) -> group context whose level-1 count pass 2 did
-        self._fused_gram = None         # the Gram sdp_pass2_gram formed with pass 2 (gram() takes it)
         self._heavy_bytes_pre = {}      # id(col) -> byte column's heavy keys, sampled with pass 1
 
     # -- small helpers ----------------------------------------------------------
@@ -692,106 +691,16 @@ class Engine:
                 out[p] = key_to_float(values[lo_r])
         return out, st['fallback']
 
-    # pass 2 of a table's NUM columns and their Pearson Gram in one read
-    # (sdp_pass2_gram).  Off by default: measured slower than the separate
-    # launches (C3 1e9: 109.8 vs 51 ms); SDP_P2GRAM=1
-    # enables it, tests/test_gpu_p2gram.py checks it either way
-    P2GRAM = os.environ.get('SDP_P2GRAM', '0') == '1'
-    P2GRAM_MAX_COLS = 16
-    P2GRAM_MAX_BINS = 10
-    P2GRAM_HEAVY_COLS = 2
-
-    @staticmethod
-    def _edges_monotone(edges):
-        return all(math.isfinite(float(x)) for x in edges) and all(
-            float(edges[j]) <= float(edges[j + 1]) for j in range(len(edges) - 1))
-
-    def _p2gram_ok(self, items, count_ctx):
-        """sdp_pass2_gram takes this table: <= 16 columns of f64/f32/i64/i32
-        of one length, 2..10 monotone finite bins, <= 2 heavy-key columns."""
-        if not self.P2GRAM or not 1 <= len(items) <= self.P2GRAM_MAX_COLS:
-            return False
-        n = items[0][0].length
-        heavy = 0
-        for i, (col, mean, edges, hi_t, lo_t) in enumerate(items):
-            if (col.kind != 'fixed' or col.dtype not in (nat.F64, nat.F32, nat.I64, nat.I32) or col.length != n
-                    or col.values.data_ptr() % 16 or not 2 <= len(edges) <= self.P2GRAM_MAX_BINS
-                    or not self._edges_monotone(edges)):
-                return False
-            ctx = count_ctx.get(i)
-            if ctx is not None and not ctx.get('d32'):
-                if not 0 <= ctx['b1'] <= 10:
-                    return False
-                if ctx['hv'] is not None and ctx['hv']['n'] > 0:
-                    if ctx['hv']['n'] > nat.HEAVY_MAX:
-                        return False
-                    heavy += 1
-            if ctx is not None and ctx.get('d32') and col.dtype == nat.F64:
-                return False
-        return heavy <= self.P2GRAM_HEAVY_COLS
-
-    def _pass2_gram(self, items, count_ctx, gram_mask):
-        """pass2_batch through sdp_pass2_gram: one launch reads every column
-        once for pass 2, the level-1 counts of count_ctx and the Pearson Gram
-        of the columns gram_mask marks (kept for gram())."""
-        s = self._s()
-        rsz = ctypes.sizeof(nat.SdpPass2Result)
-        n = items[0][0].length
-        rpb = sdp.sdp_part_rows_per_block(max(n, 1), 0)
-        grid = max(1, -(-n // rpb))
-        none = nat.SdpHeavy(None, None, None, None, 0, 0)
-        outs, tasks = [], []
-        for i, (col, mean, edges, hi_t, lo_t) in enumerate(items):
-            bins = len(edges)
-            e = self._h2d(np.array([float(x) for x in edges], dtype=np.float64))
-            res, hist = self._bytes(rsz), self._u64(bins)
-            work = self._bytes(sdp.sdp_pass2_count_workspace_bytes(col.length, bins))
-            ctx = count_ctx.get(i)
-            if ctx is None:
-                b1, ph, hc, st, hv, lo = -2, None, None, None, none, 0
-            else:
-                hvd = ctx['hv']
-                b1, ph, hc, st = ctx['b1'], ctx['h1'], ctx['hcnt'], ctx['stats']
-                hv = hvd['struct'] if hvd else none
-                lo = int(ctx.get('lo', 0))
-                self._counted[id(col)] = ctx
-            tasks.append(nat.SdpPass2Task(col.sdp(), e.data_ptr(), float(mean), float(hi_t), float(lo_t),
-                                          work.data_ptr(), res.data_ptr(), hist.data_ptr(), hv,
-                                          ph.data_ptr() if ph is not None else None,
-                                          hc.data_ptr() if hc is not None else None,
-                                          st.data_ptr() if st is not None else None,
-                                          rpb, bins, 1, b1, grid, lo))
-            outs.append((res, hist, e, work))
-        C = len(items)
-        arr = (nat.SdpPass2Task * C)(*tasks)
-        d_tasks = self._h2d(np.frombuffer(bytearray(bytes(arr)), dtype=np.uint8))
-        gw = self._bytes(sdp.sdp_pass2_gram_workspace_bytes(n, C))
-        G = torch.empty(C * C, dtype=torch.float64, device=self.device)
-        cs = torch.empty(C, dtype=torch.float64, device=self.device)
-        nn = torch.empty(1, dtype=torch.float64, device=self.device)
-        mask = sum(1 << i for i, g in enumerate(gram_mask) if g)
-        nat.annotate('table', sum(col_read_bytes(c) for c, _, _, _, _ in items))
-        sdp.sdp_pass2_gram(arr, ptr(d_tasks), C, mask, ptr(gw), gw.numel(), ptr(G), ptr(cs), ptr(nn), s)
-        idx = [i for i, g in enumerate(gram_mask) if g]
-        self._fused_gram = {'ids': [id(items[i][0]) for i in idx], 'shifts': [float(items[i][1]) for i in idx],
-                            'idx': idx, 'C': C, 'G': G, 's': cs, 'n': nn, 'keep': (d_tasks, gw, arr)}
-        return self._pass2_results(outs)
-
-    def pass2_batch(self, items, count_ctx=None, gram_mask=None):
+    def pass2_batch(self, items, count_ctx=None):
         """[(col, mean, edges, hi_t, lo_t)] -> [pass-2 dict] (see pass2), all
         launched back to back and read back once (sharded: one all-reduce of
         every column's counts and bins, one all-gather of the mad partials).
         count_ctx[i] (a _group_prepare context) makes column i's launch also do
         the level-1 count of its distinct-count partitioning (sdp_pass2_count);
-        the context is then kept for group_batch.  gram_mask[i]: column i is in
-        the Pearson matrix (utils.py:27-31) -- when the table fits
-        sdp_pass2_gram, that one launch also forms the Gram gram() returns."""
+        the context is then kept for group_batch."""
         if not items:
             return []
         count_ctx = count_ctx or {}
-        self._fused_gram = None
-        if gram_mask is not None and any(gram_mask) and self._p2gram_ok(items, count_ctx):
-            return self._pass2_gram(items, count_ctx, gram_mask)
         s = self._s()
         rsz = ctypes.sizeof(nat.SdpPass2Result)
         outs = []
@@ -987,7 +896,7 @@ class Engine:
         return {p: float(v) for p, v in zip(probs, out.cpu().numpy())}
 
     def numeric_stats_batch(self, cols, packs, bins=10, ks=None, probs=PROBS, group_cols=(), gk=None,
-                            count32_cols=None, corr=False):
+                            count32_cols=None):
         """numeric_stats of every column (None for a column with no non-null
         value) with two host readbacks in all.  A bins value the reference
         rejects (describe.py:46 with bins=1) is recorded per column and raised
@@ -1053,12 +962,7 @@ class Engine:
                     self._group_prepare(cols[i], False)
                 if ctx is not None:
                     count_ctx[j] = ctx
-        # corr=True: the Pearson matrix will be asked for the NUM columns,
-        # i.e. those with more than one distinct value (describe.py:156), which
-        # pass 1 already tells: no value, or one value and no NaN, is CONST
-        gram_mask = [not (stats[i].count == 0 or (stats[i].min == stats[i].max and stats[i].n_nan == 0))
-                     for i in p2_idx] if corr else None
-        for i, r2 in zip(p2_idx, self.pass2_batch(p2_items, count_ctx, gram_mask)):
+        for i, r2 in zip(p2_idx, self.pass2_batch(p2_items, count_ctx)):
             st = stats[i]
             st.mad = r2['abs_dev_sum']
             st.hist_counts = r2['hist']
@@ -2662,15 +2566,6 @@ class Engine:
     # Pearson (utils.py:20-36)
     # ==========================================================================
     def gram(self, cols: List[DeviceColumn], shifts, check_nan):
-        fg, self._fused_gram = getattr(self, '_fused_gram', None), None
-        if fg is not None and fg['ids'] == [id(c) for c in cols] and fg['shifts'] == [float(x) for x in shifts]:
-            # formed by pass 2's read (sdp_pass2_gram) for exactly these columns
-            C, idx = fg['C'], to_dev(fg['idx'], torch.int64, self.device)
-            G = fg['G'].view(C, C).index_select(0, idx).index_select(1, idx).reshape(-1)
-            packed = self.comm.allreduce_sum(torch.cat([G, fg['s'].index_select(0, idx), fg['n']]))
-            host = packed.cpu().numpy()
-            k = len(cols)
-            return host[:k * k].reshape(k, k), host[k * k:k * k + k], float(host[-1])
         n = cols[0].length
         C = len(cols)
         arr = (nat.SdpColumn * C)(*[c.sdp() for c in cols])
