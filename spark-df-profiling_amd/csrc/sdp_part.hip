@@ -119,8 +119,8 @@ __device__ bool rows_equal_global(const sdp_bytes_column &c, int64_t ra, int64_t
 }
 
 // ---- block scan of nb <= MAXB LDS counters (exclusive), NT threads -----------
-template <int NT, typename O = uint32_t>
-__device__ void block_excl_scan(const uint32_t *in, O *out, int nb, uint32_t *s_wsum) {
+template <int NT>
+__device__ void block_excl_scan(const uint32_t *in, uint32_t *out, int nb, uint32_t *s_wsum) {
     constexpr int PER = (MAXB + NT - 1) / NT;
     const int t = threadIdx.x;
     uint32_t v[PER];
@@ -148,7 +148,7 @@ __device__ void block_excl_scan(const uint32_t *in, O *out, int nb, uint32_t *s_
 #pragma unroll
     for (int k = 0; k < PER; ++k) {
         const int i = t * PER + k;
-        if (i < nb) out[i] = (O)run;
+        if (i < nb) out[i] = run;
         run += v[k];
     }
     lds_barrier();
@@ -414,35 +414,13 @@ __device__ __forceinline__ void wc_tile(WcLdsT<NA, L, NBM> &s, const uint64_t (&
 }
 
 constexpr int WC_RPT = 8;                       // records per thread per tile (16 spills registers, no faster)
-// The level-1 row scatter (describe.py:143's partitioning, phase 1).  One tile
-// of NT * RPT rows: hash, rank every record in its bucket by an LDS atomic,
-// scan the bucket counts, stage the tile sorted by bucket in LDS, write each
-// bucket's run contiguously at its cursor.  Two shapes:
-//   1024 threads x 16 rows (16 K-row tile, 157 KB of LDS: one workgroup per CU),
-//        with the heavy-key table -- columns that have heavy keys;
-//   512 threads x 16 rows (8 K-row tile, 78 KB: two workgroups per CU, one
-//        workgroup's LDS phases and loads overlapping the other's; no
-//        next-tile prefetch, which would not fit 128 VGPRs) -- columns without.
-template <int NT, int RPT, bool HEAVY>
-struct ScatterLdsT {
-    static constexpr int TILE = NT * RPT;
-    using Off = typename std::conditional<(TILE <= 65536), uint16_t, uint32_t>::type;
-    typename std::conditional<HEAVY, HeavyLdsT<false>, uint32_t>::type heavy;
-    uint32_t hist[MAXB];
-    Off off[MAXB];
-    uint64_t cur[MAXB];
-    uint64_t stage[TILE];
-    uint32_t wsum[NT / WAVE];
-};
 // block bx of a G-block grid (the batched launch runs several columns' grids
 // side by side, blockIdx.y = column)
-template <typename T, int NT = ST, int RPT = S_RPT, bool HEAVY = true, bool PREFETCH = true>
+template <typename T>
 __device__ __forceinline__ void scatter_rows_u64_body(const sdp_column &col, const HeavyArg &heavy, int b1,
                                                       int64_t rows_per_block, const uint64_t *offs, uint64_t *out_h,
                                                       int xcd_map, const int G, const int bx) {
-    constexpr int TILE = NT * RPT;
-    static_assert(ROWS_ALIGN % TILE == 0, "block row ranges are whole tiles");
-    __shared__ ScatterLdsT<NT, RPT, HEAVY> s;
+    __shared__ ScatterLds s;
     const int t = threadIdx.x;
     // XCD-aware: workgroups are dealt to the 8 XCDs round robin; with the map,
     // one XCD's workgroups take consecutive row blocks, so in every bucket the
@@ -453,29 +431,27 @@ __device__ __forceinline__ void scatter_rows_u64_body(const sdp_column &col, con
     const int shift = 64 - b1;
     const int64_t r0 = (int64_t)g * rows_per_block;
     const int64_t r1 = min(col.length, r0 + rows_per_block);
-    if constexpr (HEAVY) heavy_build<false>(s.heavy, heavy);
-    for (int b = t; b < nb; b += NT) {
+    heavy_build<false>(s.heavy, heavy);
+    for (int b = t; b < nb; b += ST) {
         s.hist[b] = 0;
         s.cur[b] = offs[(int64_t)b * G + g];
     }
     lds_barrier();
-    const bool any_heavy = HEAVY && heavy.n > 0;
-    RowTile<T, NT, RPT> tile;
+    const bool any_heavy = heavy.n > 0;
+    RowTile<T, ST, S_RPT> tile;
     const VBits vbm = vbits_init(col.d_validity, col.validity_bit_offset, col.d_values);
-    if (PREFETCH && r0 < r1) tile.load(col, vbm, r0, r1);
-    for (int64_t base = r0; base < r1; base += TILE) {
-        uint64_t h[RPT];
+    if (r0 < r1) tile.load(col, vbm, r0, r1);
+    for (int64_t base = r0; base < r1; base += S_TILE) {
+        uint64_t h[S_RPT];
         uint32_t vmask;
-        if (!PREFETCH) tile.load(col, vbm, base, r1);   // (the CU's other workgroup hides this wait)
         tile.hash(col, vbm, base, r1, h, vmask);
-        if (PREFETCH && base + TILE < r1) tile.load(col, vbm, base + TILE, r1);      // next tile in flight
-        uint32_t rank[RPT / 2] = {};            // 16 bits per row (< TILE): no VGPR spills
+        if (base + S_TILE < r1) tile.load(col, vbm, base + S_TILE, r1);      // next tile in flight
+        uint32_t rank[S_RPT / 2] = {};          // 16 bits per row (< S_TILE): no VGPR spills
         uint32_t keep = 0;
 #pragma unroll
-        for (int q = 0; q < RPT; ++q) {
+        for (int q = 0; q < S_RPT; ++q) {
             if ((vmask >> q) & 1u) {
-                int hv = -1;
-                if constexpr (HEAVY) hv = any_heavy ? heavy_find_u64(s.heavy, heavy.n, h[q]) : -1;
+                const int hv = any_heavy ? heavy_find_u64(s.heavy, heavy.n, h[q]) : -1;
                 if (hv < 0 && h[q] != EMPTY64) {
                     keep |= 1u << q;
                     rank[q / 2] |= atomicAdd(&s.hist[b1 ? (int)(h[q] >> shift) : 0], 1u) << (16 * (q & 1));
@@ -483,20 +459,20 @@ __device__ __forceinline__ void scatter_rows_u64_body(const sdp_column &col, con
             }
         }
         lds_barrier();
-        block_excl_scan<NT>(s.hist, s.off, nb, s.wsum);
+        block_excl_scan<ST>(s.hist, s.off, nb, s.wsum);
 #pragma unroll
-        for (int q = 0; q < RPT; ++q)
+        for (int q = 0; q < S_RPT; ++q)
             if ((keep >> q) & 1u)
                 s.stage[s.off[b1 ? (int)(h[q] >> shift) : 0] + ((rank[q / 2] >> (16 * (q & 1))) & 0xFFFFu)] = h[q];
         lds_barrier();
-        const uint32_t total = (uint32_t)s.off[nb - 1] + s.hist[nb - 1];
-        for (uint32_t j = t; j < total; j += NT) {
+        const uint32_t total = s.off[nb - 1] + s.hist[nb - 1];
+        for (uint32_t j = t; j < total; j += ST) {
             const uint64_t x = s.stage[j];
             const int b = b1 ? (int)(x >> shift) : 0;
             out_h[s.cur[b] + (j - s.off[b])] = x;
         }
         lds_barrier();
-        for (int b = t; b < nb; b += NT) {
+        for (int b = t; b < nb; b += ST) {
             s.cur[b] += s.hist[b];
             s.hist[b] = 0;
         }
@@ -509,16 +485,6 @@ __global__ void __launch_bounds__(ST) part_scatter_rows_u64_kernel(sdp_column co
                                                                    int64_t rows_per_block, const uint64_t *offs,
                                                                    uint64_t *out_h, int xcd_map) {
     scatter_rows_u64_body<T>(col, heavy, b1, rows_per_block, offs, out_h, xcd_map, (int)gridDim.x, (int)blockIdx.x);
-}
-constexpr int ST2 = 512;                        // the two-workgroups-per-CU shape (no heavy keys)
-template <typename T>
-__global__ void __launch_bounds__(ST2, 4) part_scatter_rows_u64_half_kernel(sdp_column col, int b1,
-                                                                           int64_t rows_per_block,
-                                                                           const uint64_t *offs, uint64_t *out_h,
-                                                                           int xcd_map) {
-    const HeavyArg none{nullptr, nullptr, nullptr, nullptr, 0};
-    scatter_rows_u64_body<T, ST2, S_RPT, false, false>(col, none, b1, rows_per_block, offs, out_h, xcd_map,
-                                                (int)gridDim.x, (int)blockIdx.x);
 }
 template <typename T>
 __global__ void __launch_bounds__(ST) part_scatter_rows_u64_batch_kernel(const sdp_rows_task *tasks, int xcd_map) {
@@ -2025,10 +1991,6 @@ static int grid_of(int64_t items, int64_t cap) {
 }
 
 // SDP_XCD_MAP=0 turns the XCD-aware workgroup mapping of the scatters off (A/B runs)
-static int rows_half_enabled() {
-    const char *e = getenv("SDP_ROWS_HALF");
-    return e != nullptr && e[0] == '1';
-}
 static int xcd_map_enabled() {
     const char *e = getenv("SDP_XCD_MAP");
     return (e && e[0] == '0') ? 0 : 1;
@@ -2039,9 +2001,6 @@ static void launch_rows_u64(int phase, int grid, hipStream_t s, const sdp_column
                             uint32_t *hist, const uint64_t *offs, uint64_t *out, uint64_t *hc, uint64_t *st) {
     if (phase == 0)
         hipLaunchKernelGGL((part_count_rows_u64_kernel<T>), dim3(grid), dim3(CT), 0, s, c, hv, b1, rpb, hist, hc, st);
-    else if (hv.n == 0 && rows_half_enabled())
-        hipLaunchKernelGGL((part_scatter_rows_u64_half_kernel<T>), dim3(grid), dim3(ST2), 0, s, c, b1, rpb, offs,
-                           out, xcd_map_enabled());
     else
         hipLaunchKernelGGL((part_scatter_rows_u64_kernel<T>), dim3(grid), dim3(ST), 0, s, c, hv, b1, rpb, offs, out,
                            xcd_map_enabled());
