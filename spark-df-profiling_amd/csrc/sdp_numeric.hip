@@ -1170,7 +1170,6 @@ __global__ void column_keys_kernel(sdp_column col, uint64_t lo, uint64_t hi, uin
 // counts 1), [1] violation, [2] first valid row, [3] last valid row (indices,
 // turned into keys by sorted_distinct_final_kernel).
 constexpr int SD_T = 256;
-constexpr int SD_E = 4;                 // consecutive elements per thread per step
 constexpr int SD_WALK = 256;            // rows walked back over nulls at most
 
 template <typename T>
@@ -1181,39 +1180,85 @@ __device__ __forceinline__ bool sd_fetch(const sdp_column &c, int64_t i, uint64_
     return true;
 }
 
+// Each lane takes SD_V consecutive rows (whole 16-byte vectors and one read of
+// their validity bits), counts the key changes inside them, and learns the
+// key before its first valid row from the lane to its left (__shfl_up: that
+// lane holds the rows just before); lane 0 of a wave, or a lane whose left
+// neighbour saw only nulls, walks back row by row (rare: one lookup per 64
+// lanes, or SD_V nulls in a row).  The element-at-a-time form it replaced
+// waited on every row's validity byte and value: 3.3 ms per 1e9-row int64
+// column, 2.4 TB/s.
+constexpr int SD_V = 8;                 // rows per lane per step
 template <typename T>
 __global__ void __launch_bounds__(SD_T) sorted_distinct_kernel(sdp_column col, uint64_t *out) {
+    constexpr int VPT = Vec16<T>::N;
+    constexpr int SV = SD_V > VPT ? SD_V : VPT;        // rows per lane (1-byte types: 16)
+    constexpr int NV = SV / VPT;
     const int64_t n = col.length;
-    const int64_t ngroups = (n + SD_E - 1) / SD_E;
+    const int64_t ngroups = (n + SV - 1) / SV;
     const int64_t stride = (int64_t)gridDim.x * SD_T;
+    const int lane = lane_id();
     uint64_t d = 0;
     bool viol = false;
     int64_t first = INT64_MAX, last = -1;
-    for (int64_t gi = (int64_t)blockIdx.x * SD_T + threadIdx.x; gi < ngroups; gi += stride) {
-        const int64_t i0 = gi * SD_E;
-        uint64_t prev = 0;
-        bool have = false;
-        // the previous valid row before this group (one cached load unless
-        // nulls); a null run longer than SD_WALK gives up (violation: the
-        // caller groups the column instead), so a mostly-null column costs
-        // O(n SD_WALK), never O(n^2)
-        int64_t j = i0 - 1;
-        for (int w = 0; j >= 0 && w < SD_WALK; --j, ++w)
-            if (sd_fetch<T>(col, j, prev)) { have = true; break; }
-        if (!have && j >= 0) viol = true;
+    for (int64_t gb = (int64_t)blockIdx.x * SD_T; gb < ngroups; gb += stride) {
+        const int64_t gi = gb + threadIdx.x;           // (the wave's lanes take consecutive groups)
+        const int64_t i0 = gi * SV;
+        uint64_t k[SV];
+        uint32_t vm = 0;
+        if (gi < ngroups && i0 + SV <= n) {
+            const Vec16<T> *vp = (const Vec16<T> *)col.d_values + i0 / VPT;
 #pragma unroll
-        for (int e = 0; e < SD_E; ++e) {
-            const int64_t i = i0 + e;
-            uint64_t k;
-            if (i < n && sd_fetch<T>(col, i, k)) {
-                d += (!have || k != prev);
-                viol |= have && k < prev;
-                if (!have) first = i;
-                last = i;
-                prev = k;
+            for (int u = 0; u < NV; ++u) {
+                const Vec16<T> v = vp[u];
+#pragma unroll
+                for (int e = 0; e < VPT; ++e) k[u * VPT + e] = Elem<T>::key(v.v[e]);
+            }
+            vm = valid_bits(col.d_validity, col.validity_bit_offset, i0, SV);
+        } else {
+#pragma unroll
+            for (int e = 0; e < SV; ++e) {
+                k[e] = 0;
+                const int64_t i = i0 + e;
+                if (gi < ngroups && i < n && sd_fetch<T>(col, i, k[e])) vm |= 1u << e;
+            }
+        }
+        // changes inside the lane's rows (its first valid row counted as new)
+        uint64_t prev = 0, fk = 0;
+        bool have = false;
+        uint32_t dl = 0;
+#pragma unroll
+        for (int e = 0; e < SV; ++e) {
+            if ((vm >> e) & 1u) {
+                dl += (!have || k[e] != prev);
+                viol |= have && k[e] < prev;
+                if (!have) fk = k[e];
+                prev = k[e];
                 have = true;
             }
         }
+        if (vm) {
+            first = min(first, i0 + (int64_t)__builtin_ctz(vm));
+            last = max(last, i0 + 31 - (int64_t)__builtin_clz(vm));
+        }
+        // the key before this lane's first valid row: the left lane's last one
+        const uint64_t lk = __shfl_up(prev, 1, WAVE);
+        const bool lh = __shfl_up(have ? 1 : 0, 1, WAVE) != 0;
+        if (vm) {
+            uint64_t pk = lk;
+            bool ph = lane > 0 && lh;
+            if (!ph) {                                  // walk back over nulls
+                int64_t j = i0 - 1;
+                for (int w = 0; j >= 0 && w < SD_WALK; --j, ++w)
+                    if (sd_fetch<T>(col, j, pk)) { ph = true; break; }
+                if (!ph && j >= 0) viol = true;         // (a null run too long to walk)
+            }
+            if (ph) {
+                dl -= (fk == pk);
+                viol |= fk < pk;
+            }
+        }
+        d += dl;
     }
     d = wave_sum_u64(d);
     const bool any_viol = __any(viol);
@@ -2218,7 +2263,7 @@ extern "C" int sdp_sorted_distinct(const sdp_column *col, uint64_t *d_out, void 
     hipLaunchKernelGGL(sorted_distinct_init_kernel, dim3(1), dim3(1), 0, s, d_out);
     rc = check_launch("sorted_distinct_init_kernel");
     if (rc) return rc;
-    const int64_t groups = (col->length + SD_E - 1) / SD_E;
+    const int64_t groups = (col->length + SD_V - 1) / SD_V;
     const int grid = (int)std::min<int64_t>(std::max<int64_t>((groups + SD_T - 1) / SD_T, 1), 8192);
     SDP_DISPATCH_NUMERIC(col->dtype,
         hipLaunchKernelGGL(sorted_distinct_kernel<T>, dim3(grid), dim3(SD_T), 0, s, *col, d_out);

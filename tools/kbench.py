@@ -40,6 +40,12 @@ for r in range(reps):
     elif what == 'd32':                      # sdp_distinct32 (32-bit key spaces)
         lo = 0 if col.is_float else int(col.values[:rows].min().item())
         out = e._distinct32_launch(col, lo)
+    elif what == 'sorted':                   # sdp_sorted_distinct (one streaming read), 5 launches
+        out = torch.zeros(4, dtype=torch.int64, device=dev)
+        cs = col.sdp()
+        for _ in range(5):
+            nat.annotate('sdp_sorted_distinct[%s]' % col.name, col.length * col.values.element_size())
+            sdp.sdp_sorted_distinct(ctypes.byref(cs), ptr(out), nat.stream_handle())
     elif what == 'gram':
         num = [c for c in t.columns if c.kind == 'fixed' and c.spark_type != 'date']
         e.gram(num, [0.0] * len(num), [False] * len(num))
