@@ -391,6 +391,182 @@ __device__ __forceinline__ void gw_load(const GramCol &gc, int64_t r, int64_t n,
     x.hi = u32x4{w[4], w[5], w[6], w[7]};
 }
 
+// ---- narrow tables (C <= 16): whole columns per wave while staging ---------------
+//
+// gram_kernel<16> converts in the MFMA operand layout, where the 16 lanes of a
+// lane group hold 16 different columns: every lane forms all four common
+// conversions and selects (SQ counters, profiles/r04s_gram_sq_pmc.txt: ~100
+// VALU instructions per 16-row k-block, wait_inst 0.53 of wave cycles -- issue
+// bound, not memory bound).  Here a 256-row k-step is staged into LDS first,
+// each wave converting four whole columns (column, dtype and shift are
+// wave-uniform: a uniform branch per column and k-step, then one conversion
+// per element or none), and then every wave runs the MFMAs of its four 16-row
+// groups from LDS.  The next k-step's raw loads are issued right after the
+// staging, so they are in flight during the MFMAs; four workgroups per CU.
+// Only the chunk's last k-step can be ragged (a wave-uniform test): the others
+// load without per-lane bounds checks.
+// LDS [col][row] with a pitch of 258 doubles (2 * 258 = 4 mod 64 banks): the
+// 16 lanes of an operand read (column cl, 4 consecutive rows) touch 64
+// distinct banks.  (A 16-wave form with one column per wave and its k-loop
+// instantiated per dtype ran 23.0 ms against this form's 19.1 on 1e9 x 13
+// columns: one workgroup per CU left the HBM idle during its barriers.)
+constexpr int G16_W = 4;                        // waves per workgroup
+constexpr int G16_BLOCK = G16_W * WAVE;
+constexpr int G16_R = 4 * WAVE;                 // rows per k-step: 4 per lane
+constexpr int G16_P = G16_R + 2;                // LDS pitch in doubles
+constexpr int G16_CPW = 16 / G16_W;             // columns staged per wave
+
+// stage 4 rows of a column of dtype DT: convert, shift, mask, sum, store
+template <int DT>
+__device__ __forceinline__ void g16_stage(const GwRaw &x, uint32_t kb, double K, double &csum, double *dst) {
+    double v[4];
+    if (DT == SDP_F64) {
+        v[0] = __longlong_as_double((long long)(((uint64_t)x.lo[1] << 32) | x.lo[0]));
+        v[1] = __longlong_as_double((long long)(((uint64_t)x.lo[3] << 32) | x.lo[2]));
+        v[2] = __longlong_as_double((long long)(((uint64_t)x.hi[1] << 32) | x.hi[0]));
+        v[3] = __longlong_as_double((long long)(((uint64_t)x.hi[3] << 32) | x.hi[2]));
+    } else if (DT == SDP_I64) {
+        v[0] = (double)(int64_t)(((uint64_t)x.lo[1] << 32) | x.lo[0]);
+        v[1] = (double)(int64_t)(((uint64_t)x.lo[3] << 32) | x.lo[2]);
+        v[2] = (double)(int64_t)(((uint64_t)x.hi[1] << 32) | x.hi[0]);
+        v[3] = (double)(int64_t)(((uint64_t)x.hi[3] << 32) | x.hi[2]);
+    } else if (DT == SDP_F32) {
+#pragma unroll
+        for (int m = 0; m < 4; ++m) v[m] = (double)__uint_as_float(x.lo[m]);
+    } else if (DT == SDP_I32) {
+#pragma unroll
+        for (int m = 0; m < 4; ++m) v[m] = (double)(int32_t)x.lo[m];
+    } else {
+        conv4(DT, Raw4{x.lo, x.hi}, v);
+    }
+    double y[4];
+#pragma unroll
+    for (int m = 0; m < 4; ++m) y[m] = ((kb >> m) & 1u) ? v[m] - K : 0.0;
+    csum += (y[0] + y[1]) + (y[2] + y[3]);
+    *(d4 *)dst = d4{y[0], y[1], y[2], y[3]};
+}
+__device__ __forceinline__ void g16_stage_any(int dt, const GwRaw &x, uint32_t kb, double K, double &csum,
+                                              double *dst) {
+    switch (dt) {                                      // wave-uniform
+    case SDP_F64: g16_stage<SDP_F64>(x, kb, K, csum, dst); break;
+    case SDP_I64: g16_stage<SDP_I64>(x, kb, K, csum, dst); break;
+    case SDP_F32: g16_stage<SDP_F32>(x, kb, K, csum, dst); break;
+    case SDP_I32: g16_stage<SDP_I32>(x, kb, K, csum, dst); break;
+    case SDP_U32: g16_stage<SDP_U32>(x, kb, K, csum, dst); break;
+    case SDP_I16: g16_stage<SDP_I16>(x, kb, K, csum, dst); break;
+    case SDP_U16: g16_stage<SDP_U16>(x, kb, K, csum, dst); break;
+    case SDP_I8: g16_stage<SDP_I8>(x, kb, K, csum, dst); break;
+    case SDP_U8: g16_stage<SDP_U8>(x, kb, K, csum, dst); break;
+    default: *(d4 *)dst = d4{0.0, 0.0, 0.0, 0.0};    // padding column
+    }
+}
+
+__global__ void __launch_bounds__(G16_BLOCK, 4) gram16_kernel(const GramCol *cols, int ncols, const double *shift,
+                                                            const uint32_t *keep, int64_t n, int64_t rows_per_chunk,
+                                                            double *part_g, double *part_cs, double *part_n) {
+    __shared__ double s_y[16 * G16_P];
+    const int s = blockIdx.x;
+    const int lane = lane_id();
+    const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x / WAVE);
+    const int q = lane >> 4, cl = lane & 15;
+    const int64_t c0 = (int64_t)s * rows_per_chunk;
+    const int64_t c1 = min(n, c0 + rows_per_chunk);
+
+    // the wave's columns wid, wid + 4, wid + 8, wid + 12 (dtype 0: padding, staged as zeros)
+    GramCol gc[G16_CPW];
+    double K[G16_CPW];
+#pragma unroll
+    for (int j = 0; j < G16_CPW; ++j) {
+        const int c = wid + G16_W * j;
+        gc[j] = c < ncols ? cols[c] : GramCol{nullptr, 0, 0};
+        K[j] = c < ncols ? shift[c] : 0.0;
+    }
+    double csum[G16_CPW];
+#pragma unroll
+    for (int j = 0; j < G16_CPW; ++j) csum[j] = 0.0;
+    double nkeep = 0.0;
+    d4 acc = d4{0.0, 0.0, 0.0, 0.0};   // (one chain: the f64 MFMA issue rate, not its latency, bounds it)
+
+    GwRaw raw[G16_CPW];
+    uint32_t kw = 0;
+    auto load = [&](int64_t r0) {
+        const int64_t r = r0 + 4 * lane;
+        if (r0 + G16_R <= c1) {                        // wave-uniform: a whole k-step
+            kw = keep[r >> 5];
+#pragma unroll
+            for (int j = 0; j < G16_CPW; ++j) {
+                const char *b = (const char *)gc[j].p + r * gc[j].width;
+                switch (gc[j].width) {
+                case 8:
+                    raw[j].lo = *(const __attribute__((address_space(1))) u32x4 *)b;
+                    raw[j].hi = *(const __attribute__((address_space(1))) u32x4 *)(b + 16);
+                    break;
+                case 4: raw[j].lo = *(const __attribute__((address_space(1))) u32x4 *)b; break;
+                case 2: {
+                    typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+                    const u32x2 v = *(const __attribute__((address_space(1))) u32x2 *)b;
+                    raw[j].lo[0] = v[0];
+                    raw[j].lo[1] = v[1];
+                } break;
+                case 1: raw[j].lo[0] = *(const __attribute__((address_space(1))) uint32_t *)b; break;
+                default: break;                        // padding column
+                }
+            }
+        } else {
+            kw = r < c1 ? keep[r >> 5] : 0u;
+#pragma unroll
+            for (int j = 0; j < G16_CPW; ++j) {
+                raw[j].lo = u32x4{0, 0, 0, 0};
+                raw[j].hi = u32x4{0, 0, 0, 0};
+                if (r < n) gw_load(gc[j], r, n, raw[j]);
+            }
+        }
+    };
+    if (c0 < c1) load(c0);
+    for (int64_t r0 = c0; r0 < c1; r0 += G16_R) {
+        const int64_t r = r0 + 4 * lane;
+        uint32_t kb = (kw >> (r & 31)) & 0xFu;
+        if (r0 + G16_R > c1) kb &= r >= c1 ? 0u : (r + 4 > c1 ? (1u << (int)(c1 - r)) - 1u : 0xFu);
+        if (wid == 0) nkeep += (double)__popc(kb);
+        __syncthreads();                               // the previous k-step's operand reads are done
+#pragma unroll
+        for (int j = 0; j < G16_CPW; ++j)
+            g16_stage_any(gc[j].dtype, raw[j], kb, K[j], csum[j], &s_y[(wid + G16_W * j) * G16_P + 4 * lane]);
+        if (r0 + G16_R < c1) load(r0 + G16_R);
+        __syncthreads();
+        // this wave's row groups wid, wid + 4, wid + 8, wid + 12: MFMA m takes row 4q + m
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+            const d4 v = *(const d4 *)&s_y[cl * G16_P + 16 * (wid + G16_W * g) + 4 * q];
+#pragma unroll
+            for (int m = 0; m < 4; ++m) acc = __builtin_amdgcn_mfma_f64_16x16x4f64(v[m], v[m], acc, 0, 0, 0);
+        }
+    }
+    // ---- combine the 4 waves (fixed order), write the chunk partial ----
+    __syncthreads();
+    double *s_acc = s_y;                               // 4 x 256 doubles
+#pragma unroll
+    for (int rr = 0; rr < 4; ++rr) s_acc[wid * 256 + (q + 4 * rr) * 16 + cl] = acc[rr];
+    __syncthreads();
+    {
+        const int e = threadIdx.x;                     // G16_BLOCK == 256 entries
+        double v = 0.0;
+#pragma unroll
+        for (int w = 0; w < G16_W; ++w) v += s_acc[w * 256 + e];
+        part_g[(int64_t)s * 256 + e] = v;
+    }
+    // column sums: wave wid holds columns wid + 4 j
+#pragma unroll
+    for (int j = 0; j < G16_CPW; ++j) {
+        const double v = wave_sum_f64(csum[j]);
+        if (lane == 0) part_cs[(int64_t)s * 16 + wid + G16_W * j] = v;
+    }
+    if (wid == 0) {
+        const double v = wave_sum_f64(nkeep);
+        if (lane == 0) part_n[s] = v;
+    }
+}
+
 // KIND: GW_GENERIC (any dtype mix, element-wise tail), GW_F32 / GW_F64 (every
 // column of the tile has that dtype and the chunk holds no ragged tail: the
 // staging is branch-free -- row addresses are clamped into the column and the
@@ -752,15 +928,16 @@ static GramGeom gram_geom(int64_t n, int ncols) {
     g.T = g.side * (g.side + 1) / 2;
     // enough workgroups for several rounds at full occupancy (a single
     // 1024-workgroup round left a tail when fewer than 4 waves/SIMD fit)
-    const int64_t target = g.tile == 16 ? 8192 : 4096;
+    const int64_t target = 4096;
     int64_t S = (target + g.T - 1) / g.T;
     const int64_t min_rows = 4096;
     const int64_t max_s = (n + min_rows - 1) / min_rows;
     if (S > max_s) S = max_s;
     if (S < 1) S = 1;
     int64_t rpc = (n + S - 1) / S;
-    rpc = (rpc + 63) / 64 * 64;                 // whole k-blocks per wave group
-    if (rpc < 64) rpc = 64;
+    const int64_t kstep = g.tile == 16 ? G16_R : 64;   // whole k-steps (gram16) / k-blocks per wave group
+    rpc = (rpc + kstep - 1) / kstep * kstep;
+    if (rpc < kstep) rpc = kstep;
     g.S = (int)((n + rpc - 1) / rpc);
     if (g.S < 1) g.S = 1;
     g.rows_per_chunk = rpc;
@@ -866,7 +1043,7 @@ extern "C" int sdp_gram(const sdp_column *cols, int32_t ncols, const uint32_t *d
     const dim3 grid((unsigned)(g.S * g.T));
     switch (g.tile) {
     case 16:
-        hipLaunchKernelGGL(gram_kernel<16>, grid, dim3(G_BLOCK), 0, s, d_cols, ncols, d_shift, d_keep, n, g.side, g.T,
+        hipLaunchKernelGGL(gram16_kernel, grid, dim3(G16_BLOCK), 0, s, d_cols, ncols, d_shift, d_keep, n,
                            g.rows_per_chunk, pg, pcs, pn);
         break;
     case 32:

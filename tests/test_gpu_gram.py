@@ -1,7 +1,7 @@
 """The shifted Gram product behind corr_matrix (utils.py:20-36) on every tile
 width the kernel has (16 / 32 / 64 columns per tile, diagonal and off-diagonal
 tiles), with mixed dtypes, nulls and NaN (listwise deletion, utils.py:27),
-against numpy float64.  Tolerance: 1e-12 relative to sum |x - K|^2 per entry
+against numpy float64 (tables of <= 16 columns: gram16_kernel).  Tolerance: 1e-12 relative to sum |x - K|^2 per entry
 (the kernel's summation order differs from numpy's; both are fp64)."""
 
 import numpy as np
@@ -41,8 +41,13 @@ WIDE = [(2053, 70, None), (20011, 200, None), (40000, 160, 'f32'), (9999, 130, '
         (7, 129, 'f64'), (3, 300, None)]
 
 
-@pytest.mark.parametrize('n,ncols,kind', [(5003, 12, None), (4099, 21, None), (3001, 40, None), (1, 3, None),
-                                          (37, 17, None)] + WIDE)
+# <= 16 columns take gram16_kernel (256-row k-steps, one column per wave while
+# staging): several chunks with a ragged last k-step, every dtype, 1-16 columns
+NARROW = [(5003, 12, None), (1, 3, None), (300_001, 16, None), (257, 5, None), (70_003, 16, 'f64'),
+          (1_048_579, 9, None), (4, 1, None)]
+
+
+@pytest.mark.parametrize('n,ncols,kind', NARROW + [(4099, 21, None), (3001, 40, None), (37, 17, None)] + WIDE)
 def test_gram_matches_numpy(n, ncols, kind):
     import torch
     from spark_df_profiling.columns import DeviceTable
