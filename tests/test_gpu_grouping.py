@@ -167,10 +167,10 @@ def _dedup_buckets(buckets, flags):
 
 @pytest.mark.parametrize('direct', [0, 4])
 def test_wave_dedup_kernels(direct):
-    """The two-phase wave dedup (read-first and direct-CAS modes) on crafted
-    final buckets: single and multi-batch buckets, duplicates, keys sharing
-    one home slot (collision list and its overflow past 448 entries), empty
-    buckets."""
+    """The wave dedup kernels (read-first 2048-slot tables; near-unique
+    mode: the half-space tables) on crafted final buckets: single and
+    multi-batch buckets, duplicates, keys sharing one home slot (collision list
+    and its overflow), buckets around one 1024-record batch, empty buckets."""
     g = datagen.rng(7)
     b = []
     for _ in range(300):                                   # ordinary buckets with repeats
@@ -183,6 +183,12 @@ def test_wave_dedup_kernels(direct):
     big = g.integers(0, 2 ** 63, 1500, dtype=np.uint64)
     b.append(big[g.integers(0, 1500, 6000)])               # multi-batch bucket (probe limit path)
     b.append(np.zeros(0, np.uint64))
+    u = g.integers(0, 2 ** 63, 1281, dtype=np.uint64)
+    b.append(u[:1024])                                     # one whole batch, all distinct
+    b.append(u[:1025])                                     # one past it: two batches
+    b.append(u)
+    b.append(u[g.integers(0, 40, 1280)])                   # 40 keys repeated
+    b.append(np.full(1, 12345, np.uint64))
     groups, full = _dedup_buckets(b, direct)
     want = sum(len(np.unique(x)) for x in b)
     assert full == 0

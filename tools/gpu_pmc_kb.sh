@@ -17,7 +17,7 @@ for f in glob.glob(sys.argv[1] + '/**/*counter_collection.csv', recursive=True):
         k = r['Kernel_Name'].split('(')[0].replace('void ', '')[:60]
         v[k][r['Counter_Name']] += float(r['Counter_Value'])
 for k, c in v.items():
-    if 'SQ_WAVE_CYCLES' not in c:
+    if 'SQ_WAIT_ANY' not in c:
         print('%-60s %s' % (k, '  '.join('%s %.4g' % kv for kv in sorted(c.items()))))
         continue
     wc = c['SQ_WAVE_CYCLES'] or 1

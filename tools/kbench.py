@@ -21,6 +21,9 @@ for r in range(reps):
     t0 = time.perf_counter()
     if what == 'group':
         e.group(col, col.kind == 'bytes', dense=False)
+    elif what == 'groupd':                   # the near-unique (direct) dedup mode describe() picks from its sample
+        e._near_unique.add(id(col))
+        e.group(col, False, dense=False)
     elif what == 'table':
         cap = int(os.environ['KB_CAP']) if os.environ.get('KB_CAP') else None
         e._distinct_fixed_table(col) if col.kind != 'bytes' else e.value_counts_bytes_table(col, capacity=cap)
