@@ -54,12 +54,13 @@ enum sdp_status {
 #define SDP_GSORT_MAX         8192     /* groups one sdp_sort_groups launch orders          */
 
 /* ---- layout handshake ------------------------------------------------------
- * SDP_ABI_VERSION changes whenever a struct below, a record layout or a policy
+ * SDP_ABI_VERSION changes whenever a struct below, a record layout or its hash
+ * (6: fixed-key records are the one-multiply mix64 of sdp_common.h) or a policy
  * constant above changes.  A host binding compares sdp_layout_info() with its
  * own view and refuses a library that disagrees (a record-layout mismatch
  * between the engine and the library once turned garbage metas into row
  * indices on the GPU). */
-#define SDP_ABI_VERSION 5
+#define SDP_ABI_VERSION 6
 #define SDP_LAYOUT_NSIZES 17
 typedef struct sdp_layout {
     int32_t abi_version;

@@ -87,15 +87,6 @@ bool numeric(int dt) { return integral(dt) || floating(dt); }
 // fixed-width dtypes the grouping kernels take (adds u64 and bit-packed bools)
 bool groupable(int dt) { return numeric(dt) || dt == SDP_U64 || dt == SDP_BOOL; }
 
-// inverse of mix64 (sdp_common.h): a fixed key from its partition hash
-uint64_t inv_mix64(uint64_t x) {
-    x ^= (x >> 31) ^ (x >> 62);
-    x *= 0x319642B2D24D8EC3ull;
-    x ^= (x >> 27) ^ (x >> 54);
-    x *= 0x96DE1B173F119089ull;
-    x ^= (x >> 30) ^ (x >> 60);
-    return x;
-}
 
 int64_t next_pow2_cap(int64_t x) {          // engine._next_pow2: at least 1024 slots
     int64_t c = 1024;

@@ -280,13 +280,25 @@ __device__ __forceinline__ int lane_rank(uint64_t mask) {
                                      __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0));
 }
 
-// 64-bit mixer (splitmix64 / murmur3 fmix64)
+// 64-bit mixer: fold, one odd multiply, fold -- a bijection, so a record (the
+// mix of a fixed-width key) is equal to another exactly when the keys are.
+// Round 5: splitmix64's finalizer (two 64-bit multiplies, i.e. eight
+// quarter-rate 32-bit multiplies per key) cost 1.9 of 17.0 ms in the pass-2 +
+// level-1 count of six 1e9-row f64 columns (profiles/r05q_*); this form
+// spreads structured keys (sequences, strides, small integers as doubles) over
+// the level-1 / level-2 buckets and table slots at least as evenly, and random
+// keys the same (tools/mixer_quality.py).
 __host__ __device__ __forceinline__ uint64_t mix64(uint64_t x) {
-    x ^= x >> 30;
-    x *= 0xBF58476D1CE4E5B9ull;
-    x ^= x >> 27;
-    x *= 0x94D049BB133111EBull;
-    x ^= x >> 31;
+    x ^= x >> 32;
+    x *= 0xD6E8FEB86659FD93ull;
+    x ^= x >> 32;
+    return x;
+}
+// its inverse: a fixed key from its record
+__host__ __device__ __forceinline__ uint64_t inv_mix64(uint64_t x) {
+    x ^= x >> 32;
+    x *= 0xCFEE444D8B59A89Bull;
+    x ^= x >> 32;
     return x;
 }
 

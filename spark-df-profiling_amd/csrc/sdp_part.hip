@@ -37,14 +37,6 @@ constexpr uint64_t RMASK40 = (1ull << 40) - 1ull;
 constexpr uint64_t LEN_MAX = (1ull << 24) - 1ull;
 
 // ---- hashing ------------------------------------------------------------------
-__host__ __device__ __forceinline__ uint64_t inv_mix64(uint64_t x) {
-    x ^= (x >> 31) ^ (x >> 62);
-    x *= 0x319642B2D24D8EC3ull;
-    x ^= (x >> 27) ^ (x >> 54);
-    x *= 0x96DE1B173F119089ull;
-    x ^= (x >> 30) ^ (x >> 60);
-    return x;
-}
 __device__ __forceinline__ uint64_t bh_init(uint64_t len) {
     return 0x9E3779B97F4A7C15ull ^ (len * 0xFF51AFD7ED558CCDull);
 }

@@ -27,7 +27,7 @@ BITMAP_MAX_BITS = 1 << 20        # SDP_BITMAP_MAX_BITS
 
 # the grouping policy (include/sdp.h SDP_*), shared with the library's coarse
 # entries; _load() refuses a library built with other values
-ABI_VERSION = 5              # SDP_ABI_VERSION
+ABI_VERSION = 6              # SDP_ABI_VERSION (6: records are the one-multiply mix64)
 HEAVY_MAX = 256              # SDP_HEAVY_MAX: the row kernels' heavy-key tables
 HEAVY_MAX_REC = 1024         # SDP_HEAVY_MAX_REC: byte keys on the records kernel
 HEAVY_MIN = 3                # SDP_HEAVY_MIN

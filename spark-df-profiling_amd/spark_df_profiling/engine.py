@@ -116,13 +116,9 @@ def _label(col, stage=''):
 
 def inv_mix64(x):
     """Inverse of mix64 (sdp_common.h), so a fixed key is recovered from its record."""
-    M = U64
-    x ^= (x >> 31) ^ (x >> 62)
-    x = (x * 0x319642B2D24D8EC3) & M
-    x ^= (x >> 27) ^ (x >> 54)
-    x = (x * 0x96DE1B173F119089) & M
-    x ^= (x >> 30) ^ (x >> 60)
-    return x
+    x ^= x >> 32
+    x = (x * 0xCFEE444D8B59A89B) & U64
+    return x ^ (x >> 32)
 
 
 def _next_pow2(x):
