@@ -44,12 +44,16 @@ __device__ __forceinline__ uint64_t bh_step(uint64_t h, uint64_t w) {
     h = (h ^ w) * 0x87C37B91114253D5ull;
     return (h << 31) | (h >> 33);
 }
-// hash of a string of <= 16 bytes given as zero-padded little-endian words
+// hash of a string of <= 16 bytes given as zero-padded little-endian words:
+// the second word through one odd multiply, the length through a multiply of
+// a value below 2^5 (24-bit multiplies), folded into the first word, then the
+// partition mixer -- two 64-bit multiplies per string instead of four; every
+// byte-record pass recomputes it (round 5)
 __device__ __forceinline__ uint64_t bh_short(uint64_t k0, uint64_t k1, uint64_t len) {
-    uint64_t h = bh_init(len);
-    if (len > 0) h = bh_step(h, k0);
-    if (len > 8) h = bh_step(h, k1);
-    return mix64(h);
+    const uint32_t l = (uint32_t)len & 31u;
+    const uint64_t lt = ((uint64_t)(l * 0x9E3779u) << 32) | (uint64_t)(l * 0xB97F4Bu);
+    const uint64_t m = k1 * 0x9E3779B97F4A7C15ull;
+    return mix64(k0 ^ ((m << 29) | (m >> 35)) ^ lt);
 }
 // hash of a byte record (short: recomputed from the bytes; long: carried in k0)
 __device__ __forceinline__ uint64_t rec_hash(uint64_t k0, uint64_t k1, uint64_t meta) {
