@@ -183,12 +183,17 @@ struct VecIn {
     uint32_t w0, w1, sh;
     bool in;
     // vector vi of the column (nvec >= 1 whole vectors)
+    // (global address space: a column pointer read from a task table in memory
+    // is generic, and a flat load also counts against the LDS wait counter)
     __device__ __forceinline__ void load(const Vec16<T> *vals, const VBits &vb, int64_t vi, int64_t nvec) {
         in = vi < nvec;
         const int64_t vc = in ? vi : 0;
-        v = vals[vc];
+        typedef uint32_t u32x4g __attribute__((ext_vector_type(4)));
+        const u32x4g raw = ((const __attribute__((address_space(1))) u32x4g *)vals)[vc];
+        __builtin_memcpy(&v, &raw, 16);
         const int64_t b = vb.none ? 0 : vb.bit0 + vc * VPT;
-        const uint32_t *wp = vb.base + (b >> 5);
+        const __attribute__((address_space(1))) uint32_t *wp =
+            (const __attribute__((address_space(1))) uint32_t *)vb.base + (b >> 5);
         w0 = wp[0];
         w1 = wp[1];
         sh = (uint32_t)(b & 31);

@@ -465,7 +465,7 @@ __device__ __forceinline__ void scatter_rows_u64_body(const sdp_column &col, con
         for (uint32_t j = t; j < total; j += ST) {
             const uint64_t x = s.stage[j];
             const int b = b1 ? (int)(x >> shift) : 0;
-            out_h[s.cur[b] + (j - s.off[b])] = x;
+            ((__attribute__((address_space(1))) uint64_t *)out_h)[s.cur[b] + (j - s.off[b])] = x;
         }
         lds_barrier();
         for (int b = t; b < nb; b += ST) {
