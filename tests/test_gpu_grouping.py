@@ -359,3 +359,23 @@ def test_byte_dedup_out_of_range_metas():
     want = Counter(vals)
     assert sorted(want.values()) == sorted(int(c) for c in
                                            tab['counts'][:tab['capacity']].cpu().numpy() if c > 0)
+
+
+def test_mixed_skewed_f32_and_timestamp_paths_chosen_once():
+    """>= 8 numeric columns of 64 K - 2^26 rows -- five
+    unskewed float32, three zipf-skewed high-cardinality float32 (heavy keys)
+    and a timestamp column -- each take the distinct path describe() chose
+    once, before pass 2 consumed the heavy-key samples, and match the oracle."""
+    import oracle
+    from spark_df_profiling import describe
+    g = datagen.rng(41)
+    n = 100_003
+    cols = {}
+    for k in range(5):
+        cols['f32_u%d' % k] = pa.array(g.standard_normal(n).astype(np.float32), mask=g.random(n) < 0.03)
+    for k in range(3):
+        z = np.minimum(g.zipf(1.3 + 0.1 * k, n), 10 ** 7).astype(np.float32) + np.float32(0.5)
+        cols['f32_z%d' % k] = pa.array(z)
+    cols['ts'] = pa.array(g.integers(0, 10 ** 15, n), type=pa.timestamp('us'))
+    t = pa.table(cols)
+    assert_describe_equal(describe(t, plots=False), oracle.describe(t))
