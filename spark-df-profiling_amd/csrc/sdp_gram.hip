@@ -412,7 +412,13 @@ __device__ __forceinline__ void gw_load(const GramCol &gc, int64_t r, int64_t n,
 // columns: one workgroup per CU left the HBM idle during its barriers.)
 constexpr int G16_W = 4;                        // waves per workgroup
 constexpr int G16_BLOCK = G16_W * WAVE;
-constexpr int G16_R = 4 * WAVE;                 // rows per k-step: 4 per lane
+// (G16_Q = 2 -- 512-row k-steps, two workgroups per CU at 224 VGPRs -- measured
+// 27.2 vs 17.7 ms on 1e9 x 13 columns, profiles/r05ab_gram16_two_quads_rejected_ab.log)
+#ifndef G16_Q
+#define G16_Q 1
+#endif
+constexpr int G16_QN = G16_Q;                   // 4-row quads per lane and column per k-step
+constexpr int G16_R = 4 * WAVE * G16_QN;        // rows per k-step (quad k of lane l: rows 4 l + 256 k)
 constexpr int G16_P = G16_R + 2;                // LDS pitch in doubles
 constexpr int G16_CPW = 16 / G16_W;             // columns staged per wave
 
@@ -461,7 +467,7 @@ __device__ __forceinline__ void g16_stage_any(int dt, const GwRaw &x, uint32_t k
     }
 }
 
-__global__ void __launch_bounds__(G16_BLOCK, 4) gram16_kernel(const GramCol *cols, int ncols, const double *shift,
+__global__ void __launch_bounds__(G16_BLOCK, 4 / G16_Q) gram16_kernel(const GramCol *cols, int ncols, const double *shift,
                                                             const uint32_t *keep, int64_t n, int64_t rows_per_chunk,
                                                             double *part_g, double *part_cs, double *part_n) {
     __shared__ double s_y[16 * G16_P];
@@ -487,56 +493,67 @@ __global__ void __launch_bounds__(G16_BLOCK, 4) gram16_kernel(const GramCol *col
     double nkeep = 0.0;
     d4 acc = d4{0.0, 0.0, 0.0, 0.0};   // (one chain: the f64 MFMA issue rate, not its latency, bounds it)
 
-    GwRaw raw[G16_CPW];
-    uint32_t kw = 0;
+    GwRaw raw[G16_QN][G16_CPW];
+    uint32_t kw[G16_QN];
     auto load = [&](int64_t r0) {
-        const int64_t r = r0 + 4 * lane;
-        if (r0 + G16_R <= c1) {                        // wave-uniform: a whole k-step
-            kw = keep[r >> 5];
+        const bool whole = r0 + G16_R <= c1;           // wave-uniform: a whole k-step
 #pragma unroll
-            for (int j = 0; j < G16_CPW; ++j) {
-                const char *b = (const char *)gc[j].p + r * gc[j].width;
-                switch (gc[j].width) {
-                case 8:
-                    raw[j].lo = *(const __attribute__((address_space(1))) u32x4 *)b;
-                    raw[j].hi = *(const __attribute__((address_space(1))) u32x4 *)(b + 16);
-                    break;
-                case 4: raw[j].lo = *(const __attribute__((address_space(1))) u32x4 *)b; break;
-                case 2: {
-                    typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
-                    const u32x2 v = *(const __attribute__((address_space(1))) u32x2 *)b;
-                    raw[j].lo[0] = v[0];
-                    raw[j].lo[1] = v[1];
-                } break;
-                case 1: raw[j].lo[0] = *(const __attribute__((address_space(1))) uint32_t *)b; break;
-                default: break;                        // padding column
+        for (int k = 0; k < G16_QN; ++k) {
+            const int64_t r = r0 + 4 * lane + 4 * WAVE * k;
+            if (whole) {
+                kw[k] = keep[r >> 5];
+#pragma unroll
+                for (int j = 0; j < G16_CPW; ++j) {
+                    const char *b = (const char *)gc[j].p + r * gc[j].width;
+                    switch (gc[j].width) {
+                    case 8:
+                        raw[k][j].lo = *(const __attribute__((address_space(1))) u32x4 *)b;
+                        raw[k][j].hi = *(const __attribute__((address_space(1))) u32x4 *)(b + 16);
+                        break;
+                    case 4: raw[k][j].lo = *(const __attribute__((address_space(1))) u32x4 *)b; break;
+                    case 2: {
+                        typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+                        const u32x2 v = *(const __attribute__((address_space(1))) u32x2 *)b;
+                        raw[k][j].lo[0] = v[0];
+                        raw[k][j].lo[1] = v[1];
+                    } break;
+                    case 1: raw[k][j].lo[0] = *(const __attribute__((address_space(1))) uint32_t *)b; break;
+                    default: break;                    // padding column
+                    }
                 }
-            }
-        } else {
-            kw = r < c1 ? keep[r >> 5] : 0u;
+            } else {
+                kw[k] = r < c1 ? keep[r >> 5] : 0u;
 #pragma unroll
-            for (int j = 0; j < G16_CPW; ++j) {
-                raw[j].lo = u32x4{0, 0, 0, 0};
-                raw[j].hi = u32x4{0, 0, 0, 0};
-                if (r < n) gw_load(gc[j], r, n, raw[j]);
+                for (int j = 0; j < G16_CPW; ++j) {
+                    raw[k][j].lo = u32x4{0, 0, 0, 0};
+                    raw[k][j].hi = u32x4{0, 0, 0, 0};
+                    if (r < n) gw_load(gc[j], r, n, raw[k][j]);
+                }
             }
         }
     };
     if (c0 < c1) load(c0);
     for (int64_t r0 = c0; r0 < c1; r0 += G16_R) {
-        const int64_t r = r0 + 4 * lane;
-        uint32_t kb = (kw >> (r & 31)) & 0xFu;
-        if (r0 + G16_R > c1) kb &= r >= c1 ? 0u : (r + 4 > c1 ? (1u << (int)(c1 - r)) - 1u : 0xFu);
-        if (wid == 0) nkeep += (double)__popc(kb);
+        uint32_t kb[G16_QN];
+#pragma unroll
+        for (int k = 0; k < G16_QN; ++k) {
+            const int64_t r = r0 + 4 * lane + 4 * WAVE * k;
+            kb[k] = (kw[k] >> (r & 31)) & 0xFu;
+            if (r0 + G16_R > c1) kb[k] &= r >= c1 ? 0u : (r + 4 > c1 ? (1u << (int)(c1 - r)) - 1u : 0xFu);
+            if (wid == 0) nkeep += (double)__popc(kb[k]);
+        }
         __syncthreads();                               // the previous k-step's operand reads are done
 #pragma unroll
-        for (int j = 0; j < G16_CPW; ++j)
-            g16_stage_any(gc[j].dtype, raw[j], kb, K[j], csum[j], &s_y[(wid + G16_W * j) * G16_P + 4 * lane]);
+        for (int k = 0; k < G16_QN; ++k)
+#pragma unroll
+            for (int j = 0; j < G16_CPW; ++j)
+                g16_stage_any(gc[j].dtype, raw[k][j], kb[k], K[j], csum[j],
+                              &s_y[(wid + G16_W * j) * G16_P + 4 * lane + 4 * WAVE * k]);
         if (r0 + G16_R < c1) load(r0 + G16_R);
         __syncthreads();
-        // this wave's row groups wid, wid + 4, wid + 8, wid + 12: MFMA m takes row 4q + m
+        // this wave's row groups wid + 4 g: MFMA m takes row 4q + m of the group
 #pragma unroll
-        for (int g = 0; g < 4; ++g) {
+        for (int g = 0; g < 4 * G16_QN; ++g) {
             const d4 v = *(const d4 *)&s_y[cl * G16_P + 16 * (wid + G16_W * g) + 4 * q];
 #pragma unroll
             for (int m = 0; m < 4; ++m) acc = __builtin_amdgcn_mfma_f64_16x16x4f64(v[m], v[m], acc, 0, 0, 0);
