@@ -1260,14 +1260,31 @@ __global__ void __launch_bounds__(SD_T) sorted_distinct_kernel(sdp_column col, u
         }
         d += dl;
     }
+    // one set of atomics per workgroup (per wave, 4 x 32 K same-address atomics
+    // cost ~1 ms per launch whatever the column length)
+    __shared__ uint64_t s_d[SD_T / WAVE];
+    __shared__ int64_t s_f[SD_T / WAVE], s_l[SD_T / WAVE];
+    __shared__ int s_v[SD_T / WAVE];
+    const int wid = threadIdx.x / WAVE;
     d = wave_sum_u64(d);
     const bool any_viol = __any(viol);
     const int64_t fmin = wave_min_i64(first), lmax = wave_max_i64(last);
-    if (lane_id() == 0) {
-        if (d) atomicAdd((unsigned long long *)&out[0], (unsigned long long)d);
-        if (any_viol) atomicOr((unsigned long long *)&out[1], 1ull);
-        if (fmin != INT64_MAX) atomicMin((long long *)&out[2], (long long)fmin);
-        if (lmax >= 0) atomicMax((long long *)&out[3], (long long)lmax);
+    if (lane == 0) { s_d[wid] = d; s_v[wid] = any_viol ? 1 : 0; s_f[wid] = fmin; s_l[wid] = lmax; }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint64_t bd = 0;
+        int bv = 0;
+        int64_t bf = INT64_MAX, bl = -1;
+        for (int w = 0; w < SD_T / WAVE; ++w) {
+            bd += s_d[w];
+            bv |= s_v[w];
+            bf = min(bf, s_f[w]);
+            bl = max(bl, s_l[w]);
+        }
+        if (bd) atomicAdd((unsigned long long *)&out[0], (unsigned long long)bd);
+        if (bv) atomicOr((unsigned long long *)&out[1], 1ull);
+        if (bf != INT64_MAX) atomicMin((long long *)&out[2], (long long)bf);
+        if (bl >= 0) atomicMax((long long *)&out[3], (long long)bl);
     }
 }
 __global__ void sorted_distinct_init_kernel(uint64_t *out) {
@@ -2264,7 +2281,8 @@ extern "C" int sdp_sorted_distinct(const sdp_column *col, uint64_t *d_out, void 
     rc = check_launch("sorted_distinct_init_kernel");
     if (rc) return rc;
     const int64_t groups = (col->length + SD_V - 1) / SD_V;
-    const int grid = (int)std::min<int64_t>(std::max<int64_t>((groups + SD_T - 1) / SD_T, 1), 8192);
+    // (2048 workgroups: one resident round, eight per CU)
+    const int grid = (int)std::min<int64_t>(std::max<int64_t>((groups + SD_T - 1) / SD_T, 1), 2048);
     SDP_DISPATCH_NUMERIC(col->dtype,
         hipLaunchKernelGGL(sorted_distinct_kernel<T>, dim3(grid), dim3(SD_T), 0, s, *col, d_out);
         hipLaunchKernelGGL(sorted_distinct_final_kernel<T>, dim3(1), dim3(1), 0, s, *col, d_out));
