@@ -2155,16 +2155,22 @@ __global__ void __launch_bounds__(ST) d32_scatter1_kernel(sdp_column col, int64_
 }
 
 // level 2: every level-1 run (bucket b1, block g) -> its 64 sub-buckets
+// Workgroup (b1, j) of a GG-per-bucket grid takes the level-1 chunks g0 .. g1 - 1
+// of bucket b1 as one record range: consecutive chunks of a bucket are
+// adjacent in the input, and so are their runs of every sub-bucket in the
+// output, so one cursor per sub-bucket runs across them (one workgroup per
+// chunk -- ~1900 records each at 1.25e8 rows -- cost 0.96 ms per launch there
+// in fixed per-workgroup work, against 0.27 ms of bytes).
 __global__ void __launch_bounds__(ST) d32_scatter2_kernel(const uint32_t *in, const uint64_t *offs1,
-                                                           const uint64_t *offs2, int G, uint32_t *out) {
+                                                           const uint64_t *offs2, int G, int GG, uint32_t *out) {
     __shared__ D32ScatterLds s;
     const int t = threadIdx.x;
-    const int64_t c = blockIdx.x;                          // = b1 * G + g
-    const int b1 = (int)(c / G), g = (int)(c % G);
-    const uint64_t start = offs1[c], end = offs1[c + 1];
+    const int b1 = (int)(blockIdx.x / GG), j = (int)(blockIdx.x % GG);
+    const int g0 = (int)((int64_t)j * G / GG), g1 = (int)((int64_t)(j + 1) * G / GG);
+    const uint64_t start = offs1[(int64_t)b1 * G + g0], end = offs1[(int64_t)b1 * G + g1];
     for (int b = t; b < D32_NB2; b += ST) {
         s.hist[b] = 0;
-        s.cur[b] = offs2[((int64_t)b1 * D32_NB2 + b) * G + g];
+        s.cur[b] = offs2[((int64_t)b1 * D32_NB2 + b) * G + g0];
     }
     lds_barrier();
     for (uint64_t base = start; base < end; base += S_TILE) {
@@ -2558,7 +2564,10 @@ int sdp_distinct32(const sdp_column *col, int64_t lo, const uint32_t *d_hist1, v
     }
 #undef D32_LAUNCH_ROWS
     if ((rc = sdp_scan_u32(L.h2, (int64_t)D32_NF * G, L.offs2, L.scan2, L.scan2_bytes, stream))) return rc;
-    hipLaunchKernelGGL(d32_scatter2_kernel, dim3(D32_NB1 * G), dim3(ST), 0, s, L.recs1, L.offs1, L.offs2, G, L.recs2);
+    // ~64 K records per workgroup (the column's rows spread evenly over the 64 buckets)
+    const int GG = (int)std::max<int64_t>(1, std::min<int64_t>(G, col->length / ((int64_t)D32_NB1 * 65536)));
+    hipLaunchKernelGGL(d32_scatter2_kernel, dim3(D32_NB1 * GG), dim3(ST), 0, s, L.recs1, L.offs1, L.offs2, G, GG,
+                       L.recs2);
     if ((rc = check_launch("d32_scatter2_kernel"))) return rc;
     hipLaunchKernelGGL(d32_bitmap_kernel, dim3(D32_NF), dim3(1024), 0, s, L.recs2, L.offs2, G, d_out);
     return check_launch("d32_bitmap_kernel");

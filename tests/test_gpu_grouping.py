@@ -210,16 +210,18 @@ def _distinct32(arr, lo=0):
     return d, rows
 
 
-@pytest.mark.parametrize('case', ['f32_norm', 'f32_special', 'i32_full', 'u32_full', 'i64_window', 'tiny'])
+@pytest.mark.parametrize('case', ['f32_norm', 'f32_special', 'i32_full', 'u32_full', 'i64_window', 'tiny', 'f32_groups'])
 def test_distinct32_exact(case):
     """sdp_distinct32 (4-byte records in 64 x 64 buckets + LDS bitmaps) vs
     numpy, nulls skipped, NaN one value, -0.0 == 0.0, the ends of the 32-bit
-    key space (describe.py:143)."""
+    key space (describe.py:143); 'f32_groups' is long enough (> 2 x 64 x 65536
+    rows) for the level-2 scatter to split each bucket's chunks over several
+    workgroups."""
     g = datagen.rng(17)
-    n = N if case != 'tiny' else 1000
+    n = {'tiny': 1000, 'f32_groups': 9_000_017}.get(case, N)
     lo = 0
     mask = g.random(n) < 0.07
-    if case == 'f32_norm':
+    if case in ('f32_norm', 'f32_groups'):
         v = g.standard_normal(n).astype(np.float32)
     elif case == 'f32_special':
         v = g.standard_normal(n).astype(np.float32)
