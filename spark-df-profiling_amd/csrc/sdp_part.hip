@@ -301,8 +301,8 @@ __global__ void __launch_bounds__(CT) part_count_rows_u64_kernel(sdp_column col,
 // together, the L2 merges them), and only a segment's first and last lines are
 // written in part.  Used by the record scatters: fixed keys (f64_norm 1e9
 // records: 4.1-5.1 -> 3.1 ms) and byte keys' level-1 / level-2 (64-byte lines;
-// C3 step 11.5 -> 9.4 and 9.2 -> 7.1 ms); the row scatter gained nothing from it
-// (its time is not in the write stream).
+// C3 step 11.5 -> 9.4 and 9.2 -> 7.1 ms) and, since round 5, the row scatter
+// (scatter_rows_u64_wc_body: its time had moved with where its records land).
 // (WcLdsT<NA, L, NBM>: NA parallel record arrays (1 for fixed keys, 3 for the
 // k0 / k1 / meta of byte keys), lines of L records, at most NBM buckets.)
 template <int NA, int L, int NBM>
@@ -476,20 +476,84 @@ __device__ __forceinline__ void scatter_rows_u64_body(const sdp_column &col, con
     }
 }
 
+// The same scatter with write-combined output (round 5): the records of a
+// tile go to their buckets through wc_tile -- each bucket's current 128-byte
+// line assembled in LDS and written whole -- instead of leaving the sorted
+// tile as runs that start and end inside lines.  The row scatter's time moves
+// 20 % and more with where its records land (DRAM write back-pressure,
+// profiles/r05sp_*), while the write-combined level-2 scatter, which never
+// writes a partial line, holds within 3 % across the round's boxes.  Under
+// the probe's allocator states (profiles/r05af_rows_scatter_wc_probe_ab.log):
+// 4.23-5.36 vs 4.44-5.59 ms per 1e9-row f64 column, the arena state 4.2-4.7
+// vs 5.5-5.6.  (Round 4 measured a write-combined row scatter on one box as
+// no gain, 4.7-5.1 vs 4.5-5.0 ms.)
+struct ScatterWcLds {
+    HeavyLdsT<false> heavy;
+    WcLds wc;
+};
 template <typename T>
+__device__ __forceinline__ void scatter_rows_u64_wc_body(const sdp_column &col, const HeavyArg &heavy, int b1,
+                                                         int64_t rows_per_block, const uint64_t *offs,
+                                                         uint64_t *out_h, int xcd_map, const int G, const int bx) {
+    __shared__ ScatterWcLds s;
+    const int t = threadIdx.x;
+    const int g = (xcd_map && G % 8 == 0) ? (int)((bx % 8) * (G / 8) + bx / 8) : bx;
+    const int nb = 1 << b1;
+    const int shift = 64 - b1;
+    const int64_t r0 = (int64_t)g * rows_per_block;
+    const int64_t r1 = min(col.length, r0 + rows_per_block);
+    heavy_build<false>(s.heavy, heavy);
+    for (int b = t; b < nb; b += ST) wc_start(s.wc, b, offs[(int64_t)b * G + g]);
+    if (t == 0) s.wc.nlist = 0;
+    lds_barrier();
+    const bool any_heavy = heavy.n > 0;
+    constexpr int64_t TILE = (int64_t)ST * WC_RPT;
+    RowTile<T, ST, WC_RPT> tile;
+    const VBits vbm = vbits_init(col.d_validity, col.validity_bit_offset, col.d_values);
+    WcOut<1> out;
+    out.a[0] = out_h;
+    if (r0 < r1) tile.load(col, vbm, r0, r1);
+    for (int64_t base = r0; base < r1; base += TILE) {
+        uint64_t x[1][WC_RPT];
+        uint32_t vmask;
+        tile.hash(col, vbm, base, r1, x[0], vmask);
+        if (base + TILE < r1) tile.load(col, vbm, base + TILE, r1);      // next tile in flight
+        uint32_t have = 0;
+#pragma unroll
+        for (int q = 0; q < WC_RPT; ++q) {
+            if ((vmask >> q) & 1u) {
+                const int hv = any_heavy ? heavy_find_u64(s.heavy, heavy.n, x[0][q]) : -1;
+                if (hv < 0 && x[0][q] != EMPTY64) have |= 1u << q;
+            }
+        }
+        wc_tile<ST, WC_RPT>(s.wc, x, have, nb, out, [&](int q) { return b1 ? (int)(x[0][q] >> shift) : 0; });
+    }
+    for (int b = t; b < nb; b += ST) wc_flush_partial(s.wc, b, out);
+}
+
+template <typename T, bool WC>
 __global__ void __launch_bounds__(ST) part_scatter_rows_u64_kernel(sdp_column col, HeavyArg heavy, int b1,
                                                                    int64_t rows_per_block, const uint64_t *offs,
                                                                    uint64_t *out_h, int xcd_map) {
-    scatter_rows_u64_body<T>(col, heavy, b1, rows_per_block, offs, out_h, xcd_map, (int)gridDim.x, (int)blockIdx.x);
+    if constexpr (WC)
+        scatter_rows_u64_wc_body<T>(col, heavy, b1, rows_per_block, offs, out_h, xcd_map, (int)gridDim.x,
+                                    (int)blockIdx.x);
+    else
+        scatter_rows_u64_body<T>(col, heavy, b1, rows_per_block, offs, out_h, xcd_map, (int)gridDim.x,
+                                 (int)blockIdx.x);
 }
-template <typename T>
+template <typename T, bool WC>
 __global__ void __launch_bounds__(ST) part_scatter_rows_u64_batch_kernel(const sdp_rows_task *tasks, int xcd_map) {
     const sdp_rows_task &tk = tasks[blockIdx.y];
     if ((int)blockIdx.x >= tk.grid) return;
     const HeavyArg hv{tk.heavy.d_h, nullptr, nullptr, nullptr, tk.heavy.n};
     // (the XCD map needs the column's grid to be the launch's x extent)
-    scatter_rows_u64_body<T>(tk.col, hv, tk.b1, tk.rows_per_block, tk.d_offsets, tk.d_out,
-                             xcd_map && tk.grid == (int)gridDim.x, tk.grid, (int)blockIdx.x);
+    if constexpr (WC)
+        scatter_rows_u64_wc_body<T>(tk.col, hv, tk.b1, tk.rows_per_block, tk.d_offsets, tk.d_out,
+                                    xcd_map && tk.grid == (int)gridDim.x, tk.grid, (int)blockIdx.x);
+    else
+        scatter_rows_u64_body<T>(tk.col, hv, tk.b1, tk.rows_per_block, tk.d_offsets, tk.d_out,
+                                 xcd_map && tk.grid == (int)gridDim.x, tk.grid, (int)blockIdx.x);
 }
 
 // ---- rows -> L1 buckets (byte keys) ---------------------------------------------
@@ -1986,6 +2050,11 @@ static int grid_of(int64_t items, int64_t cap) {
     return (int)(items < cap ? items : cap);
 }
 
+// SDP_ROWS_WC=0: the row scatter writes the sorted tile's runs instead of write-combined lines (A/B runs)
+static int rows_wc_enabled() {
+    const char *e = getenv("SDP_ROWS_WC");
+    return (e && e[0] == '0') ? 0 : 1;
+}
 // SDP_XCD_MAP=0 turns the XCD-aware workgroup mapping of the scatters off (A/B runs)
 static int xcd_map_enabled() {
     const char *e = getenv("SDP_XCD_MAP");
@@ -1998,7 +2067,11 @@ static void launch_rows_u64(int phase, int grid, hipStream_t s, const sdp_column
     if (phase == 0)
         hipLaunchKernelGGL((part_count_rows_u64_kernel<T>), dim3(grid), dim3(CT), 0, s, c, hv, b1, rpb, hist, hc, st);
     else
-        hipLaunchKernelGGL((part_scatter_rows_u64_kernel<T>), dim3(grid), dim3(ST), 0, s, c, hv, b1, rpb, offs, out,
+        if (rows_wc_enabled())
+            hipLaunchKernelGGL((part_scatter_rows_u64_kernel<T, true>), dim3(grid), dim3(ST), 0, s, c, hv, b1, rpb, offs, out,
+                           xcd_map_enabled());
+        else
+            hipLaunchKernelGGL((part_scatter_rows_u64_kernel<T, false>), dim3(grid), dim3(ST), 0, s, c, hv, b1, rpb, offs, out,
                            xcd_map_enabled());
 }
 
@@ -2275,19 +2348,26 @@ int sdp_part_rows_batch(const sdp_rows_task *d_tasks, int32_t ntasks, int32_t dt
     hipStream_t s = (hipStream_t)stream;
     const dim3 grid(max_grid, ntasks);
     const int xm = xcd_map_enabled();
+    const bool wc = rows_wc_enabled();
+#define ROWS_BATCH(T)                                                                                        \
+    do {                                                                                                     \
+        if (wc) hipLaunchKernelGGL((part_scatter_rows_u64_batch_kernel<T, true>), grid, dim3(ST), 0, s, d_tasks, xm); \
+        else hipLaunchKernelGGL((part_scatter_rows_u64_batch_kernel<T, false>), grid, dim3(ST), 0, s, d_tasks, xm);   \
+    } while (0)
     switch (dtype) {
-    case SDP_F64: hipLaunchKernelGGL(part_scatter_rows_u64_batch_kernel<double>, grid, dim3(ST), 0, s, d_tasks, xm); break;
-    case SDP_F32: hipLaunchKernelGGL(part_scatter_rows_u64_batch_kernel<float>, grid, dim3(ST), 0, s, d_tasks, xm); break;
-    case SDP_I64: hipLaunchKernelGGL(part_scatter_rows_u64_batch_kernel<int64_t>, grid, dim3(ST), 0, s, d_tasks, xm); break;
-    case SDP_I32: hipLaunchKernelGGL(part_scatter_rows_u64_batch_kernel<int32_t>, grid, dim3(ST), 0, s, d_tasks, xm); break;
-    case SDP_I16: hipLaunchKernelGGL(part_scatter_rows_u64_batch_kernel<int16_t>, grid, dim3(ST), 0, s, d_tasks, xm); break;
-    case SDP_I8: hipLaunchKernelGGL(part_scatter_rows_u64_batch_kernel<int8_t>, grid, dim3(ST), 0, s, d_tasks, xm); break;
-    case SDP_U64: hipLaunchKernelGGL(part_scatter_rows_u64_batch_kernel<uint64_t>, grid, dim3(ST), 0, s, d_tasks, xm); break;
-    case SDP_U32: hipLaunchKernelGGL(part_scatter_rows_u64_batch_kernel<uint32_t>, grid, dim3(ST), 0, s, d_tasks, xm); break;
-    case SDP_U16: hipLaunchKernelGGL(part_scatter_rows_u64_batch_kernel<uint16_t>, grid, dim3(ST), 0, s, d_tasks, xm); break;
-    case SDP_U8: hipLaunchKernelGGL(part_scatter_rows_u64_batch_kernel<uint8_t>, grid, dim3(ST), 0, s, d_tasks, xm); break;
+    case SDP_F64: ROWS_BATCH(double); break;
+    case SDP_F32: ROWS_BATCH(float); break;
+    case SDP_I64: ROWS_BATCH(int64_t); break;
+    case SDP_I32: ROWS_BATCH(int32_t); break;
+    case SDP_I16: ROWS_BATCH(int16_t); break;
+    case SDP_I8: ROWS_BATCH(int8_t); break;
+    case SDP_U64: ROWS_BATCH(uint64_t); break;
+    case SDP_U32: ROWS_BATCH(uint32_t); break;
+    case SDP_U16: ROWS_BATCH(uint16_t); break;
+    case SDP_U8: ROWS_BATCH(uint8_t); break;
     default: return set_error(SDP_EINVAL, "part_rows_batch: dtype %d", dtype);
     }
+#undef ROWS_BATCH
     return check_launch("part_rows_batch");
 }
 
