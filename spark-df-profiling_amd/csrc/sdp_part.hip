@@ -688,6 +688,10 @@ __device__ __forceinline__ void bytes_tile_words(const sdp_bytes_column &col, co
         w[q][4] = (ok && need > 4) ? p[4] : 0u;
     }
 }
+// (round 5) every lane forms the short-string record, selects zero for an
+// invalid row, and only a wave holding a string of more than 16 bytes takes
+// the long-hash branch: the per-row valid / short / long branches had cost
+// ~160 scalar instructions per 64 rows in exec-mask bookkeeping
 template <int NT, int RPT>
 __device__ __forceinline__ void bytes_tile_decode(const sdp_bytes_column &col, int64_t base, const BytesOffs<RPT> &a,
                                                   const uint32_t (&w)[RPT][5], uint64_t (&k0)[RPT],
@@ -695,24 +699,29 @@ __device__ __forceinline__ void bytes_tile_decode(const sdp_bytes_column &col, i
                                                   int t) {
 #pragma unroll
     for (int q = 0; q < RPT; ++q) {
-        k0[q] = k1[q] = meta[q] = h[q] = 0;
-        if (!((a.vmask >> q) & 1u)) continue;
+        const bool ok = (a.vmask >> q) & 1u;
         const int64_t row = base + (int64_t)q * NT + t;
-        const int64_t len = a.ln[q];
-        if (len <= SHORT_MAX) {
-            const uint32_t sh = (uint32_t)((uintptr_t)(col.d_data + a.o0[q]) & 3);
-            const uint64_t v0 = (uint64_t)__builtin_amdgcn_alignbyte(w[q][1], w[q][0], sh) |
-                                ((uint64_t)__builtin_amdgcn_alignbyte(w[q][2], w[q][1], sh) << 32);
-            const uint64_t v1 = (uint64_t)__builtin_amdgcn_alignbyte(w[q][3], w[q][2], sh) |
-                                ((uint64_t)__builtin_amdgcn_alignbyte(w[q][4], w[q][3], sh) << 32);
-            k0[q] = mask_bytes(v0, len);
-            k1[q] = mask_bytes(v1, len - 8);
-            h[q] = bh_short(k0[q], k1[q], (uint64_t)len);
-        } else {
-            h[q] = hash_long_global(col.d_data + a.o0[q], len);
-            k0[q] = h[q];
+        const int64_t len = a.ln[q];                   // 0 for an invalid row
+        const uint32_t sh = (uint32_t)((uintptr_t)(col.d_data + a.o0[q]) & 3);
+        const uint64_t v0 = (uint64_t)__builtin_amdgcn_alignbyte(w[q][1], w[q][0], sh) |
+                            ((uint64_t)__builtin_amdgcn_alignbyte(w[q][2], w[q][1], sh) << 32);
+        const uint64_t v1 = (uint64_t)__builtin_amdgcn_alignbyte(w[q][3], w[q][2], sh) |
+                            ((uint64_t)__builtin_amdgcn_alignbyte(w[q][4], w[q][3], sh) << 32);
+        const uint64_t a0 = mask_bytes(v0, len), a1 = mask_bytes(v1, len - 8);
+        uint64_t hh = bh_short(a0, a1, (uint64_t)len);
+        uint64_t b0 = a0, b1 = a1;
+        const bool lng = ok && len > SHORT_MAX;
+        if (__ballot(lng)) {                           // wave-uniform, rare
+            if (lng) {
+                hh = hash_long_global(col.d_data + a.o0[q], len);
+                b0 = hh;
+                b1 = 0;
+            }
         }
-        meta[q] = ((uint64_t)min((int64_t)LEN_MAX, len) << 40) | (uint64_t)(row + 1);
+        k0[q] = ok ? b0 : 0;
+        k1[q] = ok ? b1 : 0;
+        h[q] = ok ? hh : 0;
+        meta[q] = ok ? (((uint64_t)min((int64_t)LEN_MAX, len) << 40) | (uint64_t)(row + 1)) : 0;
     }
 }
 
