@@ -117,6 +117,101 @@ __device__ void block_add_u64(uint64_t v, uint64_t *dst) {
         if (tot) atomicAdd((unsigned long long *)dst, (unsigned long long)tot);
     }
 }
+// Byte heavy keys of the records kernel (round 5): a slot holds the key's
+// hash, first 16 bytes, length and index, so one probe is one pair of 16-byte
+// LDS reads instead of the chain hash -> index -> key bytes, and the rows of a
+// lane are probed together (filter words, then first probes, each a batch of
+// independent reads; further probes only in a wave that needs one).  With the
+// chained form the heavy lookup took 3.9 of 11.6 ms of the records kernel on
+// a 1e8-label column (profiles/r05ai_*: the kernel without it, writing every
+// row as a record, ran 7.7 ms).
+struct HeavySlot {
+    uint64_t h, k0, k1;
+    uint32_t len;
+    int32_t idx;
+};
+template <int MAXK>
+struct HeavyRecT {
+    static constexpr int SLOTS = heavy_slots<MAXK>();
+    HeavySlot slot[SLOTS];
+    uint32_t filter[HEAVY_FILTER / 32];
+    uint32_t cnt[MAXK];
+};
+template <int MAXK>
+__device__ void heavy_rec_build(HeavyRecT<MAXK> &s, const HeavyArg &a) {
+    constexpr int SLOTS = HeavyRecT<MAXK>::SLOTS;
+    for (int i = threadIdx.x; i < SLOTS; i += blockDim.x) s.slot[i].h = EMPTY64;
+    for (int i = threadIdx.x; i < MAXK; i += blockDim.x) s.cnt[i] = 0;
+    for (int i = threadIdx.x; i < HEAVY_FILTER / 32; i += blockDim.x) s.filter[i] = 0;
+    lds_barrier();
+    for (int i = threadIdx.x; i < a.n; i += blockDim.x) {
+        const uint64_t h = a.h[i];
+        const uint32_t fb = heavy_filter_bit(h);
+        atomicOr(&s.filter[fb >> 5], 1u << (fb & 31));
+        uint32_t pos = (uint32_t)h & (SLOTS - 1);
+        while (true) {
+            const uint64_t old = atomicCAS((unsigned long long *)&s.slot[pos].h, (unsigned long long)EMPTY64,
+                                           (unsigned long long)h);
+            if (old == EMPTY64) break;
+            pos = (pos + 1) & (SLOTS - 1);
+        }
+        s.slot[pos].k0 = a.k0[i];
+        s.slot[pos].k1 = a.k1[i];
+        s.slot[pos].len = (uint32_t)(a.meta[i] >> 40);
+        s.slot[pos].idx = i;
+    }
+    lds_barrier();
+}
+// heavy index of each of a lane's RPT rows (bit q of vmask: row q valid), or -1
+template <int MAXK, int RPT>
+__device__ __forceinline__ void heavy_rec_find(const HeavyRecT<MAXK> &s, int n, const uint64_t (&h)[RPT],
+                                               const uint64_t (&k0)[RPT], const uint64_t (&k1)[RPT],
+                                               const uint64_t (&meta)[RPT], uint32_t vmask, int (&hv)[RPT]) {
+    constexpr int SLOTS = HeavyRecT<MAXK>::SLOTS;
+#pragma unroll
+    for (int q = 0; q < RPT; ++q) hv[q] = -1;
+    if (n == 0) return;                                // (uniform)
+    uint32_t maybe = 0;
+#pragma unroll
+    for (int q = 0; q < RPT; ++q) {
+        const uint32_t fb = heavy_filter_bit(h[q]);
+        const uint32_t fw = s.filter[fb >> 5];
+        const bool c = ((vmask >> q) & 1u) && (uint32_t)(meta[q] >> 40) <= (uint32_t)SHORT_MAX && h[q] != EMPTY64;
+        maybe |= (uint32_t)(c && ((fw >> (fb & 31)) & 1u)) << q;
+    }
+    uint32_t more = 0;
+    uint32_t pos[RPT];
+#pragma unroll
+    for (int q = 0; q < RPT; ++q) {
+        pos[q] = (uint32_t)h[q] & (SLOTS - 1);
+        const HeavySlot sl = s.slot[pos[q]];           // every lane reads (no branch); masked below
+        const bool m = (maybe >> q) & 1u;
+        const bool eq = sl.h == h[q] && sl.k0 == k0[q] && sl.k1 == k1[q] && sl.len == (uint32_t)(meta[q] >> 40);
+        if (m && eq) hv[q] = sl.idx;
+        more |= (uint32_t)(m && !eq && sl.h != EMPTY64) << q;
+    }
+    while (__ballot(more != 0)) {                      // rare: further probes
+#pragma unroll
+        for (int q = 0; q < RPT; ++q) {
+            if ((more >> q) & 1u) {
+                pos[q] = (pos[q] + 1) & (SLOTS - 1);
+                const HeavySlot sl = s.slot[pos[q]];
+                if (sl.h == h[q] && sl.k0 == k0[q] && sl.k1 == k1[q] && sl.len == (uint32_t)(meta[q] >> 40)) {
+                    hv[q] = sl.idx;
+                    more &= ~(1u << q);
+                } else if (sl.h == EMPTY64) {
+                    more &= ~(1u << q);
+                }
+            }
+        }
+    }
+}
+template <int MAXK>
+__device__ void heavy_rec_flush(HeavyRecT<MAXK> &s, int n, uint64_t *counts) {
+    lds_barrier();
+    for (int i = threadIdx.x; i < n; i += blockDim.x)
+        if (s.cnt[i]) atomicAdd((unsigned long long *)&counts[i], (unsigned long long)s.cnt[i]);
+}
 template <bool BYTES, int MAXK>
 __device__ void heavy_flush(HeavyLdsT<BYTES, MAXK> &s, int n, uint64_t *counts) {
     lds_barrier();

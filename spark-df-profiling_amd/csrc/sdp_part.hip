@@ -881,10 +881,10 @@ constexpr int BR_W = BR_T / WAVE;
 constexpr int BR_RPT = 4;                   // rows per lane per tile
 
 struct BRecLds {
-    HeavyLdsT<true, HEAVY_MAX_REC> heavy;
+    HeavyRecT<HEAVY_MAX_REC> heavy;
     uint32_t hist[BR_W][MAXB];
 };
-static_assert(sizeof(BRecLds) <= 120 * 1024, "records kernel LDS");
+static_assert(sizeof(BRecLds) <= 150 * 1024, "records kernel LDS");
 
 constexpr int BR_MINB = 1;
 template <int OW>
@@ -901,7 +901,7 @@ __global__ void __launch_bounds__(BR_T, BR_MINB) part_records_rows_bytes_kernel(
     const int64_t rpw = rows_per_block / BR_W;                     // a multiple of WAVE * BR_RPT
     const int64_t s0 = min(col.length, (int64_t)g * rows_per_block + (int64_t)w * rpw);
     const int64_t s1 = min(col.length, s0 + rpw);
-    heavy_build<true>(s.heavy, heavy);
+    heavy_rec_build(s.heavy, heavy);
     for (int b = lane; b < nb; b += WAVE) s.hist[w][b] = 0;
     lds_barrier();
     uint64_t rows = 0;
@@ -918,13 +918,14 @@ __global__ void __launch_bounds__(BR_T, BR_MINB) part_records_rows_bytes_kernel(
         bytes_tile_issue<WAVE, BR_RPT, OW>(col, base + STEP, s1, raw, lane);   // the next tile's stage A
         bytes_tile_decode<WAVE, BR_RPT>(col, base, oc, wd, k0, k1, meta, h, lane);
         const uint32_t vmask = oc.vmask;
+        int hv[BR_RPT];
+        heavy_rec_find(s.heavy, heavy.n, h, k0, k1, meta, vmask, hv);
 #pragma unroll
         for (int q = 0; q < BR_RPT; ++q) {
             bool keep = false;
             if ((vmask >> q) & 1u) {
                 ++rows;
-                const int hv = heavy_find_bytes(s.heavy, heavy.n, h[q], k0[q], k1[q], (uint32_t)(meta[q] >> 40));
-                if (hv >= 0) atomicAdd(&s.heavy.cnt[hv], 1u);
+                if (hv[q] >= 0) atomicAdd(&s.heavy.cnt[hv[q]], 1u);
                 else keep = true;
             }
             const uint64_t m = __ballot(keep);
@@ -942,7 +943,7 @@ __global__ void __launch_bounds__(BR_T, BR_MINB) part_records_rows_bytes_kernel(
     lds_barrier();
     for (int b = lane; b < nb; b += WAVE) hist[(int64_t)b * C + c] = s.hist[w][b];
     if (lane == 0) chunks[c] = Chunk{s0, cur, c, C};
-    heavy_flush(s.heavy, heavy.n, heavy_counts);
+    heavy_rec_flush(s.heavy, heavy.n, heavy_counts);
     block_add_u64(rows, &stats[0]);
 }
 
