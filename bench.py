@@ -319,7 +319,8 @@ def label_kernels(label):
         st = 'count' if stage == 'count' else 'scatter'
         if dt == 'bytes':
             return ['sdp::part_%s_rows_bytes_kernel' % st]
-        return ['sdp::part_%s_rows_u64_kernel<%s>' % (st, _DT.get(dt, dt))]
+        # the scatter also carries its write-combining switch: <T, true|false>
+        return ['sdp::part_%s_rows_u64_kernel<%s%s' % (st, _DT.get(dt, dt), ',' if st == 'scatter' else '>')]
     if name == 'sdp_part_rows_records':
         return ['sdp::part_records_rows_bytes_kernel']
     if name == 'sdp_part_dedup':
@@ -336,7 +337,7 @@ def label_kernels(label):
 # PMC traffic summary the bench reads `roofline.traffic` from, chosen by name
 # (never by file mtime, which a git checkout scrambles): the newest committed
 # summary of the default workload (tools/gpu_traffic.sh -> tools/traffic_summary.py).
-TRAFFIC_SUMMARY = {'c3': 'profiles/r05h2_c3_traffic.json', 'c5': 'profiles/r04f_c5_traffic.json'}
+TRAFFIC_SUMMARY = {'c3': 'profiles/r05ai_c3_traffic.json', 'c5': 'profiles/r04f_c5_traffic.json'}
 
 
 def pmc_traffic(label, path, rows=None, workload=None):

@@ -46,3 +46,13 @@ def test_run_ranks_reprints_rank0_line_and_rc(capsys):
     assert bench.run_ranks(bad) == 3
     silent = [sys.executable, '-c', 'pass']
     assert bench.run_ranks(silent) == 1
+
+
+@pytest.mark.parametrize('label', ['sdp_part_rows[f64/scatter]', 'sdp_part_rows[i64/scatter]',
+                                   'sdp_part_rows_records[bytes/records]'])
+def test_committed_traffic_summary_covers_dominant_kernels(label):
+    """roofline.traffic comes from the committed PMC summary: each kernel that
+    has been the C3 bench's dominant one must map to its rocprof name there."""
+    path = bench.TRAFFIC_SUMMARY['c3']
+    traffic, src = bench.pmc_traffic(label, path, 1_000_000_000, 'c3')
+    assert src == path and traffic > 0
