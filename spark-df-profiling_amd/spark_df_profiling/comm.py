@@ -67,7 +67,7 @@ class LocalComm:
     def alltoall_counts(self, rows):
         return [list(r) for r in rows]
 
-    def allgather_object(self, obj):
+    def allgather_object(self, obj, cap=None):
         return [obj]
 
     def barrier(self):
@@ -197,13 +197,14 @@ class TorchComm:
     # object on any rank costs a second round sized by the largest
     OBJECT_CAP = 1 << 16
 
-    def allgather_object(self, obj):
+    def allgather_object(self, obj, cap=None):
         """all_gather_object in one tensor collective and ONE readback in the
         common case: every rank sends [size | pickled bytes padded to
         OBJECT_CAP] from pinned memory (no stream sync on the way in); torch's
         all_gather_object pays a pageable upload and two readbacks (sizes, then
         data).  A rank whose payload exceeds the cap makes every rank run a
-        second round of the largest size."""
+        second round of the largest size.  `cap` (the same on every rank)
+        raises the first round's size for a payload known to be large."""
         import pickle
         import numpy as np
         self.calls['allgather_object'] += 1
@@ -219,9 +220,11 @@ class TorchComm:
             outs = [torch.empty_like(t) for _ in range(self.world)]
             self.dist.all_gather(outs, t, group=self.group)
             return torch.stack(outs).cpu().numpy()
-        got = round_(self.OBJECT_CAP)
+        cap0 = max(self.OBJECT_CAP, int(cap or 0))
+        got = round_(cap0)
         sizes = [int(np.frombuffer(r[:8].tobytes(), dtype=np.int64)[0]) for r in got]
-        if max(sizes) > self.OBJECT_CAP:
+        if max(sizes) > cap0:
+            self.calls['allgather_object_round2'] += 1
             got = round_(max(sizes))
         return [pickle.loads(r[8:8 + sz].tobytes()) for r, sz in zip(got, sizes)]
 

@@ -28,6 +28,11 @@ from .utils import corr_from_gram, pretty_name
 
 OTHER_VALUES = '***Other Values***'                           # describe.py:262
 OTHER_DISTINCT = '***Other Values Distinct Count***'          # describe.py:263
+# sharded runs: the first all-gather round's room for one column's two
+# rendered histograms (base64 PNG strings, 25-28 KB pickled per column on
+# normal / lognormal / t3 / uniform data), so the images exchange needs no
+# second round (an overflow only costs that round)
+IMAGE_CAP_PER_COLUMN = 48 * 1024
 
 
 def fmt_bytesize(num, suffix='B'):
@@ -509,8 +514,9 @@ def describe(df, bins=10, corr_reject=0.9, **kwargs):
 
     images = {name: (fut.result() if hasattr(fut, 'result') else fut) for name, fut in pending.items()}
     if plots and sharded:
-        # one exchange of the rendered strings (~2 x 20 KB per NUM column)
-        for part in engine.comm.allgather_object(images):
+        # one exchange of the rendered strings (~28 KB per NUM column),
+        # in one round: the cap every rank derives from the same column count
+        for part in engine.comm.allgather_object(images, cap=IMAGE_CAP_PER_COLUMN * len(table.columns)):
             images.update(part)
     for name, (hist, mini) in images.items():
         ldesc[name]['histogram'], ldesc[name]['mini_histogram'] = hist, mini

@@ -49,6 +49,10 @@ def _worker(rank, world, port, q):
         # an object beyond the one-round cap on one rank: the second round
         big = {'rank': rank, 'blob': bytes([rank]) * (comm.OBJECT_CAP * 2 if rank == 1 else 10)}
         out['big'] = [(o['rank'], len(o['blob']), o['blob'][:1]) for o in comm.allgather_object(big)]
+        r2 = comm.calls['allgather_object_round2']
+        # the same object with a cap hint every rank agrees on: one round
+        out['big_cap'] = [len(o['blob']) for o in comm.allgather_object(big, cap=4 * comm.OBJECT_CAP)]
+        out['rounds2'] = (r2, comm.calls['allgather_object_round2'])
         # alltoallv (all_to_all_single, as on RCCL): rank r sends (r*10 + d) repeated d+1 times to rank d
         send = torch.cat([torch.full((d + 1,), rank * 10 + d, dtype=torch.int64) for d in range(world)])
         out['alltoallv'] = comm.alltoallv(send, [d + 1 for d in range(world)]).tolist()
@@ -95,6 +99,8 @@ def test_two_rank_merges():
         assert o['images'] == [('c0', ('h0', 'm0')), ('c1', ('h1', 'm1'))]
         from spark_df_profiling.comm import TorchComm
         assert o['big'] == [(0, 10, b'\x00'), (1, 2 * TorchComm.OBJECT_CAP, b'\x01')]
+        assert o['big_cap'] == [10, 2 * TorchComm.OBJECT_CAP]
+        assert o['rounds2'] == (1, 1)
         want = []
         for src in range(world):
             want += [src * 10 + r] * (r + 1)
