@@ -9,6 +9,12 @@ from SURVEY.md Appendix A ([upstream], Spark 2.x):
 * A.4 Percentile (exact, int columns)         * A.5 ApproximatePercentile -> the
   element at 1-based rank ceil(p*N) (defined contract)
 * A.6 histogram edges accumulated on the host * A.7 Corr (Pearson, listwise)
+  -- from float64 min / max for every column type: describe.py:209
+  `stats_df.ix[0]` upcasts the mixed int64 / float32 / float64 agg row to one
+  float64 Series before :211 (range) and :226 (edges), which overrides A.6's
+  int64 / float32 subtraction (tests/test_oracle_golden.py pins it on
+  datagen.wide_range_table: |min|, |max| > 2^53 and a float32 range that
+  rounds differently)
 * A.8 NaN/null: na.drop drops null and NaN; countDistinct counts NaN once;
   NaN orders above every number; -0.0 groups with 0.0 (3.x, recorded choice).
 
@@ -661,5 +667,12 @@ def _describe_with_raw(table, bins, corr_reject, plot, fast=False, pool=None, **
             freq_dict[var] = v
     if 'value_counts' in variable_stats.index:
         variable_stats = variable_stats.drop('value_counts')
-    out = {'table': table_stats, 'variables': variable_stats.T, 'freq': freq_dict}
+    variables = variable_stats.T
+    # integral NUM columns: their 'sum' is float(wrapped int64) (describe.py:200
+    # Sum of a LongType, upcast at :209), an exact value tests/compare.py checks
+    # with == rather than the fp64 tolerance
+    variables.attrs['integral_num'] = tuple(
+        name for name, raw in raws.items()
+        if raw.get('spark_type') in _INT_TYPES and name in ldesc and ldesc[name].get('type') == 'NUM')
+    out = {'table': table_stats, 'variables': variables, 'freq': freq_dict}
     return out, {'columns': raws, 'corr': corr}

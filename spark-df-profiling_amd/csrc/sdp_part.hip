@@ -240,14 +240,6 @@ struct CountLds {
     HeavyLdsT<false> heavy;
     uint32_t hist[MAXB];
 };
-struct ScatterLds {
-    HeavyLdsT<false> heavy;
-    uint32_t hist[MAXB];
-    uint32_t off[MAXB];
-    uint64_t cur[MAXB];
-    uint64_t stage[S_TILE];
-    uint32_t wsum[ST / WAVE];
-};
 
 template <typename T>
 __global__ void __launch_bounds__(CT) part_count_rows_u64_kernel(sdp_column col, HeavyArg heavy, int b1,
@@ -412,71 +404,7 @@ __device__ __forceinline__ void wc_tile(WcLdsT<NA, L, NBM> &s, const uint64_t (&
 constexpr int WC_RPT = 8;                       // records per thread per tile (16 spills registers, no faster)
 // block bx of a G-block grid (the batched launch runs several columns' grids
 // side by side, blockIdx.y = column)
-template <typename T>
-__device__ __forceinline__ void scatter_rows_u64_body(const sdp_column &col, const HeavyArg &heavy, int b1,
-                                                      int64_t rows_per_block, const uint64_t *offs, uint64_t *out_h,
-                                                      int xcd_map, const int G, const int bx) {
-    __shared__ ScatterLds s;
-    const int t = threadIdx.x;
-    // XCD-aware: workgroups are dealt to the 8 XCDs round robin; with the map,
-    // one XCD's workgroups take consecutive row blocks, so in every bucket the
-    // runs it writes at once are adjacent (one L2 sees both halves of a line
-    // two blocks share, and the XCD's write stream stays within fewer pages)
-    const int g = (xcd_map && G % 8 == 0) ? (int)((bx % 8) * (G / 8) + bx / 8) : bx;
-    const int nb = 1 << b1;
-    const int shift = 64 - b1;
-    const int64_t r0 = (int64_t)g * rows_per_block;
-    const int64_t r1 = min(col.length, r0 + rows_per_block);
-    heavy_build<false>(s.heavy, heavy);
-    for (int b = t; b < nb; b += ST) {
-        s.hist[b] = 0;
-        s.cur[b] = offs[(int64_t)b * G + g];
-    }
-    lds_barrier();
-    const bool any_heavy = heavy.n > 0;
-    RowTile<T, ST, S_RPT> tile;
-    const VBits vbm = vbits_init(col.d_validity, col.validity_bit_offset, col.d_values);
-    if (r0 < r1) tile.load(col, vbm, r0, r1);
-    for (int64_t base = r0; base < r1; base += S_TILE) {
-        uint64_t h[S_RPT];
-        uint32_t vmask;
-        tile.hash(col, vbm, base, r1, h, vmask);
-        if (base + S_TILE < r1) tile.load(col, vbm, base + S_TILE, r1);      // next tile in flight
-        uint32_t rank[S_RPT / 2] = {};          // 16 bits per row (< S_TILE): no VGPR spills
-        uint32_t keep = 0;
-#pragma unroll
-        for (int q = 0; q < S_RPT; ++q) {
-            if ((vmask >> q) & 1u) {
-                const int hv = any_heavy ? heavy_find_u64(s.heavy, heavy.n, h[q]) : -1;
-                if (hv < 0 && h[q] != EMPTY64) {
-                    keep |= 1u << q;
-                    rank[q / 2] |= atomicAdd(&s.hist[b1 ? (int)(h[q] >> shift) : 0], 1u) << (16 * (q & 1));
-                }
-            }
-        }
-        lds_barrier();
-        block_excl_scan<ST>(s.hist, s.off, nb, s.wsum);
-#pragma unroll
-        for (int q = 0; q < S_RPT; ++q)
-            if ((keep >> q) & 1u)
-                s.stage[s.off[b1 ? (int)(h[q] >> shift) : 0] + ((rank[q / 2] >> (16 * (q & 1))) & 0xFFFFu)] = h[q];
-        lds_barrier();
-        const uint32_t total = s.off[nb - 1] + s.hist[nb - 1];
-        for (uint32_t j = t; j < total; j += ST) {
-            const uint64_t x = s.stage[j];
-            const int b = b1 ? (int)(x >> shift) : 0;
-            ((__attribute__((address_space(1))) uint64_t *)out_h)[s.cur[b] + (j - s.off[b])] = x;
-        }
-        lds_barrier();
-        for (int b = t; b < nb; b += ST) {
-            s.cur[b] += s.hist[b];
-            s.hist[b] = 0;
-        }
-        lds_barrier();
-    }
-}
-
-// The same scatter with write-combined output (round 5): the records of a
+// The row scatter (write-combined since round 5): the records of a
 // tile go to their buckets through wc_tile -- each bucket's current 128-byte
 // line assembled in LDS and written whole -- instead of leaving the sorted
 // tile as runs that start and end inside lines.  The row scatter's time moves
@@ -531,29 +459,20 @@ __device__ __forceinline__ void scatter_rows_u64_wc_body(const sdp_column &col, 
     for (int b = t; b < nb; b += ST) wc_flush_partial(s.wc, b, out);
 }
 
-template <typename T, bool WC>
+template <typename T>
 __global__ void __launch_bounds__(ST) part_scatter_rows_u64_kernel(sdp_column col, HeavyArg heavy, int b1,
                                                                    int64_t rows_per_block, const uint64_t *offs,
                                                                    uint64_t *out_h, int xcd_map) {
-    if constexpr (WC)
-        scatter_rows_u64_wc_body<T>(col, heavy, b1, rows_per_block, offs, out_h, xcd_map, (int)gridDim.x,
-                                    (int)blockIdx.x);
-    else
-        scatter_rows_u64_body<T>(col, heavy, b1, rows_per_block, offs, out_h, xcd_map, (int)gridDim.x,
-                                 (int)blockIdx.x);
+    scatter_rows_u64_wc_body<T>(col, heavy, b1, rows_per_block, offs, out_h, xcd_map, (int)gridDim.x, (int)blockIdx.x);
 }
-template <typename T, bool WC>
+template <typename T>
 __global__ void __launch_bounds__(ST) part_scatter_rows_u64_batch_kernel(const sdp_rows_task *tasks, int xcd_map) {
     const sdp_rows_task &tk = tasks[blockIdx.y];
     if ((int)blockIdx.x >= tk.grid) return;
     const HeavyArg hv{tk.heavy.d_h, nullptr, nullptr, nullptr, tk.heavy.n};
     // (the XCD map needs the column's grid to be the launch's x extent)
-    if constexpr (WC)
-        scatter_rows_u64_wc_body<T>(tk.col, hv, tk.b1, tk.rows_per_block, tk.d_offsets, tk.d_out,
-                                    xcd_map && tk.grid == (int)gridDim.x, tk.grid, (int)blockIdx.x);
-    else
-        scatter_rows_u64_body<T>(tk.col, hv, tk.b1, tk.rows_per_block, tk.d_offsets, tk.d_out,
-                                 xcd_map && tk.grid == (int)gridDim.x, tk.grid, (int)blockIdx.x);
+    scatter_rows_u64_wc_body<T>(tk.col, hv, tk.b1, tk.rows_per_block, tk.d_offsets, tk.d_out,
+                                xcd_map && tk.grid == (int)gridDim.x, tk.grid, (int)blockIdx.x);
 }
 
 // ---- rows -> L1 buckets (byte keys) ---------------------------------------------
@@ -2060,11 +1979,6 @@ static int grid_of(int64_t items, int64_t cap) {
     return (int)(items < cap ? items : cap);
 }
 
-// SDP_ROWS_WC=0: the row scatter writes the sorted tile's runs instead of write-combined lines (A/B runs)
-static int rows_wc_enabled() {
-    const char *e = getenv("SDP_ROWS_WC");
-    return (e && e[0] == '0') ? 0 : 1;
-}
 // SDP_XCD_MAP=0 turns the XCD-aware workgroup mapping of the scatters off (A/B runs)
 static int xcd_map_enabled() {
     const char *e = getenv("SDP_XCD_MAP");
@@ -2077,11 +1991,7 @@ static void launch_rows_u64(int phase, int grid, hipStream_t s, const sdp_column
     if (phase == 0)
         hipLaunchKernelGGL((part_count_rows_u64_kernel<T>), dim3(grid), dim3(CT), 0, s, c, hv, b1, rpb, hist, hc, st);
     else
-        if (rows_wc_enabled())
-            hipLaunchKernelGGL((part_scatter_rows_u64_kernel<T, true>), dim3(grid), dim3(ST), 0, s, c, hv, b1, rpb, offs, out,
-                           xcd_map_enabled());
-        else
-            hipLaunchKernelGGL((part_scatter_rows_u64_kernel<T, false>), dim3(grid), dim3(ST), 0, s, c, hv, b1, rpb, offs, out,
+        hipLaunchKernelGGL((part_scatter_rows_u64_kernel<T>), dim3(grid), dim3(ST), 0, s, c, hv, b1, rpb, offs, out,
                            xcd_map_enabled());
 }
 
@@ -2358,12 +2268,7 @@ int sdp_part_rows_batch(const sdp_rows_task *d_tasks, int32_t ntasks, int32_t dt
     hipStream_t s = (hipStream_t)stream;
     const dim3 grid(max_grid, ntasks);
     const int xm = xcd_map_enabled();
-    const bool wc = rows_wc_enabled();
-#define ROWS_BATCH(T)                                                                                        \
-    do {                                                                                                     \
-        if (wc) hipLaunchKernelGGL((part_scatter_rows_u64_batch_kernel<T, true>), grid, dim3(ST), 0, s, d_tasks, xm); \
-        else hipLaunchKernelGGL((part_scatter_rows_u64_batch_kernel<T, false>), grid, dim3(ST), 0, s, d_tasks, xm);   \
-    } while (0)
+#define ROWS_BATCH(T) hipLaunchKernelGGL((part_scatter_rows_u64_batch_kernel<T>), grid, dim3(ST), 0, s, d_tasks, xm)
     switch (dtype) {
     case SDP_F64: ROWS_BATCH(double); break;
     case SDP_F32: ROWS_BATCH(float); break;

@@ -88,6 +88,35 @@ def small_edge_table():
     })
 
 
+def wide_range_table(n=4099, seed=53):
+    """Columns whose histogram range depends on the type the min / max have at
+    describe.py:211 / :226: stats_df.ix[0] (:209) upcasts
+    the agg row to float64, so the range and the accumulated edges are float64
+    arithmetic on float64(min) / float64(max) -- not int64 (|min|, |max| >
+    2^53 here, where float(int(max) - int(min)) rounds differently) and not
+    float32 (max - min rounds to another float32).  The int64 sum wraps."""
+    g = rng(seed)
+    big = g.integers(-(2 ** 60), 2 ** 61, n, dtype=np.int64)
+    big[0], big[1] = 2 ** 61 + 200, -(2 ** 60) - 200            # max / min
+    big[6:40] = 2 ** 61 + 100 - np.arange(34)                    # many values near the top edges
+    f32 = (g.standard_normal(n) * 1e3).astype(np.float32)
+    f32[0], f32[1] = np.float32(1.0e8), np.float32(-3.3333333)
+    # values right at the float64 edges of the float32 column
+    lo, hi = float(np.float32(-3.3333333)), float(np.float32(1.0e8))
+    w = (hi - lo) / 10.0
+    e, edges = lo, []
+    for _ in range(10):
+        edges.append(e)
+        e += w
+    f32[2:12] = np.array(edges, dtype=np.float32)
+    wrap = np.full(n, 2 ** 62, dtype=np.int64)                   # sum wraps past 2^63 several times
+    wrap[::3] = -(2 ** 61)
+    m = _mask(g, n, 0.03)
+    m[:12] = False
+    return pa.table({'i64_big': pa.array(big, mask=m), 'f32_range': pa.array(f32, mask=m),
+                     'i64_wrap': pa.array(wrap, mask=m)})
+
+
 def categorical_table(n, seed=7, card=(100, 5000)):
     g = rng(seed)
     words = np.array(['w%05d_%s' % (i, 'x' * (i % 13)) for i in range(max(card))], dtype=object)

@@ -33,7 +33,7 @@ def _check_hist(raw, want_raw):
 
 
 @pytest.mark.parametrize('maker', [datagen.legacy_table, datagen.legacy_table_pandas_typed,
-                                   datagen.small_edge_table])
+                                   datagen.small_edge_table, datagen.wide_range_table])
 def test_small_tables(maker):
     got, raw, want, want_raw = _run(maker())
     assert_describe_equal(got, want)

@@ -81,3 +81,45 @@ def test_corr_reject_order():
     assert v.loc['b', 'type'] == 'CORR' and v.loc['b', 'correlation_var'] == 'a'
     assert v.loc['e', 'type'] == 'CORR'
     assert d['table']['REJECTED'] == d['table']['CONST'] + d['table']['CORR']
+
+
+def _accumulate(lo, hi, bins=10):
+    w = (hi - lo) / float(bins)
+    e, out = lo, []
+    for _ in range(bins):
+        out.append(e)
+        e = e + w
+    return out
+
+
+def test_range_and_edges_are_float64_after_the_row_upcast():
+    """describe.py:209 `stats_df.ix[0]` turns the mixed int64 / float32 /
+    float64 agg row into one float64 Series before :211 (range) and :226
+    (generate_hist_data), so min / max are float64 there.  SURVEY.md A.6's
+    int64 (resp. float32) subtraction would give other ranges and edges on
+    these columns; the oracle follows the upcast."""
+    t = datagen.wide_range_table()
+    d, raw = oracle.profile_raw(t)
+    v = d['variables']
+    # int64 beyond 2^53: float64(max) - float64(min) != float(int(max) - int(min))
+    import pyarrow.compute as pc
+    mm = pc.min_max(t.column('i64_big'))
+    imax, imin = mm['max'].as_py(), mm['min'].as_py()
+    assert abs(imax) > 2 ** 53 and abs(imin) > 2 ** 53
+    assert v.loc['i64_big', 'range'] == float(imax) - float(imin)
+    assert float(imax) - float(imin) != float(imax - imin)
+    assert raw['columns']['i64_big']['hist']['edges'] == _accumulate(float(imin), float(imax))
+    assert _accumulate(float(imin), float(imax)) != [float(e) for e in _accumulate(imin, imax)]
+    # float32: the range in float32 rounds differently
+    mm = pc.min_max(t.column('f32_range'))
+    fmax, fmin = np.float32(mm['max'].as_py()), np.float32(mm['min'].as_py())
+    assert v.loc['f32_range', 'range'] == float(fmax) - float(fmin)
+    assert float(np.float32(fmax - fmin)) != float(fmax) - float(fmin)
+    assert raw['columns']['f32_range']['hist']['edges'] == _accumulate(float(fmin), float(fmax))
+    # the int64 sum wraps (Spark LongType Sum) and is compared exactly
+    w = t.column('i64_wrap')
+    wv = np.asarray(pc.drop_null(w).to_numpy(), dtype=np.int64)
+    s = int(np.sum(wv, dtype=np.int64))
+    assert abs(sum(int(x) for x in wv)) >= 2 ** 63          # it did wrap
+    assert v.loc['i64_wrap', 'sum'] == float(s)
+    assert set(v.attrs['integral_num']) >= {'i64_big', 'i64_wrap'}
