@@ -51,17 +51,19 @@ enum sdp_status {
 #define SDP_PART_SAMPLE       16384    /* heavy-key sample rows, fixed-width keys           */
 #define SDP_PART_SAMPLE_BYTES 65536    /* heavy-key sample rows, byte keys                  */
 #define SDP_PART_CHUNK        131072   /* level-2 records per chunk                         */
+#define SDP_L2_BLOCK          64       /* records per block of sdp_part_l2_blocks           */
 #define SDP_GSORT_MAX         8192     /* groups one sdp_sort_groups launch orders          */
 
 /* ---- layout handshake ------------------------------------------------------
  * SDP_ABI_VERSION changes whenever a struct below, a record layout or its hash
- * (6: fixed-key records are the one-multiply mix64 of sdp_common.h) or a policy
+ * (6: fixed-key records are the one-multiply mix64 of sdp_common.h; 7: level-2
+ * block layout, sdp_blocks) or a policy
  * constant above changes.  A host binding compares sdp_layout_info() with its
  * own view and refuses a library that disagrees (a record-layout mismatch
  * between the engine and the library once turned garbage metas into row
  * indices on the GPU). */
-#define SDP_ABI_VERSION 6
-#define SDP_LAYOUT_NSIZES 17
+#define SDP_ABI_VERSION 7
+#define SDP_LAYOUT_NSIZES 18
 typedef struct sdp_layout {
     int32_t abi_version;
     int32_t n_sizes;                   /* SDP_LAYOUT_NSIZES                           */
@@ -71,12 +73,13 @@ typedef struct sdp_layout {
     int32_t byte_record_stride;
     int32_t fixed_record_bytes;        /* fixed-key level-1 / level-2 records (mix64 h) */
     int32_t heavy_max, heavy_max_rec, heavy_min;
-    int32_t part_sample, part_sample_bytes, gsort_max, _pad;
+    int32_t part_sample, part_sample_bytes, gsort_max, l2_block;
     int64_t part_chunk;
     /* sizeof: sdp_column, sdp_bytes_column, sdp_records, sdp_heavy, sdp_chunk,
      * sdp_qplan, sdp_pass1_result, sdp_select_task, sdp_compact_task,
      * sdp_pass1_task, sdp_pass2_task, sdp_rows_task, sdp_pass2_result,
-     * sdp_minmax_result, sdp_distinct_result, sdp_topk_entry, sdp_topk_result */
+     * sdp_minmax_result, sdp_distinct_result, sdp_topk_entry, sdp_topk_result,
+     * sdp_blocks */
     int64_t sizes[SDP_LAYOUT_NSIZES];
 } sdp_layout;
 int sdp_layout_info(sdp_layout *out);      /* host only; always 0 */
@@ -606,6 +609,38 @@ int64_t sdp_distinct32_workspace_bytes(int64_t length);
  * the column is then read once here instead of twice. */
 int sdp_distinct32(const sdp_column *col, int64_t lo, const uint32_t *d_hist1, void *d_work, int64_t work_bytes,
                    uint64_t *d_out, void *stream);
+/* ---- level 2 without a count pass (round 6) --------------------------------
+ * One workgroup per level-1 bucket i (d_order[k]: the bucket the k-th
+ * workgroup takes, largest first) splits its records by hash bits
+ * [64-b1-b2, 64-b1) into blocks of SDP_L2_BLOCK records handed out in LDS from
+ * the bucket's block region [d_rbase[i], d_rbase[i+1]) (at least
+ * ceil(S_i / SDP_L2_BLOCK) + 2^b2 blocks): no count pass and no offsets.
+ * Bucket i = records [d_bstart[i], d_bstart[i+1]) of `in`, or (d_chunks
+ * non-NULL) the chunks d_chunks[d_coff[i] .. d_coff[i+1]) (start / end used).
+ * Output: block b holds out[b * SDP_L2_BLOCK ..); final bucket f = i * 2^b2 + j
+ * has d_fcnt[f] records, record r at block d_list[d_floff[f] + r / SDP_L2_BLOCK],
+ * slot r % SDP_L2_BLOCK.  d_bmeta: scratch, one u64 per block.  2^b2 <= 1024
+ * (fixed keys) / 512 (byte keys). */
+typedef struct sdp_blocks {
+    uint32_t *d_fcnt;       /* records per final bucket              */
+    uint32_t *d_floff;      /* first d_list entry per final bucket   */
+    uint32_t *d_list;       /* block ids, in order within each bucket */
+} sdp_blocks;
+int sdp_part_l2_blocks(const sdp_records *in, int32_t is_bytes, const uint64_t *d_bstart,
+                       const sdp_chunk *d_chunks, const int64_t *d_coff, const uint32_t *d_rbase,
+                       const uint32_t *d_order, int64_t nbuckets, int32_t b1, int32_t b2,
+                       const sdp_records *out, uint64_t *d_bmeta, const sdp_blocks *blk, void *stream);
+/* sdp_part_dedup over the final buckets of sdp_part_l2_blocks (the same modes
+ * and outputs; groups of f go to the block positions of its records 0 ..
+ * d_ngroups[f]). */
+int sdp_part_dedup_blocks(const sdp_records *in, int32_t is_bytes, const sdp_bytes_column *bcol,
+                          const sdp_blocks *blk, int64_t nbuckets, int32_t with_counts,
+                          uint64_t *d_out_key, uint64_t *d_out_cnt, uint32_t *d_ngroups,
+                          uint64_t *d_stats, void *stream);
+/* sdp_part_compact over block-laid buckets. */
+int sdp_part_compact_blocks(const uint64_t *d_src_a, const uint64_t *d_src_b, const sdp_blocks *blk,
+                            const uint32_t *d_ngroups, const uint64_t *d_out_offsets, int64_t nbuckets,
+                            uint64_t *d_dst_a, uint64_t *d_dst_b, void *stream);
 /* Pack the per-bucket groups: src[d_starts[f] ..+ngroups[f]) -> dst[d_out_offsets[f] ..). */
 int sdp_part_compact(const uint64_t *d_src_a, const uint64_t *d_src_b, const uint64_t *d_starts,
                      const uint32_t *d_ngroups, const uint64_t *d_out_offsets, int64_t nbuckets,

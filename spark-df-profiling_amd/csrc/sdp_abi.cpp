@@ -27,7 +27,7 @@ bool aligned16(const void *p) { return (((uintptr_t)p) & 15u) == 0; }
 }  // namespace sdp
 
 extern "C" const char *sdp_last_error(void) { return sdp::g_err; }
-extern "C" const char *sdp_version(void) { return "sdp-mi355x 0.5.0 (gfx950)"; }
+extern "C" const char *sdp_version(void) { return "sdp-mi355x 0.6.0 (gfx950)"; }
 
 // The layout this library was built with (include/sdp.h, SDP_ABI_VERSION): the
 // host binding refuses a library whose structs, record layout or grouping
@@ -47,11 +47,13 @@ extern "C" int sdp_layout_info(sdp_layout *out) {
     out->part_sample_bytes = SDP_PART_SAMPLE_BYTES;
     out->gsort_max = SDP_GSORT_MAX;
     out->part_chunk = SDP_PART_CHUNK;
+    out->l2_block = SDP_L2_BLOCK;
     const int64_t sz[SDP_LAYOUT_NSIZES] = {
         sizeof(sdp_column), sizeof(sdp_bytes_column), sizeof(sdp_records), sizeof(sdp_heavy), sizeof(sdp_chunk),
         sizeof(sdp_qplan), sizeof(sdp_pass1_result), sizeof(sdp_select_task), sizeof(sdp_compact_task),
         sizeof(sdp_pass1_task), sizeof(sdp_pass2_task), sizeof(sdp_rows_task), sizeof(sdp_pass2_result),
-        sizeof(sdp_minmax_result), sizeof(sdp_distinct_result), sizeof(sdp_topk_entry), sizeof(sdp_topk_result)};
+        sizeof(sdp_minmax_result), sizeof(sdp_distinct_result), sizeof(sdp_topk_entry), sizeof(sdp_topk_result),
+        sizeof(sdp_blocks)};
     for (int i = 0; i < SDP_LAYOUT_NSIZES; ++i) out->sizes[i] = sz[i];
     return SDP_OK;
 }

@@ -1177,7 +1177,263 @@ __global__ void __launch_bounds__(ST) part_scatter_recs_wc_kernel(const uint64_t
     if (t < nb) wc_flush_partial(s, t, out);
 }
 
+// ---- level 2 into blocks, no count pass (round 6) -----------------------------------
+// The exact-offset level 2 above needs a count pass over every record first
+// (part_count_recs_*: 7.6 GB read per 1e9-row f64 column) because several
+// workgroups fill one level-1 bucket's sub-buckets.  Here ONE workgroup owns a
+// whole level-1 bucket, so the cursors of its sub-buckets are its own and no
+// prior count is needed: sub-bucket j's records go to blocks of L2B records
+// that the workgroup hands out from the bucket's region in LDS (one LDS atomic
+// per sub-bucket per tile that crosses a block edge); every bucket's current
+// line is assembled in LDS and written whole (as wc_tile).  The region of
+// bucket i holds ceil(S_i / L2B) + nb2 blocks (each sub-bucket leaves at most
+// one block partly filled), so nothing can overflow.  At the end of the bucket
+// the workgroup writes every final bucket f = i * nb2 + j as (records fcnt[f],
+// block list at floff[f]) and fills the list in block order: record r of f
+// lives at list[floff[f] + r / L2B] * L2B + r % L2B.  The de-duplication and
+// compaction kernels read that layout (BLK template parameter).
+constexpr int L2B = 64;                          // records per block: one wave-wide load
+template <bool BYTES> struct L2BCfg {
+    static constexpr int NA = BYTES ? 3 : 1;
+    static constexpr int L = BYTES ? 8 : 16;     // records per line: 64 B (three arrays) / 128 B
+    static constexpr int NBM = BYTES ? 512 : MAXB;
+    static constexpr int RPT = BYTES ? 4 : WC_RPT;
+};
+template <int NA, int L, int NBM>
+struct L2BLds {
+    uint64_t line[NA][NBM][L];                   // sub-bucket j's current line
+    uint32_t cur[NBM];                           // records of j so far (bucket-local positions)
+    uint32_t cnt[NBM];                           // this tile's records of j
+    int32_t nbase[NBM];                          // block k of j allocated in this tile: nbase[j] + k (region-relative)
+    uint32_t cb[NBM];                            // region-relative block holding position cur[j] (cur % L2B != 0)
+    uint16_t list[NBM];                          // sub-buckets whose current line this tile completes
+    uint32_t nlist, next;
+    uint32_t wsum[ST / WAVE];
+};
+static_assert(sizeof(L2BLds<1, 16, MAXB>) <= 160 * 1024, "level-2 block scatter LDS (fixed keys)");
+static_assert(sizeof(L2BLds<3, 8, 512>) <= 160 * 1024, "level-2 block scatter LDS (byte keys)");
+
+// region-relative block of position p of sub-bucket j (p >= cur[j], within this tile's span)
+template <int NA, int L, int NBM>
+__device__ __forceinline__ uint32_t l2b_block(const L2BLds<NA, L, NBM> &s, int j, uint32_t p) {
+    const uint32_t c = s.cur[j], k = p / L2B;
+    return (k == c / L2B && (c % L2B) != 0) ? s.cb[j] : (uint32_t)(s.nbase[j] + (int32_t)k);
+}
+
+// i: bucket index; in_*: records; bucket i = records [bstart[i], bstart[i+1])
+// (chunks == nullptr) or the chunks chunks[coff[i] .. coff[i+1]) (start/end
+// used; the sharded owner's buckets arrive in one segment per source rank);
+// rbase[i]: the bucket's first block (rbase[i+1] - rbase[i] >= ceil(S_i / L2B)
+// + nb2); order[blockIdx.x]: the bucket this workgroup takes (largest first).
+// bmeta: scratch, one u64 per block (sub-bucket << 32 | block index in it).
+template <bool BYTES>
+__global__ void __launch_bounds__(ST) part_l2_blocks_kernel(const uint64_t *in_k0, const uint64_t *in_k1,
+                                                            const uint64_t *in_meta, const uint64_t *bstart,
+                                                            const Chunk *chunks, const int64_t *coff,
+                                                            const uint32_t *rbase, const uint32_t *order, int b1,
+                                                            int b2, uint64_t *out_k0, uint64_t *out_k1,
+                                                            uint64_t *out_meta, uint64_t *bmeta, uint32_t *blist,
+                                                            uint32_t *fcnt, uint32_t *floff) {
+    using C = L2BCfg<BYTES>;
+    constexpr int NA = C::NA, L = C::L, RPT = C::RPT;
+    constexpr int TILE = ST * RPT;
+    __shared__ L2BLds<NA, L, C::NBM> s;
+    const int t = threadIdx.x;
+    const int nb = 1 << b2;
+    const int shift = 64 - b1 - b2;
+    const uint64_t mask = (uint64_t)(nb - 1);
+    const uint32_t bi = order[blockIdx.x];
+    const uint32_t RB = rbase[bi];
+    uint64_t *out[NA];
+    out[0] = out_k0;
+    if constexpr (BYTES) { out[1] = out_k1; out[2] = out_meta; }
+    for (int j = t; j < nb; j += ST) { s.cur[j] = 0; s.cnt[j] = 0; }
+    if (t == 0) { s.nlist = 0; s.next = 0; }
+    lds_barrier();
+    const int64_t c0 = chunks ? coff[bi] : 0, c1 = chunks ? coff[bi + 1] : 1;
+    auto load_tile = [&](int64_t base, int64_t end, uint64_t (&a)[NA][RPT]) {
+#pragma unroll
+        for (int q = 0; q < RPT; ++q) {
+            const int64_t r = base + (int64_t)q * ST + t;
+            if (r < end) {
+                a[0][q] = in_k0[r];
+                if constexpr (BYTES) { a[1][q] = in_k1[r]; a[2][q] = in_meta[r]; }
+            }
+        }
+    };
+    for (int64_t c = c0; c < c1; ++c) {
+        const int64_t lo = chunks ? chunks[c].start : (int64_t)bstart[bi];
+        const int64_t hi = chunks ? chunks[c].end : (int64_t)bstart[bi + 1];
+        uint64_t k[NA][RPT];
+        if (lo < hi) load_tile(lo, hi, k);
+        for (int64_t base = lo; base < hi; base += TILE) {
+            uint64_t x[NA][RPT];
+            uint32_t have = 0;
+            uint32_t bkp[(RPT + 1) / 2] = {};            // sub-bucket of record q, 16 bits each
+#pragma unroll
+            for (int q = 0; q < RPT; ++q) {
+#pragma unroll
+                for (int a = 0; a < NA; ++a) x[a][q] = k[a][q];
+                if (base + (int64_t)q * ST + t < hi) {
+                    have |= 1u << q;
+                    uint64_t h;
+                    if constexpr (BYTES) h = rec_hash(x[0][q], x[1][q], x[2][q]);
+                    else h = x[0][q];
+                    bkp[q / 2] |= (uint32_t)((h >> shift) & mask) << (16 * (q & 1));
+                }
+            }
+            if (base + TILE < hi) load_tile(base + TILE, hi, k);     // next tile in flight
+            auto bk = [&](int q) { return (int)((bkp[q / 2] >> (16 * (q & 1))) & 0xFFFFu); };
+            // ranks within this tile's records of each sub-bucket
+            uint32_t r[(RPT + 1) / 2] = {};
+#pragma unroll
+            for (int q = 0; q < RPT; ++q)
+                if ((have >> q) & 1u) r[q / 2] |= atomicAdd(&s.cnt[bk(q)], 1u) << (16 * (q & 1));
+            lds_barrier();
+            // owners: blocks this tile starts (consecutive ids), lines it completes
+            for (int j = t; j < nb; j += ST) {
+                const uint32_t cc = s.cur[j], e = cc + s.cnt[j];
+                if (e > cc) {
+                    const uint32_t kf = (cc % L2B) ? cc / L2B + 1 : cc / L2B, kl = (e - 1) / L2B;
+                    if (kl >= kf) {
+                        const uint32_t nn = kl - kf + 1;
+                        const uint32_t b0 = atomicAdd(&s.next, nn);
+                        s.nbase[j] = (int32_t)b0 - (int32_t)kf;
+                        for (uint32_t u = 0; u < nn; ++u)
+                            bmeta[(uint64_t)RB + b0 + u] = ((uint64_t)j << 32) | (uint64_t)(kf + u);
+                    }
+                    if (e / L != cc / L) s.list[atomicAdd(&s.nlist, 1u)] = (uint16_t)j;
+                }
+            }
+            lds_barrier();
+            // records of the current line into LDS, of lines this tile fills
+            // entirely straight out, of the new partial line held back
+            uint32_t pend = 0;
+            uint64_t slots = 0;
+#pragma unroll
+            for (int q = 0; q < RPT; ++q) {
+                if ((have >> q) & 1u) {
+                    const int j = bk(q);
+                    const uint32_t cc = s.cur[j];
+                    const uint32_t p = cc + ((r[q / 2] >> (16 * (q & 1))) & 0xFFFFu), e = cc + s.cnt[j];
+                    if (p / L == cc / L) {
+#pragma unroll
+                        for (int a = 0; a < NA; ++a) s.line[a][j][p % L] = x[a][q];
+                    } else if (p / L != e / L) {
+                        const uint64_t o = ((uint64_t)RB + l2b_block(s, j, p)) * L2B + p % L2B;
+#pragma unroll
+                        for (int a = 0; a < NA; ++a) out[a][o] = x[a][q];
+                    } else {
+                        pend |= 1u << q;
+                        slots |= (uint64_t)(p % L) << (4 * q);
+                    }
+                }
+            }
+            lds_barrier();
+            // completed current lines: L lanes per line, one aligned write per array
+            const uint32_t nl = s.nlist;
+            for (uint32_t i = t / L; i < nl; i += ST / L) {
+                const int j = s.list[i], l = t & (L - 1);
+                const uint32_t p = (s.cur[j] / L) * L + l;
+                const uint64_t o = ((uint64_t)RB + l2b_block(s, j, p)) * L2B + p % L2B;
+#pragma unroll
+                for (int a = 0; a < NA; ++a) out[a][o] = s.line[a][j][l];
+            }
+            lds_barrier();
+#pragma unroll
+            for (int q = 0; q < RPT; ++q)
+                if ((pend >> q) & 1u) {
+                    const int j = bk(q), sl = (int)((slots >> (4 * q)) & 15);
+#pragma unroll
+                    for (int a = 0; a < NA; ++a) s.line[a][j][sl] = x[a][q];
+                }
+            for (int j = t; j < nb; j += ST) {
+                const uint32_t e = s.cur[j] + s.cnt[j];
+                if (e % L2B) s.cb[j] = l2b_block(s, j, e);
+                s.cur[j] = e;
+                s.cnt[j] = 0;
+            }
+            if (t == 0) s.nlist = 0;
+            lds_barrier();
+        }
+    }
+    // partial lines (positions < cur, so their block is cb)
+    for (int j = t; j < nb; j += ST) {
+        const uint32_t cc = s.cur[j];
+        if (cc % L) {
+            const uint64_t o = ((uint64_t)RB + s.cb[j]) * L2B + ((cc / L) * L) % L2B;
+            for (uint32_t l = 0; l < cc % L; ++l)
+#pragma unroll
+                for (int a = 0; a < NA; ++a) out[a][o + l] = s.line[a][j][l];
+        }
+        s.cnt[j] = (cc + L2B - 1) / L2B;                 // blocks of j
+    }
+    lds_barrier();
+    block_excl_scan<ST>(s.cnt, (uint32_t *)s.nbase, nb, s.wsum);
+    const uint64_t f0 = (uint64_t)bi << b2;
+    for (int j = t; j < nb; j += ST) {
+        fcnt[f0 + j] = s.cur[j];
+        floff[f0 + j] = RB + (uint32_t)s.nbase[j];
+    }
+    // the block lists, in block order within each sub-bucket (bmeta was written
+    // by other waves of this workgroup: their stores complete before the
+    // barrier, and device-scope loads read them from L2, not a stale L1 line)
+    __threadfence();
+    __syncthreads();
+    const uint32_t nblk = s.next;
+    for (uint32_t u = t; u < nblk; u += ST) {
+        const uint64_t m = __hip_atomic_load(&bmeta[(uint64_t)RB + u], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const int j = (int)(m >> 32);
+        blist[RB + (uint32_t)s.nbase[j] + (uint32_t)m] = RB + u;
+    }
+}
+
 // ---- final buckets: LDS grouping -------------------------------------------------
+// Records of a final bucket: contiguous [starts[f], starts[f+1]) (BLK false),
+// or fcnt[f] records in the blocks blist[floff[f] ..] of part_l2_blocks_kernel
+// (BLK true).  Bucket-local index i; lo = 0 for blocks.
+struct BlkArg {
+    const uint32_t *fcnt, *floff, *blist;
+};
+template <bool BLK>
+struct RecAt {
+    const uint32_t *blist;
+    uint32_t l0;
+    __device__ __forceinline__ int64_t at(int64_t i) const {
+        if constexpr (BLK) return (int64_t)blist[l0 + (uint32_t)(i / L2B)] * L2B + (i % L2B);
+        else return i;
+    }
+    // records rb + q * WAVE + lane start here (rb a multiple of WAVE,
+    // wave-uniform): the block is wave-uniform, so its list entry is a scalar
+    // load and the pointer a scalar base (the lists carry WV_Q entries of
+    // padding: a batch's last entries may lie past the bucket's blocks)
+    __device__ __forceinline__ const uint64_t *wave_base(const uint64_t *p, int64_t rb, int q) const {
+        if constexpr (BLK) {
+            static_assert(L2B == WAVE, "one block per wave-wide load");
+            const uint32_t li = __builtin_amdgcn_readfirstlane(l0 + (uint32_t)(rb / L2B) + (uint32_t)q);
+            return p + (uint64_t)blist[li] * L2B;
+        } else {
+            return p + rb + (int64_t)q * WAVE;
+        }
+    }
+};
+// bucket f's range and record mapping
+template <bool BLK>
+__device__ __forceinline__ RecAt<BLK> bucket_of(const uint64_t *starts, const BlkArg &ba, int64_t f, int64_t &lo,
+                                                int64_t &hi) {
+    RecAt<BLK> ra{nullptr, 0};
+    if constexpr (BLK) {
+        lo = 0;
+        hi = ba.fcnt[f];
+        ra.blist = ba.blist;
+        ra.l0 = ba.floff[f];
+    } else {
+        lo = starts[f];
+        hi = starts[f + 1];
+    }
+    return ra;
+}
+
 constexpr int DT = 1024;                // dedup threads per workgroup
 constexpr int D_U64 = 8192;             // table slots, fixed keys, distinct only (64 KB: 2 workgroups/CU)
 constexpr int D_U64C = 8192;            // fixed keys with counts (96 KB)
@@ -1190,9 +1446,9 @@ constexpr int DU_BATCH = 8;             // records per thread loaded before prob
 // [4 + (f & 63)] groups.
 // Each round loads DU_BATCH records per thread (all loads in flight at once),
 // then inserts them: a bucket of <= 8 K records costs one memory latency (the next bucket batch is already in flight).
-template <bool COUNTS>
+template <bool COUNTS, bool BLK>
 __global__ void __launch_bounds__(DTU) part_dedup_u64_kernel(const uint64_t *in_h, const uint64_t *starts,
-                                                            int64_t nbuckets, uint64_t *out_key,
+                                                            BlkArg ba, int64_t nbuckets, uint64_t *out_key,
                                                             uint64_t *out_cnt, uint32_t *ngroups,
                                                             uint64_t *stats) {
     constexpr int S = COUNTS ? D_U64C : D_U64;
@@ -1203,31 +1459,31 @@ __global__ void __launch_bounds__(DTU) part_dedup_u64_kernel(const uint64_t *in_
     // the first batch of the next bucket is loaded while this one is probed
     int64_t f = blockIdx.x;
     int64_t lo = 0, hi = 0;
+    RecAt<BLK> ra{nullptr, 0};
     uint64_t hb[DU_BATCH];
     // per-block totals, flushed once (one global atomic per bucket would serialise
     // hundreds of thousands of device-scope atomics on a few addresses)
     uint64_t acc_groups = 0, acc_special = 0;
     bool acc_full = false;
-    auto load_batch = [&](int64_t from, int64_t to, uint64_t (&dst)[DU_BATCH]) {
+    auto load_batch = [&](const RecAt<BLK> &rr, int64_t from, int64_t to, uint64_t (&dst)[DU_BATCH]) {
 #pragma unroll
         for (int q = 0; q < DU_BATCH; ++q) {
             const int64_t r = from + (int64_t)q * DTU + t;
-            dst[q] = r < to ? in_h[r] : EMPTY64;
+            dst[q] = r < to ? in_h[rr.at(r)] : EMPTY64;
         }
     };
     if (f < nbuckets) {
-        lo = starts[f];
-        hi = starts[f + 1];
-        load_batch(lo, hi, hb);
+        ra = bucket_of<BLK>(starts, ba, f, lo, hi);
+        load_batch(ra, lo, hi, hb);
     }
     for (; f < nbuckets; f += gridDim.x) {
         const int64_t fn = f + gridDim.x;
         int64_t lo_n = 0, hi_n = 0;
+        RecAt<BLK> ra_n{nullptr, 0};
         uint64_t hn[DU_BATCH];
         if (fn < nbuckets) {
-            lo_n = starts[fn];
-            hi_n = starts[fn + 1];
-            load_batch(lo_n, hi_n, hn);
+            ra_n = bucket_of<BLK>(starts, ba, fn, lo_n, hi_n);
+            load_batch(ra_n, lo_n, hi_n, hn);
         }
         if (lo == hi) {
             if (COUNTS && t == 0) ngroups[f] = 0;
@@ -1241,7 +1497,7 @@ __global__ void __launch_bounds__(DTU) part_dedup_u64_kernel(const uint64_t *in_
             uint32_t fresh = 0, special = 0;
             bool full = false;
             for (int64_t rb = lo; rb < hi; rb += (int64_t)DTU * DU_BATCH) {
-                if (rb != lo) load_batch(rb, hi, hb);          // buckets beyond one batch
+                if (rb != lo) load_batch(ra, rb, hi, hb);      // buckets beyond one batch
                 // Lane-local queue: each lane walks its own records, so a long probe
                 // sequence delays only that lane's later records, not the whole wave.
                 const int64_t rem = hi - rb - t;
@@ -1289,8 +1545,9 @@ __global__ void __launch_bounds__(DTU) part_dedup_u64_kernel(const uint64_t *in_
                     const uint64_t h = s_key[i];
                     if (h != EMPTY64) {
                         const uint32_t p = atomicAdd(&s_n, 1u);
-                        out_key[lo + p] = inv_mix64(h);
-                        out_cnt[lo + p] = s_cnt[i];
+                        const int64_t o = ra.at(lo + p);
+                        out_key[o] = inv_mix64(h);
+                        out_cnt[o] = s_cnt[i];
                     }
                 }
                 lds_barrier();
@@ -1305,6 +1562,7 @@ __global__ void __launch_bounds__(DTU) part_dedup_u64_kernel(const uint64_t *in_
         }
         lo = lo_n;
         hi = hi_n;
+        ra = ra_n;
 #pragma unroll
         for (int q = 0; q < DU_BATCH; ++q) hb[q] = hn[q];
     }
@@ -1328,12 +1586,23 @@ constexpr int WV_W = 4;                 // waves per workgroup
 constexpr int WV_SLOTS = 2048;          // table slots per wave (16 KB)
 constexpr int WV_Q = 20;                // records per lane per batch
 constexpr int WV_BATCH = WV_Q * WAVE;   // 1280
-__device__ __forceinline__ void wave_load_batch(uint64_t (&hq)[WV_Q], const uint64_t *in_h, int64_t rb, int64_t hi,
-                                                int lane) {
+template <bool BLK>
+__device__ __forceinline__ void wave_load_batch(uint64_t (&hq)[WV_Q], const uint64_t *in_h, const RecAt<BLK> &ra,
+                                                int64_t rb, int64_t hi, int lane) {
+    if constexpr (BLK) {
+        const uint32_t bl = ra.blist[ra.l0 + (uint32_t)(rb / L2B) + (uint32_t)(lane < WV_Q ? lane : WV_Q - 1)];
+#pragma unroll
+        for (int q = 0; q < WV_Q; ++q) {
+            const int64_t r = rb + (int64_t)q * WAVE + lane;
+            const uint64_t *pb = in_h + (uint64_t)__builtin_amdgcn_readlane(bl, q) * L2B;
+            hq[q] = r < hi ? pb[lane] : EMPTY64;
+        }
+        return;
+    }
 #pragma unroll
     for (int q = 0; q < WV_Q; ++q) {
         const int64_t r = rb + (int64_t)q * WAVE + lane;
-        hq[q] = r < hi ? in_h[r] : EMPTY64;
+        hq[q] = r < hi ? ra.wave_base(in_h, rb, q)[lane] : EMPTY64;
     }
 }
 // Two-phase wave dedup (round 3).  The round-2 register-queue loop (each lane
@@ -1380,10 +1649,10 @@ __device__ __forceinline__ uint32_t wave2_probe(uint64_t *T, uint64_t x, bool &f
     }
 }
 // one batch (records rb + q * 64 + lane, q < WV_Q, below hi) -> new groups of this lane
-template <int MODE, bool LIMIT>
+template <int MODE, bool LIMIT, bool BLK>
 __device__ __forceinline__ uint32_t wave2_insert(uint64_t *T, uint64_t *O, const uint64_t (&hq)[WV_Q],
-                                                 const uint64_t *in_h, int64_t rb, int64_t hi, int lane,
-                                                 bool &full) {
+                                                 const uint64_t *in_h, const RecAt<BLK> &ra, int64_t rb, int64_t hi,
+                                                 int lane, bool &full) {
     const int64_t rem = hi - rb - lane;
     const int left = rem <= 0 ? 0 : (int)min((int64_t)WV_Q, (rem + WAVE - 1) / WAVE);
     uint64_t cur[WV_Q];
@@ -1437,16 +1706,16 @@ __device__ __forceinline__ uint32_t wave2_insert(uint64_t *T, uint64_t *O, const
     while (late) {                                           // list overflow: re-read from L2
         const int q = __builtin_ctz(late);
         late &= late - 1;
-        fresh += wave2_probe<MODE, LIMIT>(T, in_h[rb + (int64_t)q * WAVE + lane], full);
+        fresh += wave2_probe<MODE, LIMIT>(T, ra.wave_base(in_h, rb, q)[lane], full);
     }
     __builtin_amdgcn_wave_barrier();
     return fresh;
 }
 // ngroups (optional): groups of every bucket (a batch of columns' buckets in
 // one launch needs them per column)
-template <int MODE>
+template <int MODE, bool BLK>
 __global__ void __launch_bounds__(WV_W * WAVE) part_dedup_u64_wave2_kernel(const uint64_t *in_h,
-                                                                           const uint64_t *starts,
+                                                                           const uint64_t *starts, BlkArg ba,
                                                                            int64_t nbuckets, uint32_t *ngroups,
                                                                            uint64_t *stats) {
     __shared__ uint64_t tab[WV_W][WV_SLOTS];
@@ -1457,22 +1726,22 @@ __global__ void __launch_bounds__(WV_W * WAVE) part_dedup_u64_wave2_kernel(const
     uint64_t groups = 0;
     bool full = false;
     const int64_t stride = (int64_t)gridDim.x * WV_W;
-    int64_t f = (int64_t)blockIdx.x * WV_W + w;
+    int64_t f = (int64_t)__builtin_amdgcn_readfirstlane((int)(blockIdx.x * WV_W + w));
     int64_t lo = 0, hi = 0;
+    RecAt<BLK> ra{nullptr, 0};
     uint64_t hq[WV_Q];
     if (f < nbuckets) {
-        lo = starts[f];
-        hi = starts[f + 1];
-        wave_load_batch(hq, in_h, lo, hi, lane);
+        ra = bucket_of<BLK>(starts, ba, f, lo, hi);
+        wave_load_batch<BLK>(hq, in_h, ra, lo, hi, lane);
     }
     uint64_t hn[WV_Q];
     auto step = [&](uint64_t (&cur)[WV_Q], uint64_t (&nxt)[WV_Q]) {
         const int64_t fn = f + stride;
         int64_t lo_n = 0, hi_n = 0;
+        RecAt<BLK> ra_n{nullptr, 0};
         if (fn < nbuckets) {
-            lo_n = starts[fn];
-            hi_n = starts[fn + 1];
-            wave_load_batch(nxt, in_h, lo_n, hi_n, lane);
+            ra_n = bucket_of<BLK>(starts, ba, fn, lo_n, hi_n);
+            wave_load_batch<BLK>(nxt, in_h, ra_n, lo_n, hi_n, lane);
         }
         if (lo != hi) {
             ulonglong2 *T2 = (ulonglong2 *)T;
@@ -1481,11 +1750,11 @@ __global__ void __launch_bounds__(WV_W * WAVE) part_dedup_u64_wave2_kernel(const
             __builtin_amdgcn_wave_barrier();
             uint32_t fresh = 0;
             if (hi - lo <= WV_BATCH) {
-                fresh = wave2_insert<MODE, false>(T, O, cur, in_h, lo, hi, lane, full);
+                fresh = wave2_insert<MODE, false, BLK>(T, O, cur, in_h, ra, lo, hi, lane, full);
             } else {
                 for (int64_t rb = lo; rb < hi; rb += WV_BATCH) {
-                    if (rb != lo) wave_load_batch(cur, in_h, rb, hi, lane);
-                    fresh += wave2_insert<MODE, true>(T, O, cur, in_h, rb, hi, lane, full);
+                    if (rb != lo) wave_load_batch<BLK>(cur, in_h, ra, rb, hi, lane);
+                    fresh += wave2_insert<MODE, true, BLK>(T, O, cur, in_h, ra, rb, hi, lane, full);
                 }
             }
             groups += fresh;
@@ -1499,6 +1768,7 @@ __global__ void __launch_bounds__(WV_W * WAVE) part_dedup_u64_wave2_kernel(const
         }
         lo = lo_n;
         hi = hi_n;
+        ra = ra_n;
         f = fn;
     };
     while (f < nbuckets) {
@@ -1530,12 +1800,25 @@ constexpr int WH_SLOTS = 1024;
 constexpr int WH_Q = 16;                        // records per lane per batch (1024 per wave)
 constexpr int WH_BATCH = WH_Q * WAVE;
 constexpr int WH_OVF = 256;                     // collision-list entries per wave (2 KB)
-__device__ __forceinline__ void wave_load_batch16(uint64_t (&hq)[WH_Q], const uint64_t *in_h, int64_t rb, int64_t hi,
-                                                  int lane) {
+template <bool BLK>
+__device__ __forceinline__ void wave_load_batch16(uint64_t (&hq)[WH_Q], const uint64_t *in_h, const RecAt<BLK> &ra,
+                                                  int64_t rb, int64_t hi, int lane) {
+    if constexpr (BLK) {
+        // the batch's WH_Q list entries in one load (lane q holds block q),
+        // handed to the loads by readlane
+        const uint32_t bl = ra.blist[ra.l0 + (uint32_t)(rb / L2B) + (uint32_t)(lane < WH_Q ? lane : WH_Q - 1)];
+#pragma unroll
+        for (int q = 0; q < WH_Q; ++q) {
+            const int64_t r = rb + (int64_t)q * WAVE + lane;
+            const uint64_t *pb = in_h + (uint64_t)__builtin_amdgcn_readlane(bl, q) * L2B;
+            hq[q] = r < hi ? pb[lane] : EMPTY64;
+        }
+        return;
+    }
 #pragma unroll
     for (int q = 0; q < WH_Q; ++q) {
         const int64_t r = rb + (int64_t)q * WAVE + lane;
-        hq[q] = r < hi ? in_h[r] : EMPTY64;
+        hq[q] = r < hi ? ra.wave_base(in_h, rb, q)[lane] : EMPTY64;
     }
 }
 template <int MODE, bool LIMIT>
@@ -1557,10 +1840,10 @@ __device__ __forceinline__ uint32_t wh_probe(uint64_t *T, uint64_t x, bool &full
     }
 }
 // the records of half `hb` (hash bit 10) among this lane's batch -> new groups
-template <int MODE, bool LIMIT>
+template <int MODE, bool LIMIT, bool BLK>
 __device__ __forceinline__ uint32_t wh_insert(uint64_t *T, uint64_t *O, const uint64_t (&hq)[WH_Q],
-                                              const uint64_t *in_h, int64_t rb, int64_t hi, int lane, uint32_t hb,
-                                              bool &full) {
+                                              const uint64_t *in_h, const RecAt<BLK> &ra, int64_t rb, int64_t hi,
+                                              int lane, uint32_t hb, bool &full) {
     const int64_t rem = hi - rb - lane;
     const int left = rem <= 0 ? 0 : (int)min((int64_t)WH_Q, (rem + WAVE - 1) / WAVE);
     uint64_t cur[WH_Q];
@@ -1616,14 +1899,14 @@ __device__ __forceinline__ uint32_t wh_insert(uint64_t *T, uint64_t *O, const ui
     while (late) {
         const int q = __builtin_ctz(late);
         late &= late - 1;
-        fresh += wh_probe<MODE, LIMIT>(T, in_h[rb + (int64_t)q * WAVE + lane], full);
+        fresh += wh_probe<MODE, LIMIT>(T, ra.wave_base(in_h, rb, q)[lane], full);
     }
     __builtin_amdgcn_wave_barrier();
     return fresh;
 }
-template <int MODE>
+template <int MODE, bool BLK>
 __global__ void __launch_bounds__(WV_W * WAVE, 4) part_dedup_u64_half_kernel(const uint64_t *in_h,
-                                                                             const uint64_t *starts,
+                                                                             const uint64_t *starts, BlkArg ba,
                                                                              int64_t nbuckets, uint32_t *ngroups,
                                                                              uint64_t *stats) {
     // (no next-bucket prefetch in registers: 16 waves per CU hide the loads)
@@ -1636,11 +1919,12 @@ __global__ void __launch_bounds__(WV_W * WAVE, 4) part_dedup_u64_half_kernel(con
     bool full = false;
     const int64_t stride = (int64_t)gridDim.x * WV_W;
     for (int64_t f = (int64_t)blockIdx.x * WV_W + w; f < nbuckets; f += stride) {
-        const int64_t lo = starts[f], hi = starts[f + 1];
+        int64_t lo, hi;
+        const RecAt<BLK> ra = bucket_of<BLK>(starts, ba, f, lo, hi);
         uint32_t fresh = 0;
         if (lo != hi) {
             uint64_t hq[WH_Q];
-            wave_load_batch16(hq, in_h, lo, hi, lane);
+            wave_load_batch16<BLK>(hq, in_h, ra, lo, hi, lane);
             const bool one = hi - lo <= WH_BATCH;
 #pragma unroll 1
             for (uint32_t hb = 0; hb < 2; ++hb) {
@@ -1649,13 +1933,13 @@ __global__ void __launch_bounds__(WV_W * WAVE, 4) part_dedup_u64_half_kernel(con
                 for (int k = 0; k < WH_SLOTS / (2 * WAVE); ++k) T2[k * WAVE + lane] = make_ulonglong2(EMPTY64, EMPTY64);
                 __builtin_amdgcn_wave_barrier();
                 if (one) {
-                    fresh += wh_insert<MODE, false>(T, O, hq, in_h, lo, hi, lane, hb, full);
+                    fresh += wh_insert<MODE, false, BLK>(T, O, hq, in_h, ra, lo, hi, lane, hb, full);
                 } else {
                     // (a bucket beyond one batch: its batches are re-read from L2 per half)
 #pragma unroll 1
                     for (int64_t rb = lo; rb < hi; rb += WH_BATCH) {
-                        if (rb != lo || hb) wave_load_batch16(hq, in_h, rb, hi, lane);
-                        fresh += wh_insert<MODE, true>(T, O, hq, in_h, rb, hi, lane, hb, full);
+                        if (rb != lo || hb) wave_load_batch16<BLK>(hq, in_h, ra, rb, hi, lane);
+                        fresh += wh_insert<MODE, true, BLK>(T, O, hq, in_h, ra, rb, hi, lane, hb, full);
                     }
                 }
                 __builtin_amdgcn_wave_barrier();
@@ -1689,20 +1973,24 @@ constexpr int D_RPT = 4;
 struct DRound {
     uint64_t k0[D_RPT], k1[D_RPT], meta[D_RPT];
 };
+template <bool BLK>
 __device__ __forceinline__ void dedup_load_round(DRound &r, const uint64_t *in_k0, const uint64_t *in_k1,
-                                                 const uint64_t *in_meta, int64_t rb, int64_t hi) {
+                                                 const uint64_t *in_meta, const RecAt<BLK> &ra, int64_t rb,
+                                                 int64_t hi) {
 #pragma unroll
     for (int q = 0; q < D_RPT; ++q) {
         const int64_t i = rb + (int64_t)q * DT + threadIdx.x;
         const bool in = i < hi;
-        r.k0[q] = in ? in_k0[i] : 0ull;
-        r.k1[q] = in ? in_k1[i] : 0ull;
-        r.meta[q] = in ? in_meta[i] : 0ull;
+        const int64_t a = in ? ra.at(i) : 0;
+        r.k0[q] = in ? in_k0[a] : 0ull;
+        r.k1[q] = in ? in_k1[a] : 0ull;
+        r.meta[q] = in ? in_meta[a] : 0ull;
     }
 }
+template <bool BLK>
 __global__ void __launch_bounds__(DT) part_dedup_bytes_kernel(const uint64_t *in_k0, const uint64_t *in_k1,
                                                               const uint64_t *in_meta, const uint64_t *starts,
-                                                              int64_t nbuckets, sdp_bytes_column col,
+                                                              BlkArg ba, int64_t nbuckets, sdp_bytes_column col,
                                                               uint64_t *out_key, uint64_t *out_cnt,
                                                               uint32_t *ngroups, uint64_t *stats) {
     __shared__ uint64_t s_h[D_B];
@@ -1720,23 +2008,23 @@ __global__ void __launch_bounds__(DT) part_dedup_bytes_kernel(const uint64_t *in
     uint64_t acc_groups = 0;
     bool acc_full = false, acc_coll = false;
     int64_t f = blockIdx.x, lo = 0, hi = 0;
+    RecAt<BLK> ra{nullptr, 0};
     DRound cur, nxt;
     for (int i = t; i < D_B; i += DT) {                 // once: buckets reset only their own slots
         s_h[i] = EMPTY64;
         s_cnt[i] = 0;
     }
     if (f < nbuckets) {
-        lo = starts[f];
-        hi = starts[f + 1];
-        dedup_load_round(cur, in_k0, in_k1, in_meta, lo, hi);
+        ra = bucket_of<BLK>(starts, ba, f, lo, hi);
+        dedup_load_round<BLK>(cur, in_k0, in_k1, in_meta, ra, lo, hi);
     }
     for (; f < nbuckets; f += gridDim.x) {
         const int64_t fn = f + gridDim.x;
         int64_t lo_n = 0, hi_n = 0;
+        RecAt<BLK> ra_n{nullptr, 0};
         if (fn < nbuckets) {                                     // next bucket in flight
-            lo_n = starts[fn];
-            hi_n = starts[fn + 1];
-            dedup_load_round(nxt, in_k0, in_k1, in_meta, lo_n, hi_n);
+            ra_n = bucket_of<BLK>(starts, ba, fn, lo_n, hi_n);
+            dedup_load_round<BLK>(nxt, in_k0, in_k1, in_meta, ra_n, lo_n, hi_n);
         }
         if (lo == hi) {
             if (t == 0) ngroups[f] = 0;
@@ -1744,7 +2032,7 @@ __global__ void __launch_bounds__(DT) part_dedup_bytes_kernel(const uint64_t *in
             if (t == 0) { s_n = 0; s_full = 0; s_coll = 0; }
             lds_barrier();
             for (int64_t rb = lo; rb < hi; rb += (int64_t)DT * D_RPT) {
-                if (rb != lo) dedup_load_round(cur, in_k0, in_k1, in_meta, rb, hi);   // buckets beyond one round
+                if (rb != lo) dedup_load_round<BLK>(cur, in_k0, in_k1, in_meta, ra, rb, hi);   // buckets beyond one round
                 int pos[D_RPT];
                 uint32_t mine = 0;
 #pragma unroll
@@ -1810,8 +2098,9 @@ __global__ void __launch_bounds__(DT) part_dedup_bytes_kernel(const uint64_t *in
             for (uint32_t i = t; i < ng; i += DT) {                // the bucket's groups, claim order
                 const int p = s_list[i];
                 const uint64_t hk = s_h[p];
-                out_key[lo + i] = ((hk >> 40) << 40) | (s_meta[p] & RMASK40);
-                out_cnt[lo + i] = s_cnt[p];
+                const int64_t o = ra.at(lo + i);
+                out_key[o] = ((hk >> 40) << 40) | (s_meta[p] & RMASK40);
+                out_cnt[o] = s_cnt[p];
             }
             lds_barrier();
             for (uint32_t i = t; i < ng; i += DT) {                // reset the claimed slots
@@ -1829,6 +2118,7 @@ __global__ void __launch_bounds__(DT) part_dedup_bytes_kernel(const uint64_t *in
         }
         lo = lo_n;
         hi = hi_n;
+        ra = ra_n;
         cur = nxt;
     }
     if (t == 0) {
@@ -1839,16 +2129,20 @@ __global__ void __launch_bounds__(DT) part_dedup_bytes_kernel(const uint64_t *in
 }
 
 // groups of bucket f: src[starts[f] .. +ngroups[f]) -> dst[out_off[f] ..)
+template <bool BLK>
 __global__ void __launch_bounds__(PT) part_compact_kernel(const uint64_t *src_a, const uint64_t *src_b,
-                                                          const uint64_t *starts, const uint32_t *ngroups,
+                                                          const uint64_t *starts, BlkArg ba, const uint32_t *ngroups,
                                                           const uint64_t *out_off, int64_t nbuckets,
                                                           uint64_t *dst_a, uint64_t *dst_b) {
     for (int64_t f = blockIdx.x; f < nbuckets; f += gridDim.x) {
-        const int64_t lo = starts[f], o = out_off[f];
+        int64_t lo, hi;
+        const RecAt<BLK> ra = bucket_of<BLK>(starts, ba, f, lo, hi);
+        const int64_t o = out_off[f];
         const uint32_t m = ngroups[f];
         for (uint32_t i = threadIdx.x; i < m; i += PT) {
-            dst_a[o + i] = src_a[lo + i];
-            if (src_b) dst_b[o + i] = src_b[lo + i];
+            const int64_t a = ra.at(lo + i);
+            dst_a[o + i] = src_a[a];
+            if (src_b) dst_b[o + i] = src_b[a];
         }
     }
 }
@@ -2229,6 +2523,37 @@ __global__ void __launch_bounds__(1024) d32_bitmap_kernel(const uint32_t *in, co
 
 using namespace sdp;
 
+template <bool BLK>
+static int dedup_launch(const sdp_records *in, int32_t is_bytes, const sdp_bytes_column *bcol, const uint64_t *d_starts,
+                        const BlkArg &ba, int64_t nbuckets, int32_t with_counts, uint64_t *d_out_key,
+                        uint64_t *d_out_cnt, uint32_t *d_ngroups, uint64_t *d_stats, void *stream) {
+    if (in == nullptr || nbuckets < 1 || d_stats == nullptr) return set_error(SDP_EINVAL, "part_dedup: args");
+    if (((with_counts & 1) || is_bytes) && (d_out_key == nullptr || d_out_cnt == nullptr || d_ngroups == nullptr))
+        return set_error(SDP_EINVAL, "part_dedup: group outputs");
+    const int grid = grid_of(nbuckets, 256 * 8);
+    hipStream_t s = (hipStream_t)stream;
+    if (is_bytes) {
+        if (bcol == nullptr) return set_error(SDP_EINVAL, "part_dedup: byte keys need the column");
+        hipLaunchKernelGGL(part_dedup_bytes_kernel<BLK>, dim3(grid), dim3(DT), 0, s, in->d_k0, in->d_k1, in->d_meta,
+                           d_starts, ba, nbuckets, *bcol, d_out_key, d_out_cnt, d_ngroups, d_stats);
+    } else if (with_counts & 1) {
+        hipLaunchKernelGGL((part_dedup_u64_kernel<true, BLK>), dim3(grid), dim3(DTU), 0, s, in->d_k0, d_starts, ba,
+                           nbuckets, d_out_key, d_out_cnt, d_ngroups, d_stats);
+    } else if (with_counts & 2) {       // buckets beyond the wave tables (> 2^30 rows per device)
+        hipLaunchKernelGGL((part_dedup_u64_kernel<false, BLK>), dim3(grid), dim3(DTU), 0, s, in->d_k0, d_starts, ba,
+                           nbuckets, nullptr, nullptr, nullptr, d_stats);
+    } else {
+        const int wgrid = grid_of((nbuckets + WV_W - 1) / WV_W, 256 * 16);
+        if (with_counts & 4)            // near-unique keys: one CAS per probe, half-space tables
+            hipLaunchKernelGGL((part_dedup_u64_half_kernel<1, BLK>), dim3(wgrid), dim3(WV_W * WAVE), 0, s, in->d_k0,
+                               d_starts, ba, nbuckets, d_ngroups, d_stats);
+        else                            // repeated keys: read-first probes, 2048-slot tables
+            hipLaunchKernelGGL((part_dedup_u64_wave2_kernel<0, BLK>), dim3(wgrid), dim3(WV_W * WAVE), 0, s, in->d_k0,
+                               d_starts, ba, nbuckets, d_ngroups, d_stats);
+    }
+    return check_launch("part_dedup");
+}
+
 extern "C" {
 
 int64_t sdp_part_rows_per_block(int64_t length, int32_t is_bytes) {
@@ -2429,32 +2754,45 @@ int64_t sdp_part_bucket_target(int32_t is_bytes, int32_t with_counts) {
 int sdp_part_dedup(const sdp_records *in, int32_t is_bytes, const sdp_bytes_column *bcol, const uint64_t *d_starts,
                    int64_t nbuckets, int32_t with_counts, uint64_t *d_out_key, uint64_t *d_out_cnt,
                    uint32_t *d_ngroups, uint64_t *d_stats, void *stream) {
-    if (in == nullptr || d_starts == nullptr || nbuckets < 1 || d_stats == nullptr)
-        return set_error(SDP_EINVAL, "part_dedup: args");
-    if (((with_counts & 1) || is_bytes) && (d_out_key == nullptr || d_out_cnt == nullptr || d_ngroups == nullptr))
-        return set_error(SDP_EINVAL, "part_dedup: group outputs");
-    const int grid = grid_of(nbuckets, 256 * 8);
+    if (d_starts == nullptr) return set_error(SDP_EINVAL, "part_dedup: args");
+    return dedup_launch<false>(in, is_bytes, bcol, d_starts, BlkArg{nullptr, nullptr, nullptr}, nbuckets, with_counts,
+                               d_out_key, d_out_cnt, d_ngroups, d_stats, stream);
+}
+
+int sdp_part_dedup_blocks(const sdp_records *in, int32_t is_bytes, const sdp_bytes_column *bcol, const sdp_blocks *blk,
+                          int64_t nbuckets, int32_t with_counts, uint64_t *d_out_key, uint64_t *d_out_cnt,
+                          uint32_t *d_ngroups, uint64_t *d_stats, void *stream) {
+    if (blk == nullptr || blk->d_fcnt == nullptr || blk->d_floff == nullptr || blk->d_list == nullptr)
+        return set_error(SDP_EINVAL, "part_dedup_blocks: blocks");
+    return dedup_launch<true>(in, is_bytes, bcol, nullptr, BlkArg{blk->d_fcnt, blk->d_floff, blk->d_list}, nbuckets,
+                              with_counts, d_out_key, d_out_cnt, d_ngroups, d_stats, stream);
+}
+
+int sdp_part_l2_blocks(const sdp_records *in, int32_t is_bytes, const uint64_t *d_bstart, const sdp_chunk *d_chunks,
+                       const int64_t *d_coff, const uint32_t *d_rbase, const uint32_t *d_order, int64_t nbuckets,
+                       int32_t b1, int32_t b2, const sdp_records *out, uint64_t *d_bmeta, const sdp_blocks *blk,
+                       void *stream) {
+    if (in == nullptr || out == nullptr || d_rbase == nullptr || d_order == nullptr || d_bmeta == nullptr ||
+        blk == nullptr || blk->d_fcnt == nullptr || blk->d_floff == nullptr || blk->d_list == nullptr ||
+        nbuckets < 1 || nbuckets > INT32_MAX || b1 < 0 || b2 < 1 || b1 + b2 > 63)
+        return set_error(SDP_EINVAL, "part_l2_blocks: args");
+    if ((d_chunks == nullptr) == (d_bstart == nullptr) || (d_chunks != nullptr && d_coff == nullptr))
+        return set_error(SDP_EINVAL, "part_l2_blocks: exactly one of bstart / chunks");
+    if ((1 << b2) > (is_bytes ? L2BCfg<true>::NBM : L2BCfg<false>::NBM))
+        return set_error(SDP_EINVAL, "part_l2_blocks: %d sub-buckets", 1 << b2);
+    if (is_bytes && (in->d_k1 == nullptr || in->d_meta == nullptr || out->d_k1 == nullptr || out->d_meta == nullptr))
+        return set_error(SDP_EINVAL, "part_l2_blocks: byte records need k1/meta");
     hipStream_t s = (hipStream_t)stream;
-    if (is_bytes) {
-        if (bcol == nullptr) return set_error(SDP_EINVAL, "part_dedup: byte keys need the column");
-        hipLaunchKernelGGL(part_dedup_bytes_kernel, dim3(grid), dim3(DT), 0, s, in->d_k0, in->d_k1, in->d_meta,
-                           d_starts, nbuckets, *bcol, d_out_key, d_out_cnt, d_ngroups, d_stats);
-    } else if (with_counts & 1) {
-        hipLaunchKernelGGL(part_dedup_u64_kernel<true>, dim3(grid), dim3(DTU), 0, s, in->d_k0, d_starts, nbuckets,
-                           d_out_key, d_out_cnt, d_ngroups, d_stats);
-    } else if (with_counts & 2) {       // buckets beyond the wave tables (> 2^30 rows per device)
-        hipLaunchKernelGGL(part_dedup_u64_kernel<false>, dim3(grid), dim3(DTU), 0, s, in->d_k0, d_starts, nbuckets,
-                           nullptr, nullptr, nullptr, d_stats);
-    } else {
-        const int wgrid = grid_of((nbuckets + WV_W - 1) / WV_W, 256 * 16);
-        if (with_counts & 4)            // near-unique keys: one CAS per probe, half-space tables
-            hipLaunchKernelGGL(part_dedup_u64_half_kernel<1>, dim3(wgrid), dim3(WV_W * WAVE), 0, s, in->d_k0,
-                               d_starts, nbuckets, d_ngroups, d_stats);
-        else                            // repeated keys: read-first probes, 2048-slot tables
-            hipLaunchKernelGGL(part_dedup_u64_wave2_kernel<0>, dim3(wgrid), dim3(WV_W * WAVE), 0, s, in->d_k0,
-                               d_starts, nbuckets, d_ngroups, d_stats);
-    }
-    return check_launch("part_dedup");
+    const Chunk *ch = (const Chunk *)d_chunks;
+    if (is_bytes)
+        hipLaunchKernelGGL(part_l2_blocks_kernel<true>, dim3((uint32_t)nbuckets), dim3(ST), 0, s, in->d_k0, in->d_k1,
+                           in->d_meta, d_bstart, ch, d_coff, d_rbase, d_order, b1, b2, out->d_k0, out->d_k1,
+                           out->d_meta, d_bmeta, blk->d_list, blk->d_fcnt, blk->d_floff);
+    else
+        hipLaunchKernelGGL(part_l2_blocks_kernel<false>, dim3((uint32_t)nbuckets), dim3(ST), 0, s, in->d_k0, nullptr,
+                           nullptr, d_bstart, ch, d_coff, d_rbase, d_order, b1, b2, out->d_k0, nullptr, nullptr,
+                           d_bmeta, blk->d_list, blk->d_fcnt, blk->d_floff);
+    return check_launch("part_l2_blocks_kernel");
 }
 
 int sdp_part_compact(const uint64_t *d_src_a, const uint64_t *d_src_b, const uint64_t *d_starts,
@@ -2462,8 +2800,21 @@ int sdp_part_compact(const uint64_t *d_src_a, const uint64_t *d_src_b, const uin
                      uint64_t *d_dst_b, void *stream) {
     if (d_src_a == nullptr || d_dst_a == nullptr || nbuckets < 1 || (d_src_b != nullptr) != (d_dst_b != nullptr))
         return set_error(SDP_EINVAL, "part_compact: args");
-    hipLaunchKernelGGL(part_compact_kernel, dim3(grid_of(nbuckets, 8192)), dim3(PT), 0, (hipStream_t)stream, d_src_a,
-                       d_src_b, d_starts, d_ngroups, d_out_offsets, nbuckets, d_dst_a, d_dst_b);
+    hipLaunchKernelGGL(part_compact_kernel<false>, dim3(grid_of(nbuckets, 8192)), dim3(PT), 0, (hipStream_t)stream,
+                       d_src_a, d_src_b, d_starts, BlkArg{nullptr, nullptr, nullptr}, d_ngroups, d_out_offsets,
+                       nbuckets, d_dst_a, d_dst_b);
+    return check_launch("part_compact_kernel");
+}
+
+int sdp_part_compact_blocks(const uint64_t *d_src_a, const uint64_t *d_src_b, const sdp_blocks *blk,
+                            const uint32_t *d_ngroups, const uint64_t *d_out_offsets, int64_t nbuckets,
+                            uint64_t *d_dst_a, uint64_t *d_dst_b, void *stream) {
+    if (d_src_a == nullptr || d_dst_a == nullptr || nbuckets < 1 || (d_src_b != nullptr) != (d_dst_b != nullptr) ||
+        blk == nullptr || blk->d_fcnt == nullptr || blk->d_floff == nullptr || blk->d_list == nullptr)
+        return set_error(SDP_EINVAL, "part_compact_blocks: args");
+    hipLaunchKernelGGL(part_compact_kernel<true>, dim3(grid_of(nbuckets, 8192)), dim3(PT), 0, (hipStream_t)stream,
+                       d_src_a, d_src_b, nullptr, BlkArg{blk->d_fcnt, blk->d_floff, blk->d_list}, d_ngroups,
+                       d_out_offsets, nbuckets, d_dst_a, d_dst_b);
     return check_launch("part_compact_kernel");
 }
 

@@ -27,13 +27,14 @@ BITMAP_MAX_BITS = 1 << 20        # SDP_BITMAP_MAX_BITS
 
 # the grouping policy (include/sdp.h SDP_*), shared with the library's coarse
 # entries; _load() refuses a library built with other values
-ABI_VERSION = 6              # SDP_ABI_VERSION (6: records are the one-multiply mix64)
+ABI_VERSION = 7              # SDP_ABI_VERSION (7: level-2 block layout, sdp_blocks)
 HEAVY_MAX = 256              # SDP_HEAVY_MAX: the row kernels' heavy-key tables
 HEAVY_MAX_REC = 1024         # SDP_HEAVY_MAX_REC: byte keys on the records kernel
 HEAVY_MIN = 3                # SDP_HEAVY_MIN
 PART_SAMPLE = 16384          # SDP_PART_SAMPLE
 PART_SAMPLE_BYTES = 65536    # SDP_PART_SAMPLE_BYTES
 PART_CHUNK = 131072          # SDP_PART_CHUNK
+L2_BLOCK = 64                # SDP_L2_BLOCK: records per block of sdp_part_l2_blocks
 GSORT_MAX = 8192             # SDP_GSORT_MAX
 BYTE_RECORD_ARRAYS = 3       # byte-key records: k0[], k1[], meta[] (sdp_records)
 RECORD_WORD = 8              # bytes between one record's words in each array
@@ -149,9 +150,13 @@ class SdpTopkResult(ctypes.Structure):             # sdp_topk_result (sdp_value_
                 ('path', ctypes.c_int32)]
 
 
+class SdpBlocks(ctypes.Structure):                 # sdp_blocks (sdp_part_l2_blocks)
+    _fields_ = [('d_fcnt', ctypes.c_void_p), ('d_floff', ctypes.c_void_p), ('d_list', ctypes.c_void_p)]
+
+
 QUANTILES_MAX = 16       # SDP_QUANTILES_MAX
 
-LAYOUT_NSIZES = 17           # SDP_LAYOUT_NSIZES
+LAYOUT_NSIZES = 18           # SDP_LAYOUT_NSIZES
 
 
 class SdpLayout(ctypes.Structure):                 # sdp_layout (sdp_layout_info)
@@ -160,14 +165,14 @@ class SdpLayout(ctypes.Structure):                 # sdp_layout (sdp_layout_info
                 ('fixed_record_bytes', ctypes.c_int32), ('heavy_max', ctypes.c_int32),
                 ('heavy_max_rec', ctypes.c_int32), ('heavy_min', ctypes.c_int32),
                 ('part_sample', ctypes.c_int32), ('part_sample_bytes', ctypes.c_int32),
-                ('gsort_max', ctypes.c_int32), ('_pad', ctypes.c_int32), ('part_chunk', ctypes.c_int64),
+                ('gsort_max', ctypes.c_int32), ('l2_block', ctypes.c_int32), ('part_chunk', ctypes.c_int64),
                 ('sizes', ctypes.c_int64 * LAYOUT_NSIZES)]
 
 
 # the structs in sdp_layout.sizes order
 _LAYOUT_STRUCTS = [SdpColumn, SdpBytesColumn, SdpRecords, SdpHeavy, SdpChunk, SdpQPlan, SdpPass1Result,
                    SdpSelectTask, SdpCompactTask, SdpPass1Task, SdpPass2Task, SdpRowsTask, SdpPass2Result,
-                   SdpMinmaxResult, SdpDistinctResult, SdpTopkEntry, SdpTopkResult]
+                   SdpMinmaxResult, SdpDistinctResult, SdpTopkEntry, SdpTopkResult, SdpBlocks]
 
 
 def expected_layout():
@@ -176,6 +181,7 @@ def expected_layout():
             'byte_record_stride': RECORD_WORD, 'fixed_record_bytes': RECORD_WORD, 'heavy_max': HEAVY_MAX,
             'heavy_max_rec': HEAVY_MAX_REC, 'heavy_min': HEAVY_MIN, 'part_sample': PART_SAMPLE,
             'part_sample_bytes': PART_SAMPLE_BYTES, 'gsort_max': GSORT_MAX, 'part_chunk': PART_CHUNK,
+            'l2_block': L2_BLOCK,
             'sizes': [ctypes.sizeof(t) for t in _LAYOUT_STRUCTS]}
 
 
@@ -266,6 +272,11 @@ _SIGNATURES = {
     'sdp_part_rows_records': (ctypes.c_int, [_BCOL, _HVY, _I32, _P, _P, _REC, _P, _P, _P]),
     'sdp_part_dedup': (ctypes.c_int, [_REC, _I32, _BCOL, _P, _I64, _I32, _P, _P, _P, _P, _P]),
     'sdp_part_compact': (ctypes.c_int, [_P, _P, _P, _P, _P, _I64, _P, _P, _P]),
+    'sdp_part_l2_blocks': (ctypes.c_int, [_REC, _I32, _P, _P, _P, _P, _P, _I64, _I32, _I32, _REC, _P,
+                                          ctypes.POINTER(SdpBlocks), _P]),
+    'sdp_part_dedup_blocks': (ctypes.c_int, [_REC, _I32, _BCOL, ctypes.POINTER(SdpBlocks), _I64, _I32, _P, _P, _P,
+                                             _P, _P]),
+    'sdp_part_compact_blocks': (ctypes.c_int, [_P, _P, ctypes.POINTER(SdpBlocks), _P, _P, _I64, _P, _P, _P]),
     'sdp_distinct32_workspace_bytes': (_I64, [_I64]),
     'sdp_distinct32': (ctypes.c_int, [_COL, _I64, _P, _P, _I64, _P, _P]),
     'sdp_scan_workspace_bytes': (_I64, [_I64]),

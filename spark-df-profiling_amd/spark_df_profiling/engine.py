@@ -67,6 +67,11 @@ PASS1_BATCH = os.environ.get('SDP_PASS1_BATCH', '1') != '0'
 BITS32 = os.environ.get('SDP_BITS32', '1') != '0'
 # SDP_PASS2_BATCH=0: one sdp_pass2_count launch per column on wide tables too
 PASS2_BATCH = os.environ.get('SDP_PASS2_BATCH', '1') != '0'
+# level 2 into blocks, one workgroup per level-1 bucket, no count pass
+# (sdp_part_l2_blocks, round 6); SDP_L2_BLOCKS=0: the counted exact-offset
+# level 2 (sdp_part_recs phase 0 + 1) for A/B runs
+L2_BLOCKS = os.environ.get('SDP_L2_BLOCKS', '1') != '0'
+L2_BLOCK = nat.L2_BLOCK
 CAND_FULL_BUDGET = 1 << 30   # bytes of room-for-every-row candidate slots per pass-1 batch
 
 # Test knob for the quantile edge paths (never set in production):
@@ -1183,6 +1188,41 @@ class Engine:
                            keep[2].data_ptr() if isb else None)
         return r, keep
 
+    @staticmethod
+    def _l2b_ok(isb, b2):
+        """sdp_part_l2_blocks takes this level 2 (<= 1024 sub-buckets of fixed
+        keys, <= 512 of byte keys: the LDS lines of one workgroup)."""
+        return L2_BLOCKS and 1 <= b2 and (1 << b2) <= (512 if isb else 1024)
+
+    def _l2_blocks(self, r1, isb, b1, b2, sizes, bstart=None, chunks=None, coff=None):
+        """Level 2 of len(sizes) level-1 buckets (records per bucket `sizes`,
+        host array) into blocks (sdp_part_l2_blocks): bucket i is records
+        [bstart[i], bstart[i+1]) of r1 (device u64), or the chunks
+        chunks[coff[i] .. coff[i+1]).  No count pass, no scan: one workgroup per
+        bucket, largest first.  Returns (records, their tensors, SdpBlocks, the
+        block tensors)."""
+        nbk = len(sizes)
+        nb2 = 1 << b2
+        nblk = -(-np.asarray(sizes, dtype=np.int64) // L2_BLOCK) + nb2
+        rbase = np.zeros(nbk + 1, dtype=np.int64)
+        rbase[1:] = np.cumsum(nblk)
+        total = int(rbase[-1])
+        if total >= (1 << 32):
+            raise nat.NativeError('l2_blocks: %d blocks' % total)
+        order = np.argsort(-np.asarray(sizes), kind='stable')
+        ro = self._h2d(np.concatenate([rbase, order]).astype(np.uint32).view(np.int32))
+        rf, keepf = self._records(total * L2_BLOCK, isb)
+        bmeta = self._u64(total)
+        # (the dedup kernels read a batch's list entries in one load: padding)
+        lst = torch.empty(total + 32, dtype=torch.int32, device=self.device)
+        fc = torch.empty(2 * nbk * nb2, dtype=torch.int32, device=self.device)
+        blk = nat.SdpBlocks(fc.data_ptr(), fc.data_ptr() + 4 * nbk * nb2, lst.data_ptr())
+        sdp.sdp_part_l2_blocks(ctypes.byref(r1), int(isb), ptr(bstart), ptr(chunks), ptr(coff), ptr(ro),
+                               ctypes.c_void_p(ro.data_ptr() + 4 * (nbk + 1)), nbk, b1, b2, ctypes.byref(rf),
+                               ptr(bmeta), ctypes.byref(blk), self._s())
+        del bmeta, ro
+        return rf, keepf, blk, (fc, lst)
+
     def _heavy_keys(self, col, isb, gather=False):
         """Keys seen >= HEAVY_MIN times in an evenly spaced sample: counted
         outside the partitions (describe.py:251's hot groups).  gather=True
@@ -1481,9 +1521,16 @@ class Engine:
             sdp.sdp_part_rows(cref, bref, hvref, b1, 1, None, ptr(o1), ctypes.byref(r1), ptr(hcnt), ptr(stats), s)
         # level 2: each L1 bucket -> nb2 sub-buckets, chunk by chunk
         bstarts = o1[0:nb1 * grid:grid]
+        blk = None
         if b2 == 0 or nrec == 0:
             starts = torch.cat([bstarts, o1[-1:]]) if b2 == 0 else self._u64(nb1 * nb2 + 1, zero=True)
             rf, keepf = r1, keep1
+        elif self._l2b_ok(isb, b2):
+            nat.annotate(('bytes' if isb else 'u64') + '/l2blocks', 2 * nrec * recw)
+            rf, keepf, blk, blk_keep = self._l2_blocks(r1, isb, b1, b2, np.diff(bsn),
+                                                       bstart=torch.cat([bstarts, o1[-1:]]))
+            del keep1, r1
+            starts = None
         else:
             bs = bsn
             sizes = np.diff(bs)
@@ -1514,15 +1561,21 @@ class Engine:
         ngroups = torch.zeros(nfinal, dtype=torch.int32, device=self.device)
         out_key = out_cnt = None
         if with_counts:
-            out_key, out_cnt = self._u64(max(nrec, 1)), self._u64(max(nrec, 1))
+            nout = keepf[0].numel() if blk is not None else max(nrec, 1)
+            out_key, out_cnt = self._u64(nout), self._u64(nout)
         if nrec:
             nat.annotate('bytes' if isb else ('u64/counts' if with_counts else 'u64'), nrec * recw)
             direct = 4 if (not isb and not with_counts and not large and id(col) in self._near_unique) else 0
-            sdp.sdp_part_dedup(ctypes.byref(rf), int(isb), bref, ptr(starts), nfinal,
-                               int(with_counts) | (2 if large else 0) | direct,
-                               ptr(out_key), ptr(out_cnt), ptr(ngroups), ptr(stats), s)
+            mode = int(with_counts) | (2 if large else 0) | direct
+            if blk is not None:
+                sdp.sdp_part_dedup_blocks(ctypes.byref(rf), int(isb), bref, ctypes.byref(blk), nfinal, mode,
+                                          ptr(out_key), ptr(out_cnt), ptr(ngroups), ptr(stats), s)
+            else:
+                sdp.sdp_part_dedup(ctypes.byref(rf), int(isb), bref, ptr(starts), nfinal, mode,
+                                   ptr(out_key), ptr(out_cnt), ptr(ngroups), ptr(stats), s)
         del keepf, rf
-        ctx.update({'starts': starts, 'ngroups': ngroups, 'out_key': out_key, 'out_cnt': out_cnt, 'nfinal': nfinal})
+        ctx.update({'starts': starts, 'ngroups': ngroups, 'out_key': out_key, 'out_cnt': out_cnt, 'nfinal': nfinal,
+                    'blk': blk, 'blk_keep': blk_keep if blk is not None else None})
         del ctx['o1'], ctx['bsn_dev']
         ctx['stats_dev'] = torch.cat([stats, hcnt[:hv['n']]]) if hv else stats
 
@@ -1612,6 +1665,24 @@ class Engine:
         for ctx in ctxs:
             del ctx['o1'], ctx['bsn_dev']
         del shared
+        nfinal = nb1 * nb2
+        nf = nfinal * len(ctxs)
+        if self._l2b_ok(False, b2):
+            # level 2 of every column's level-1 buckets into blocks: one
+            # workgroup per (column, bucket), no count pass
+            bst = np.concatenate([bs[:-1] for bs in bsns] + [[total]]).astype(np.int64)
+            nat.annotate('u64/l2blocks', 2 * total * 8)
+            rf, keepf, blk, blk_keep = self._l2_blocks(r1, False, b1, b2, np.diff(bst), bstart=self._h2d(bst))
+            del keep1, r1
+            ngroups = torch.empty(nf, dtype=torch.int32, device=self.device)
+            stats = self._u64(68, zero=True)
+            nat.annotate('u64', total * 8)
+            direct = 4 if id(ctxs[0]['col']) in self._near_unique else 0
+            sdp.sdp_part_dedup_blocks(ctypes.byref(rf), 0, None, ctypes.byref(blk), nf, direct, None, None,
+                                      ptr(ngroups), ptr(stats), s)
+            del keepf, rf, blk_keep
+            self._fused_stats(ctxs, ngroups, stats, nfinal)
+            return
         base = np.array([bs[0] for bs in bsns] + [total], dtype=np.int64)
         bsns = [bs - bs[0] for bs in bsns]                      # column-local bucket starts
         # every column's level-2 chunk table at once ([column, L1 bucket] arrays):
@@ -1649,14 +1720,18 @@ class Engine:
         sdp.sdp_part_recs(ctypes.byref(r1), 0, ptr(chunks), len(ch), b1, b2, 1, None, ptr(o2), ctypes.byref(rf), s)
         del keep1, r1, h2
         starts = o2[self._h2d(np.append(sidx, hb))].contiguous()
-        nfinal = nb1 * nb2
-        nf = nfinal * len(ctxs)
         ngroups = torch.empty(nf, dtype=torch.int32, device=self.device)
         stats = self._u64(68, zero=True)
         nat.annotate('u64', total * 8)
         direct = 4 if id(ctxs[0]['col']) in self._near_unique else 0
         sdp.sdp_part_dedup(ctypes.byref(rf), 0, None, ptr(starts), nf, direct, None, None, ptr(ngroups), ptr(stats), s)
         del keepf, rf
+        self._fused_stats(ctxs, ngroups, stats, nfinal)
+
+    @staticmethod
+    def _fused_stats(ctxs, ngroups, stats, nfinal):
+        """Every fused column's statistics vector from the shared dedup's
+        per-bucket group counts and flags."""
         per_col = ngroups.view(len(ctxs), nfinal).to(torch.int64).sum(1)
         for ci, ctx in enumerate(ctxs):
             st = ctx['stats']
@@ -1685,8 +1760,12 @@ class Engine:
             counts = self._u64(max(total, 1))
             if groups_local:
                 offs = self._scan(ngroups)
-                sdp.sdp_part_compact(ptr(ctx['out_key']), ptr(ctx['out_cnt']), ptr(starts), ptr(ngroups), ptr(offs),
-                                     nfinal, ptr(keys), ptr(counts), s)
+                if ctx.get('blk') is not None:
+                    sdp.sdp_part_compact_blocks(ptr(ctx['out_key']), ptr(ctx['out_cnt']), ctypes.byref(ctx['blk']),
+                                                ptr(ngroups), ptr(offs), nfinal, ptr(keys), ptr(counts), s)
+                else:
+                    sdp.sdp_part_compact(ptr(ctx['out_key']), ptr(ctx['out_cnt']), ptr(starts), ptr(ngroups),
+                                         ptr(offs), nfinal, ptr(keys), ptr(counts), s)
             extra_k, extra_c = [], []
             if hv:
                 hh = hv['h_host']
@@ -1865,6 +1944,24 @@ class Engine:
             part_base = np.concatenate([[0], np.cumsum(part_tot)[:-1]]).astype(np.int64)
             st0 = part_base[:, None] + np.concatenate([np.zeros((world, 1), np.int64),
                                                       np.cumsum(S, axis=1)[:, :-1]], axis=1)
+            rin = nat.SdpRecords(recv.data_ptr(), None, None)
+            if self._l2b_ok(False, b2):
+                # level 2 into blocks: bucket bi = one segment per source rank
+                ch = np.zeros((nmy * world, 4), dtype=np.int64)
+                ch[:, 0] = st0.T.reshape(-1)
+                ch[:, 1] = ch[:, 0] + S.T.reshape(-1)
+                coff = np.arange(nmy + 1, dtype=np.int64) * world
+                tab = self._h2d(np.concatenate([ch.reshape(-1), coff]))
+                nat.annotate('u64/l2blocks', 2 * nrecv * 8)
+                rf, keepf, blk, blk_keep = self._l2_blocks(rin, False, B1, b2, S.sum(axis=0), chunks=tab,
+                                                           coff=tab[ch.size:])
+                ngroups = torch.zeros(nmy * nb2, dtype=torch.int32, device=self.device)
+                nat.annotate('u64', nrecv * 8)
+                sdp.sdp_part_dedup_blocks(ctypes.byref(rf), 0, None, ctypes.byref(blk), nmy * nb2,
+                                          4 if id(col) in self._near_unique else 0, None, None, ptr(ngroups),
+                                          ptr(stats), s)
+                del keepf, rf, blk_keep
+                return
             cnt = -(-S // PART_CHUNK)                                   # chunks per (source, bucket)
             cb, csrc = cnt.T.reshape(-1), np.tile(np.arange(world), nmy)
             bi_of = np.repeat(np.arange(nmy), world)
@@ -1882,7 +1979,6 @@ class Engine:
             ch[:, 2] = nb2 * k0[rep_b] + j
             ch[:, 3] = nch[rep_b]
             chunks = self._h2d(ch)
-            rin = nat.SdpRecords(recv.data_ptr(), None, None)
             h2 = torch.empty(nb2 * K, dtype=torch.int32, device=self.device)
             nat.annotate('u64/count', nrecv * 8)
             sdp.sdp_part_recs(ctypes.byref(rin), 0, ptr(chunks), K, B1, b2, 0, ptr(h2), None, None, s)

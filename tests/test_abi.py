@@ -54,7 +54,7 @@ STRUCTS = {'sdp_column': 'SdpColumn', 'sdp_bytes_column': 'SdpBytesColumn', 'sdp
            'sdp_pass1_task': 'SdpPass1Task', 'sdp_pass2_task': 'SdpPass2Task',
            'sdp_rows_task': 'SdpRowsTask', 'sdp_minmax_result': 'SdpMinmaxResult',
            'sdp_distinct_result': 'SdpDistinctResult', 'sdp_topk_entry': 'SdpTopkEntry',
-           'sdp_topk_result': 'SdpTopkResult'}
+           'sdp_topk_result': 'SdpTopkResult', 'sdp_blocks': 'SdpBlocks'}
 
 
 def test_struct_layouts_match_c():
@@ -164,7 +164,8 @@ def test_policy_constants_come_from_the_header():
     for c, v in (('SDP_HEAVY_MAX', _native.HEAVY_MAX), ('SDP_HEAVY_MAX_REC', _native.HEAVY_MAX_REC),
                  ('SDP_HEAVY_MIN', _native.HEAVY_MIN), ('SDP_PART_SAMPLE', _native.PART_SAMPLE),
                  ('SDP_PART_SAMPLE_BYTES', _native.PART_SAMPLE_BYTES), ('SDP_PART_CHUNK', _native.PART_CHUNK),
-                 ('SDP_GSORT_MAX', _native.GSORT_MAX), ('SDP_ABI_VERSION', _native.ABI_VERSION)):
+                 ('SDP_GSORT_MAX', _native.GSORT_MAX), ('SDP_ABI_VERSION', _native.ABI_VERSION),
+                 ('SDP_L2_BLOCK', _native.L2_BLOCK)):
         m = re.search(r'#define %s\s+(\d+)' % c, text)
         assert m and int(m.group(1)) == v, c
     assert (engine.PART_SAMPLE, engine.PART_SAMPLE_BYTES, engine.HEAVY_MIN, engine.PART_CHUNK, engine.GSORT_MAX) == \
