@@ -610,26 +610,28 @@ int64_t sdp_distinct32_workspace_bytes(int64_t length);
 int sdp_distinct32(const sdp_column *col, int64_t lo, const uint32_t *d_hist1, void *d_work, int64_t work_bytes,
                    uint64_t *d_out, void *stream);
 /* ---- level 2 without a count pass (round 6) --------------------------------
- * One workgroup per level-1 bucket i (d_order[k]: the bucket the k-th
- * workgroup takes, largest first) splits its records by hash bits
- * [64-b1-b2, 64-b1) into blocks of SDP_L2_BLOCK records handed out in LDS from
- * the bucket's block region [d_rbase[i], d_rbase[i+1]) (at least
- * ceil(S_i / SDP_L2_BLOCK) + 2^b2 blocks): no count pass and no offsets.
- * Bucket i = records [d_bstart[i], d_bstart[i+1]) of `in`, or (d_chunks
- * non-NULL) the chunks d_chunks[d_coff[i] .. d_coff[i+1]) (start / end used).
- * Output: block b holds out[b * SDP_L2_BLOCK ..); final bucket f = i * 2^b2 + j
- * has d_fcnt[f] records, record r at block d_list[d_floff[f] + r / SDP_L2_BLOCK],
- * slot r % SDP_L2_BLOCK.  d_bmeta: scratch, one u64 per block.  2^b2 <= 1024
- * (fixed keys) / 512 (byte keys). */
+ * One workgroup owns a whole level-1 bucket and splits its records by hash
+ * bits [64-b1-b2, 64-b1) into blocks of SDP_L2_BLOCK records that it hands
+ * out in LDS from the bucket's block region: no count pass and no offsets.
+ * Workgroup g (nwg of them) walks the segments d_segs[d_soff[g] ..
+ * d_soff[g+1]): segment = records [start, end) of `in` belonging to bucket
+ * hbase; hstride = the bucket's first block (bits 0-31; a multiple of 8, the
+ * region holding at least ceil(S / SDP_L2_BLOCK) + 2^b2 blocks for the
+ * bucket's S records) | bit 32: first segment of the bucket | bit 33: its
+ * last.  A bucket's segments are consecutive in one workgroup's list.
+ * Output: block b holds out[b * SDP_L2_BLOCK ..); final bucket
+ * f = bucket * 2^b2 + j has d_fcnt[f] records, record r at block
+ * d_list[d_floff[f] + r / SDP_L2_BLOCK], slot r % SDP_L2_BLOCK (d_list needs 32
+ * entries of padding past the last block).  d_bmeta: scratch, one u64 per
+ * block.  2^b2 <= 1024 (fixed keys) / 512 (byte keys). */
 typedef struct sdp_blocks {
     uint32_t *d_fcnt;       /* records per final bucket              */
     uint32_t *d_floff;      /* first d_list entry per final bucket   */
     uint32_t *d_list;       /* block ids, in order within each bucket */
 } sdp_blocks;
-int sdp_part_l2_blocks(const sdp_records *in, int32_t is_bytes, const uint64_t *d_bstart,
-                       const sdp_chunk *d_chunks, const int64_t *d_coff, const uint32_t *d_rbase,
-                       const uint32_t *d_order, int64_t nbuckets, int32_t b1, int32_t b2,
-                       const sdp_records *out, uint64_t *d_bmeta, const sdp_blocks *blk, void *stream);
+int sdp_part_l2_blocks(const sdp_records *in, int32_t is_bytes, const sdp_chunk *d_segs, const int64_t *d_soff,
+                       int32_t nwg, int32_t b1, int32_t b2, const sdp_records *out, uint64_t *d_bmeta,
+                       const sdp_blocks *blk, void *stream);
 /* sdp_part_dedup over the final buckets of sdp_part_l2_blocks (the same modes
  * and outputs; groups of f go to the block positions of its records 0 ..
  * d_ngroups[f]). */

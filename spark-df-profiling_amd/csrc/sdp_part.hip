@@ -1220,20 +1220,22 @@ __device__ __forceinline__ uint32_t l2b_block(const L2BLds<NA, L, NBM> &s, int j
     return (k == c / L2B && (c % L2B) != 0) ? s.cb[j] : (uint32_t)(s.nbase[j] + (int32_t)k);
 }
 
-// i: bucket index; in_*: records; bucket i = records [bstart[i], bstart[i+1])
-// (chunks == nullptr) or the chunks chunks[coff[i] .. coff[i+1]) (start/end
-// used; the sharded owner's buckets arrive in one segment per source rank);
-// rbase[i]: the bucket's first block (rbase[i+1] - rbase[i] >= ceil(S_i / L2B)
-// + nb2); order[blockIdx.x]: the bucket this workgroup takes (largest first).
-// bmeta: scratch, one u64 per block (sub-bucket << 32 | block index in it).
+// Workgroup g walks the segments segs[soff[g] .. soff[g+1]) (host-built, so
+// the buckets are dealt to workgroups by size): segment = records [start, end)
+// of bucket `bucket`, info = first block of the bucket's region | bit 32: the
+// bucket's first segment | bit 33: its last.  A bucket's segments are
+// consecutive (one per bucket on a single rank, one per source rank on a
+// sharded owner).  The next segment's first tile is loaded while the last
+// tile of the current one is placed, across buckets too, so a bucket change
+// costs no exposed memory latency.  bmeta: scratch, one u64 per block (sub-bucket
+// << 32 | block index in it); regions start at multiples of 8 blocks (no
+// 64-byte line of bmeta is shared by two buckets' regions).
 template <bool BYTES>
 __global__ void __launch_bounds__(ST) part_l2_blocks_kernel(const uint64_t *in_k0, const uint64_t *in_k1,
-                                                            const uint64_t *in_meta, const uint64_t *bstart,
-                                                            const Chunk *chunks, const int64_t *coff,
-                                                            const uint32_t *rbase, const uint32_t *order, int b1,
-                                                            int b2, uint64_t *out_k0, uint64_t *out_k1,
-                                                            uint64_t *out_meta, uint64_t *bmeta, uint32_t *blist,
-                                                            uint32_t *fcnt, uint32_t *floff) {
+                                                            const uint64_t *in_meta, const Chunk *segs,
+                                                            const int64_t *soff, int b1, int b2, uint64_t *out_k0,
+                                                            uint64_t *out_k1, uint64_t *out_meta, uint64_t *bmeta,
+                                                            uint32_t *blist, uint32_t *fcnt, uint32_t *floff) {
     using C = L2BCfg<BYTES>;
     constexpr int NA = C::NA, L = C::L, RPT = C::RPT;
     constexpr int TILE = ST * RPT;
@@ -1242,15 +1244,11 @@ __global__ void __launch_bounds__(ST) part_l2_blocks_kernel(const uint64_t *in_k
     const int nb = 1 << b2;
     const int shift = 64 - b1 - b2;
     const uint64_t mask = (uint64_t)(nb - 1);
-    const uint32_t bi = order[blockIdx.x];
-    const uint32_t RB = rbase[bi];
+    const int64_t s0 = soff[blockIdx.x], s1 = soff[blockIdx.x + 1];
+    if (s0 >= s1) return;                       // (workgroup-uniform)
     uint64_t *out[NA];
     out[0] = out_k0;
     if constexpr (BYTES) { out[1] = out_k1; out[2] = out_meta; }
-    for (int j = t; j < nb; j += ST) { s.cur[j] = 0; s.cnt[j] = 0; }
-    if (t == 0) { s.nlist = 0; s.next = 0; }
-    lds_barrier();
-    const int64_t c0 = chunks ? coff[bi] : 0, c1 = chunks ? coff[bi + 1] : 1;
     auto load_tile = [&](int64_t base, int64_t end, uint64_t (&a)[NA][RPT]) {
 #pragma unroll
         for (int q = 0; q < RPT; ++q) {
@@ -1261,11 +1259,27 @@ __global__ void __launch_bounds__(ST) part_l2_blocks_kernel(const uint64_t *in_k
             }
         }
     };
-    for (int64_t c = c0; c < c1; ++c) {
-        const int64_t lo = chunks ? chunks[c].start : (int64_t)bstart[bi];
-        const int64_t hi = chunks ? chunks[c].end : (int64_t)bstart[bi + 1];
-        uint64_t k[NA][RPT];
-        if (lo < hi) load_tile(lo, hi, k);
+    auto uniform_seg = [](const Chunk &x) {
+        auto u = [](int64_t v) {
+            const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v);
+            const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)((uint64_t)v >> 32));
+            return (int64_t)(((uint64_t)hi << 32) | lo);
+        };
+        return Chunk{u(x.start), u(x.end), u(x.hbase), u(x.hstride)};
+    };
+    uint64_t k[NA][RPT];
+    Chunk sg = uniform_seg(segs[s0]);
+    load_tile(sg.start, sg.end, k);
+    uint32_t RB = 0;
+    for (int64_t si = s0; si < s1; ++si) {
+        const Chunk sn = si + 1 < s1 ? uniform_seg(segs[si + 1]) : Chunk{0, 0, 0, 0};
+        if ((sg.hstride >> 32) & 1) {                          // a bucket's first segment
+            RB = (uint32_t)sg.hstride;
+            for (int j = t; j < nb; j += ST) { s.cur[j] = 0; s.cnt[j] = 0; }
+            if (t == 0) { s.nlist = 0; s.next = 0; }
+            lds_barrier();
+        }
+        const int64_t lo = sg.start, hi = sg.end;
         for (int64_t base = lo; base < hi; base += TILE) {
             uint64_t x[NA][RPT];
             uint32_t have = 0;
@@ -1282,7 +1296,9 @@ __global__ void __launch_bounds__(ST) part_l2_blocks_kernel(const uint64_t *in_k
                     bkp[q / 2] |= (uint32_t)((h >> shift) & mask) << (16 * (q & 1));
                 }
             }
-            if (base + TILE < hi) load_tile(base + TILE, hi, k);     // next tile in flight
+            // the next tile: of this segment, or the next segment's first
+            const bool last = base + TILE >= hi;                // wave-uniform
+            load_tile(last ? sn.start : base + TILE, last ? sn.end : hi, k);
             auto bk = [&](int q) { return (int)((bkp[q / 2] >> (16 * (q & 1))) & 0xFFFFu); };
             // ranks within this tile's records of each sub-bucket
             uint32_t r[(RPT + 1) / 2] = {};
@@ -1356,35 +1372,40 @@ __global__ void __launch_bounds__(ST) part_l2_blocks_kernel(const uint64_t *in_k
             if (t == 0) s.nlist = 0;
             lds_barrier();
         }
-    }
-    // partial lines (positions < cur, so their block is cb)
-    for (int j = t; j < nb; j += ST) {
-        const uint32_t cc = s.cur[j];
-        if (cc % L) {
-            const uint64_t o = ((uint64_t)RB + s.cb[j]) * L2B + ((cc / L) * L) % L2B;
-            for (uint32_t l = 0; l < cc % L; ++l)
+        if (lo >= hi) load_tile(sn.start, sn.end, k);        // (an empty segment prefetched nothing)
+        if ((sg.hstride >> 33) & 1) {                          // the bucket's last segment: finish it
+            const uint32_t bi = (uint32_t)sg.hbase;
+            // partial lines (positions < cur, so their block is cb)
+            for (int j = t; j < nb; j += ST) {
+                const uint32_t cc = s.cur[j];
+                if (cc % L) {
+                    const uint64_t o = ((uint64_t)RB + s.cb[j]) * L2B + ((cc / L) * L) % L2B;
+                    for (uint32_t l = 0; l < cc % L; ++l)
 #pragma unroll
-                for (int a = 0; a < NA; ++a) out[a][o + l] = s.line[a][j][l];
+                        for (int a = 0; a < NA; ++a) out[a][o + l] = s.line[a][j][l];
+                }
+                s.cnt[j] = (cc + L2B - 1) / L2B;                 // blocks of j
+            }
+            lds_barrier();
+            block_excl_scan<ST>(s.cnt, (uint32_t *)s.nbase, nb, s.wsum);
+            const uint64_t f0 = (uint64_t)bi << b2;
+            for (int j = t; j < nb; j += ST) {
+                fcnt[f0 + j] = s.cur[j];
+                floff[f0 + j] = RB + (uint32_t)s.nbase[j];
+            }
+            // the block lists, in block order within each sub-bucket: bmeta was
+            // written by the waves of this workgroup (their stores complete
+            // before the barrier) and no line of this region was read before,
+            // so the loads miss the L1 and read L2
+            __syncthreads();
+            const uint32_t nblk = s.next;
+            for (uint32_t u = t; u < nblk; u += ST) {
+                const uint64_t m = bmeta[(uint64_t)RB + u];
+                blist[RB + (uint32_t)s.nbase[(int)(m >> 32)] + (uint32_t)m] = RB + u;
+            }
+            lds_barrier();                                     // (LDS reused by the next bucket)
         }
-        s.cnt[j] = (cc + L2B - 1) / L2B;                 // blocks of j
-    }
-    lds_barrier();
-    block_excl_scan<ST>(s.cnt, (uint32_t *)s.nbase, nb, s.wsum);
-    const uint64_t f0 = (uint64_t)bi << b2;
-    for (int j = t; j < nb; j += ST) {
-        fcnt[f0 + j] = s.cur[j];
-        floff[f0 + j] = RB + (uint32_t)s.nbase[j];
-    }
-    // the block lists, in block order within each sub-bucket (bmeta was written
-    // by other waves of this workgroup: their stores complete before the
-    // barrier, and device-scope loads read them from L2, not a stale L1 line)
-    __threadfence();
-    __syncthreads();
-    const uint32_t nblk = s.next;
-    for (uint32_t u = t; u < nblk; u += ST) {
-        const uint64_t m = __hip_atomic_load(&bmeta[(uint64_t)RB + u], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        const int j = (int)(m >> 32);
-        blist[RB + (uint32_t)s.nbase[j] + (uint32_t)m] = RB + u;
+        sg = sn;
     }
 }
 
@@ -2768,30 +2789,27 @@ int sdp_part_dedup_blocks(const sdp_records *in, int32_t is_bytes, const sdp_byt
                               with_counts, d_out_key, d_out_cnt, d_ngroups, d_stats, stream);
 }
 
-int sdp_part_l2_blocks(const sdp_records *in, int32_t is_bytes, const uint64_t *d_bstart, const sdp_chunk *d_chunks,
-                       const int64_t *d_coff, const uint32_t *d_rbase, const uint32_t *d_order, int64_t nbuckets,
-                       int32_t b1, int32_t b2, const sdp_records *out, uint64_t *d_bmeta, const sdp_blocks *blk,
-                       void *stream) {
-    if (in == nullptr || out == nullptr || d_rbase == nullptr || d_order == nullptr || d_bmeta == nullptr ||
+int sdp_part_l2_blocks(const sdp_records *in, int32_t is_bytes, const sdp_chunk *d_segs, const int64_t *d_soff,
+                       int32_t nwg, int32_t b1, int32_t b2, const sdp_records *out, uint64_t *d_bmeta,
+                       const sdp_blocks *blk, void *stream) {
+    if (in == nullptr || out == nullptr || d_segs == nullptr || d_soff == nullptr || d_bmeta == nullptr ||
         blk == nullptr || blk->d_fcnt == nullptr || blk->d_floff == nullptr || blk->d_list == nullptr ||
-        nbuckets < 1 || nbuckets > INT32_MAX || b1 < 0 || b2 < 1 || b1 + b2 > 63)
+        nwg < 1 || nwg > 65535 || b1 < 0 || b2 < 1 || b1 + b2 > 63)
         return set_error(SDP_EINVAL, "part_l2_blocks: args");
-    if ((d_chunks == nullptr) == (d_bstart == nullptr) || (d_chunks != nullptr && d_coff == nullptr))
-        return set_error(SDP_EINVAL, "part_l2_blocks: exactly one of bstart / chunks");
     if ((1 << b2) > (is_bytes ? L2BCfg<true>::NBM : L2BCfg<false>::NBM))
         return set_error(SDP_EINVAL, "part_l2_blocks: %d sub-buckets", 1 << b2);
     if (is_bytes && (in->d_k1 == nullptr || in->d_meta == nullptr || out->d_k1 == nullptr || out->d_meta == nullptr))
         return set_error(SDP_EINVAL, "part_l2_blocks: byte records need k1/meta");
     hipStream_t s = (hipStream_t)stream;
-    const Chunk *ch = (const Chunk *)d_chunks;
+    const Chunk *sg = (const Chunk *)d_segs;
     if (is_bytes)
-        hipLaunchKernelGGL(part_l2_blocks_kernel<true>, dim3((uint32_t)nbuckets), dim3(ST), 0, s, in->d_k0, in->d_k1,
-                           in->d_meta, d_bstart, ch, d_coff, d_rbase, d_order, b1, b2, out->d_k0, out->d_k1,
-                           out->d_meta, d_bmeta, blk->d_list, blk->d_fcnt, blk->d_floff);
+        hipLaunchKernelGGL(part_l2_blocks_kernel<true>, dim3(nwg), dim3(ST), 0, s, in->d_k0, in->d_k1, in->d_meta,
+                           sg, d_soff, b1, b2, out->d_k0, out->d_k1, out->d_meta, d_bmeta, blk->d_list, blk->d_fcnt,
+                           blk->d_floff);
     else
-        hipLaunchKernelGGL(part_l2_blocks_kernel<false>, dim3((uint32_t)nbuckets), dim3(ST), 0, s, in->d_k0, nullptr,
-                           nullptr, d_bstart, ch, d_coff, d_rbase, d_order, b1, b2, out->d_k0, nullptr, nullptr,
-                           d_bmeta, blk->d_list, blk->d_fcnt, blk->d_floff);
+        hipLaunchKernelGGL(part_l2_blocks_kernel<false>, dim3(nwg), dim3(ST), 0, s, in->d_k0, nullptr, nullptr, sg,
+                           d_soff, b1, b2, out->d_k0, nullptr, nullptr, d_bmeta, blk->d_list, blk->d_fcnt,
+                           blk->d_floff);
     return check_launch("part_l2_blocks_kernel");
 }
 

@@ -272,8 +272,8 @@ _SIGNATURES = {
     'sdp_part_rows_records': (ctypes.c_int, [_BCOL, _HVY, _I32, _P, _P, _REC, _P, _P, _P]),
     'sdp_part_dedup': (ctypes.c_int, [_REC, _I32, _BCOL, _P, _I64, _I32, _P, _P, _P, _P, _P]),
     'sdp_part_compact': (ctypes.c_int, [_P, _P, _P, _P, _P, _I64, _P, _P, _P]),
-    'sdp_part_l2_blocks': (ctypes.c_int, [_REC, _I32, _P, _P, _P, _P, _P, _I64, _I32, _I32, _REC, _P,
-                                          ctypes.POINTER(SdpBlocks), _P]),
+    'sdp_part_l2_blocks': (ctypes.c_int, [_REC, _I32, _P, _P, _I32, _I32, _I32, _REC, _P, ctypes.POINTER(SdpBlocks),
+                                          _P]),
     'sdp_part_dedup_blocks': (ctypes.c_int, [_REC, _I32, _BCOL, ctypes.POINTER(SdpBlocks), _I64, _I32, _P, _P, _P,
                                              _P, _P]),
     'sdp_part_compact_blocks': (ctypes.c_int, [_P, _P, ctypes.POINTER(SdpBlocks), _P, _P, _I64, _P, _P, _P]),

@@ -1194,33 +1194,56 @@ class Engine:
         keys, <= 512 of byte keys: the LDS lines of one workgroup)."""
         return L2_BLOCKS and 1 <= b2 and (1 << b2) <= (512 if isb else 1024)
 
-    def _l2_blocks(self, r1, isb, b1, b2, sizes, bstart=None, chunks=None, coff=None):
-        """Level 2 of len(sizes) level-1 buckets (records per bucket `sizes`,
-        host array) into blocks (sdp_part_l2_blocks): bucket i is records
-        [bstart[i], bstart[i+1]) of r1 (device u64), or the chunks
-        chunks[coff[i] .. coff[i+1]).  No count pass, no scan: one workgroup per
-        bucket, largest first.  Returns (records, their tensors, SdpBlocks, the
-        block tensors)."""
-        nbk = len(sizes)
+    L2B_WG = 256                       # persistent workgroups of sdp_part_l2_blocks (one per CU)
+
+    def _l2_blocks(self, r1, isb, b1, b2, seg_lo, seg_hi, seg_bucket, nbk):
+        """Level 2 of nbk level-1 buckets into blocks (sdp_part_l2_blocks): the
+        records of bucket i are the segments [seg_lo, seg_hi) of r1 whose
+        seg_bucket is i (host arrays, a bucket's segments consecutive).  No
+        count pass, no scan: one workgroup per bucket at a time, buckets dealt
+        to the workgroups by size (largest first, snake order).  Returns
+        (records, their tensors, SdpBlocks, the block tensors)."""
+        seg_lo = np.asarray(seg_lo, dtype=np.int64)
+        seg_hi = np.asarray(seg_hi, dtype=np.int64)
+        seg_bucket = np.asarray(seg_bucket, dtype=np.int64)
         nb2 = 1 << b2
-        nblk = -(-np.asarray(sizes, dtype=np.int64) // L2_BLOCK) + nb2
+        sizes = np.bincount(seg_bucket, weights=seg_hi - seg_lo, minlength=nbk).astype(np.int64)
+        nblk = (-(-sizes // L2_BLOCK) + nb2 + 7) // 8 * 8        # regions on 64-byte lines of bmeta
         rbase = np.zeros(nbk + 1, dtype=np.int64)
         rbase[1:] = np.cumsum(nblk)
         total = int(rbase[-1])
         if total >= (1 << 32):
             raise nat.NativeError('l2_blocks: %d blocks' % total)
-        order = np.argsort(-np.asarray(sizes), kind='stable')
-        ro = self._h2d(np.concatenate([rbase, order]).astype(np.uint32).view(np.int32))
+        G = min(self.L2B_WG, nbk)
+        rank = np.empty(nbk, dtype=np.int64)
+        rank[np.argsort(-sizes, kind='stable')] = np.arange(nbk)
+        rnd, pos = rank // G, rank % G
+        wg = np.where(rnd % 2 == 0, pos, G - 1 - pos)             # snake: round-robin, reversed every round
+        # segments in (workgroup, bucket rank, segment) order
+        nseg = len(seg_lo)
+        order = np.lexsort((np.arange(nseg), rank[seg_bucket], wg[seg_bucket]))
+        sb = seg_bucket[order]
+        first = np.ones(nseg, dtype=bool)
+        first[1:] = sb[1:] != sb[:-1]
+        last = np.ones(nseg, dtype=bool)
+        last[:-1] = sb[1:] != sb[:-1]
+        tab = np.empty((nseg, 4), dtype=np.int64)
+        tab[:, 0] = seg_lo[order]
+        tab[:, 1] = seg_hi[order]
+        tab[:, 2] = sb
+        tab[:, 3] = rbase[sb] | (first.astype(np.int64) << 32) | (last.astype(np.int64) << 33)
+        soff = np.zeros(G + 1, dtype=np.int64)
+        soff[1:] = np.cumsum(np.bincount(wg[sb], minlength=G))
+        dt = self._h2d(np.concatenate([tab.reshape(-1), soff]))
         rf, keepf = self._records(total * L2_BLOCK, isb)
         bmeta = self._u64(total)
         # (the dedup kernels read a batch's list entries in one load: padding)
         lst = torch.empty(total + 32, dtype=torch.int32, device=self.device)
         fc = torch.empty(2 * nbk * nb2, dtype=torch.int32, device=self.device)
         blk = nat.SdpBlocks(fc.data_ptr(), fc.data_ptr() + 4 * nbk * nb2, lst.data_ptr())
-        sdp.sdp_part_l2_blocks(ctypes.byref(r1), int(isb), ptr(bstart), ptr(chunks), ptr(coff), ptr(ro),
-                               ctypes.c_void_p(ro.data_ptr() + 4 * (nbk + 1)), nbk, b1, b2, ctypes.byref(rf),
-                               ptr(bmeta), ctypes.byref(blk), self._s())
-        del bmeta, ro
+        sdp.sdp_part_l2_blocks(ctypes.byref(r1), int(isb), ptr(dt), ctypes.c_void_p(dt.data_ptr() + 8 * tab.size), G,
+                               b1, b2, ctypes.byref(rf), ptr(bmeta), ctypes.byref(blk), self._s())
+        del bmeta, dt
         return rf, keepf, blk, (fc, lst)
 
     def _heavy_keys(self, col, isb, gather=False):
@@ -1527,8 +1550,7 @@ class Engine:
             rf, keepf = r1, keep1
         elif self._l2b_ok(isb, b2):
             nat.annotate(('bytes' if isb else 'u64') + '/l2blocks', 2 * nrec * recw)
-            rf, keepf, blk, blk_keep = self._l2_blocks(r1, isb, b1, b2, np.diff(bsn),
-                                                       bstart=torch.cat([bstarts, o1[-1:]]))
+            rf, keepf, blk, blk_keep = self._l2_blocks(r1, isb, b1, b2, bsn[:-1], bsn[1:], np.arange(nb1), nb1)
             del keep1, r1
             starts = None
         else:
@@ -1672,7 +1694,8 @@ class Engine:
             # workgroup per (column, bucket), no count pass
             bst = np.concatenate([bs[:-1] for bs in bsns] + [[total]]).astype(np.int64)
             nat.annotate('u64/l2blocks', 2 * total * 8)
-            rf, keepf, blk, blk_keep = self._l2_blocks(r1, False, b1, b2, np.diff(bst), bstart=self._h2d(bst))
+            rf, keepf, blk, blk_keep = self._l2_blocks(r1, False, b1, b2, bst[:-1], bst[1:], np.arange(len(bst) - 1),
+                                                       len(bst) - 1)
             del keep1, r1
             ngroups = torch.empty(nf, dtype=torch.int32, device=self.device)
             stats = self._u64(68, zero=True)
@@ -1947,14 +1970,10 @@ class Engine:
             rin = nat.SdpRecords(recv.data_ptr(), None, None)
             if self._l2b_ok(False, b2):
                 # level 2 into blocks: bucket bi = one segment per source rank
-                ch = np.zeros((nmy * world, 4), dtype=np.int64)
-                ch[:, 0] = st0.T.reshape(-1)
-                ch[:, 1] = ch[:, 0] + S.T.reshape(-1)
-                coff = np.arange(nmy + 1, dtype=np.int64) * world
-                tab = self._h2d(np.concatenate([ch.reshape(-1), coff]))
+                lo_s = st0.T.reshape(-1)
                 nat.annotate('u64/l2blocks', 2 * nrecv * 8)
-                rf, keepf, blk, blk_keep = self._l2_blocks(rin, False, B1, b2, S.sum(axis=0), chunks=tab,
-                                                           coff=tab[ch.size:])
+                rf, keepf, blk, blk_keep = self._l2_blocks(rin, False, B1, b2, lo_s, lo_s + S.T.reshape(-1),
+                                                           np.repeat(np.arange(nmy), world), nmy)
                 ngroups = torch.zeros(nmy * nb2, dtype=torch.int32, device=self.device)
                 nat.annotate('u64', nrecv * 8)
                 sdp.sdp_part_dedup_blocks(ctypes.byref(rf), 0, None, ctypes.byref(blk), nmy * nb2,
