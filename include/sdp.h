@@ -615,18 +615,22 @@ int sdp_distinct32(const sdp_column *col, int64_t lo, const uint32_t *d_hist1, v
  * out in LDS from the bucket's block region: no count pass and no offsets.
  * Workgroup g (nwg of them) walks the segments d_segs[d_soff[g] ..
  * d_soff[g+1]): segment = records [start, end) of `in` belonging to bucket
- * hbase; hstride = the bucket's first block (bits 0-31; a multiple of 8, the
- * region holding at least ceil(S / SDP_L2_BLOCK) + 2^b2 blocks for the
- * bucket's S records) | bit 32: first segment of the bucket | bit 33: its
- * last.  A bucket's segments are consecutive in one workgroup's list.
+ * hbase; hstride = the region's first block (bits 0-31; a multiple of 8) |
+ * bit 32: first segment of the bucket | bit 33: its last | R (bits 40-63).
+ * A bucket's segments are consecutive in one workgroup's list.
+ * Sub-bucket j of a bucket fills a run of R blocks (hstride bits 40-63) at
+ * region block + j * R, then overflow blocks after the bucket's 2^b2 runs (the
+ * region holds 2^b2 * R + ceil(S / SDP_L2_BLOCK) + 8 blocks for S records).
  * Output: block b holds out[b * SDP_L2_BLOCK ..); final bucket
- * f = bucket * 2^b2 + j has d_fcnt[f] records, record r at block
- * d_list[d_floff[f] + r / SDP_L2_BLOCK], slot r % SDP_L2_BLOCK (d_list needs 32
- * entries of padding past the last block).  d_bmeta: scratch, one u64 per
+ * f = bucket * 2^b2 + j is described by d_desc[f * SDP_L2_DESC_W ..] = {records
+ * n, first overflow-list entry l, run block, run records rl}: record r < rl
+ * lies at run block * SDP_L2_BLOCK + r, record r >= rl at block
+ * d_list[l + (r - rl) / SDP_L2_BLOCK], slot r % SDP_L2_BLOCK.  d_list needs 32
+ * entries of padding past the last block.  d_bmeta: scratch, one u64 per
  * block.  2^b2 <= 1024 (fixed keys) / 512 (byte keys). */
+#define SDP_L2_DESC_W 4
 typedef struct sdp_blocks {
-    uint32_t *d_fcnt;       /* records per final bucket              */
-    uint32_t *d_floff;      /* first d_list entry per final bucket   */
+    uint32_t *d_desc;       /* SDP_L2_DESC_W u32 per final bucket      */
     uint32_t *d_list;       /* block ids, in order within each bucket */
 } sdp_blocks;
 int sdp_part_l2_blocks(const sdp_records *in, int32_t is_bytes, const sdp_chunk *d_segs, const int64_t *d_soff,

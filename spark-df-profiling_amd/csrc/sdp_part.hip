@@ -1177,22 +1177,28 @@ __global__ void __launch_bounds__(ST) part_scatter_recs_wc_kernel(const uint64_t
     if (t < nb) wc_flush_partial(s, t, out);
 }
 
-// ---- level 2 into blocks, no count pass (round 6) -----------------------------------
+// ---- level 2 into runs + blocks, no count pass (round 6) ----------------------------
 // The exact-offset level 2 above needs a count pass over every record first
 // (part_count_recs_*: 7.6 GB read per 1e9-row f64 column) because several
 // workgroups fill one level-1 bucket's sub-buckets.  Here ONE workgroup owns a
 // whole level-1 bucket, so the cursors of its sub-buckets are its own and no
-// prior count is needed: sub-bucket j's records go to blocks of L2B records
-// that the workgroup hands out from the bucket's region in LDS (one LDS atomic
-// per sub-bucket per tile that crosses a block edge); every bucket's current
-// line is assembled in LDS and written whole (as wc_tile).  The region of
-// bucket i holds ceil(S_i / L2B) + nb2 blocks (each sub-bucket leaves at most
-// one block partly filled), so nothing can overflow.  At the end of the bucket
-// the workgroup writes every final bucket f = i * nb2 + j as (records fcnt[f],
-// block list at floff[f]) and fills the list in block order: record r of f
-// lives at list[floff[f] + r / L2B] * L2B + r % L2B.  The de-duplication and
-// compaction kernels read that layout (BLK template parameter).
+// prior count is needed.  Sub-bucket j's records fill a contiguous run of R
+// blocks (L2B records each) at a fixed place of the bucket's region -- R is
+// sized from the bucket's record count S as mean + 4 sigma of a sub-bucket's
+// share, so near-unique keys practically never leave their run -- and the
+// records past the run go to overflow blocks the workgroup hands out in LDS
+// (one LDS atomic per sub-bucket per tile that crosses a block edge).  Every
+// sub-bucket's current line is assembled in LDS and written whole (as wc_tile).
+// The region holds nb2 * R run blocks and ceil(S / L2B) + 8 overflow blocks,
+// so nothing can overflow.  At the end of the bucket the workgroup writes
+// every final bucket f = bucket * nb2 + j as a descriptor {records n, first
+// entry of its overflow list, run block, run records} and fills the overflow
+// lists: record r of f lies in the run
+// (r < run records) or at overflow block list[l + (r - run) / L2B].  The
+// de-duplication and compaction kernels read that layout (BLK template
+// parameter); on the common path it is the contiguous layout of before.
 constexpr int L2B = 64;                          // records per block: one wave-wide load
+constexpr int DESC_W = 4;                        // u32 words per final-bucket descriptor
 template <bool BYTES> struct L2BCfg {
     static constexpr int NA = BYTES ? 3 : 1;
     static constexpr int L = BYTES ? 8 : 16;     // records per line: 64 B (three arrays) / 128 B
@@ -1204,8 +1210,8 @@ struct L2BLds {
     uint64_t line[NA][NBM][L];                   // sub-bucket j's current line
     uint32_t cur[NBM];                           // records of j so far (bucket-local positions)
     uint32_t cnt[NBM];                           // this tile's records of j
-    int32_t nbase[NBM];                          // block k of j allocated in this tile: nbase[j] + k (region-relative)
-    uint32_t cb[NBM];                            // region-relative block holding position cur[j] (cur % L2B != 0)
+    int32_t nbase[NBM];                          // overflow block k of j allocated in this tile: nbase[j] + k
+    uint32_t cb[NBM];                            // overflow block holding position cur[j] (past the run, % L2B != 0)
     uint16_t list[NBM];                          // sub-buckets whose current line this tile completes
     uint32_t nlist, next;
     uint32_t wsum[ST / WAVE];
@@ -1213,29 +1219,38 @@ struct L2BLds {
 static_assert(sizeof(L2BLds<1, 16, MAXB>) <= 160 * 1024, "level-2 block scatter LDS (fixed keys)");
 static_assert(sizeof(L2BLds<3, 8, 512>) <= 160 * 1024, "level-2 block scatter LDS (byte keys)");
 
-// region-relative block of position p of sub-bucket j (p >= cur[j], within this tile's span)
+// The record index of position p of sub-bucket j (p >= cur[j], within this
+// tile's span): in the run (RL records from block RB + j * R) or an overflow
+// block (from block OB).
+struct L2Geo {
+    uint64_t RB, OB;                             // region's first run block, first overflow block
+    uint32_t R, RL;                              // run blocks, run records
+};
 template <int NA, int L, int NBM>
-__device__ __forceinline__ uint32_t l2b_block(const L2BLds<NA, L, NBM> &s, int j, uint32_t p) {
-    const uint32_t c = s.cur[j], k = p / L2B;
-    return (k == c / L2B && (c % L2B) != 0) ? s.cb[j] : (uint32_t)(s.nbase[j] + (int32_t)k);
+__device__ __forceinline__ uint64_t l2b_rec(const L2BLds<NA, L, NBM> &s, const L2Geo &g, int j, uint32_t p) {
+    if (p < g.RL) return (g.RB + (uint64_t)j * g.R) * L2B + p;
+    const uint32_t c = s.cur[j], oc = c > g.RL ? c - g.RL : 0u, o = p - g.RL, k = o / L2B;
+    const uint32_t b = (k == oc / L2B && (oc % L2B) != 0) ? s.cb[j] : (uint32_t)(s.nbase[j] + (int32_t)k);
+    return (g.OB + b) * L2B + o % L2B;
 }
 
 // Workgroup g walks the segments segs[soff[g] .. soff[g+1]) (host-built, so
 // the buckets are dealt to workgroups by size): segment = records [start, end)
-// of bucket `bucket`, info = first block of the bucket's region | bit 32: the
-// bucket's first segment | bit 33: its last.  A bucket's segments are
-// consecutive (one per bucket on a single rank, one per source rank on a
-// sharded owner).  The next segment's first tile is loaded while the last
-// tile of the current one is placed, across buckets too, so a bucket change
-// costs no exposed memory latency.  bmeta: scratch, one u64 per block (sub-bucket
-// << 32 | block index in it); regions start at multiples of 8 blocks (no
-// 64-byte line of bmeta is shared by two buckets' regions).
+// of bucket `hbase`; hstride = the region's first block (bits 0-31) | bit 32:
+// the bucket's first segment | bit 33: its last | run blocks R (bits 40-63).
+// A bucket's segments are consecutive (one per bucket on a single rank, one
+// per source rank on a sharded owner).  The next segment's first tile is
+// loaded while the last tile of the current one is placed, across buckets
+// too, so a bucket change costs no exposed memory latency.  bmeta: scratch,
+// one u64 per block (sub-bucket << 32 | overflow block index in it); regions
+// start at multiples of 8 blocks (no 64-byte line of bmeta is shared by two
+// buckets' regions).
 template <bool BYTES>
 __global__ void __launch_bounds__(ST) part_l2_blocks_kernel(const uint64_t *in_k0, const uint64_t *in_k1,
                                                             const uint64_t *in_meta, const Chunk *segs,
                                                             const int64_t *soff, int b1, int b2, uint64_t *out_k0,
                                                             uint64_t *out_k1, uint64_t *out_meta, uint64_t *bmeta,
-                                                            uint32_t *blist, uint32_t *fcnt, uint32_t *floff) {
+                                                            uint32_t *blist, uint32_t *desc) {
     using C = L2BCfg<BYTES>;
     constexpr int NA = C::NA, L = C::L, RPT = C::RPT;
     constexpr int TILE = ST * RPT;
@@ -1270,11 +1285,14 @@ __global__ void __launch_bounds__(ST) part_l2_blocks_kernel(const uint64_t *in_k
     uint64_t k[NA][RPT];
     Chunk sg = uniform_seg(segs[s0]);
     load_tile(sg.start, sg.end, k);
-    uint32_t RB = 0;
+    L2Geo g{0, 0, 1, L2B};
     for (int64_t si = s0; si < s1; ++si) {
         const Chunk sn = si + 1 < s1 ? uniform_seg(segs[si + 1]) : Chunk{0, 0, 0, 0};
         if ((sg.hstride >> 32) & 1) {                          // a bucket's first segment
-            RB = (uint32_t)sg.hstride;
+            g.RB = (uint32_t)sg.hstride;
+            g.R = (uint32_t)((uint64_t)sg.hstride >> 40);
+            g.RL = g.R * L2B;
+            g.OB = g.RB + (uint64_t)nb * g.R;
             for (int j = t; j < nb; j += ST) { s.cur[j] = 0; s.cnt[j] = 0; }
             if (t == 0) { s.nlist = 0; s.next = 0; }
             lds_barrier();
@@ -1306,20 +1324,21 @@ __global__ void __launch_bounds__(ST) part_l2_blocks_kernel(const uint64_t *in_k
             for (int q = 0; q < RPT; ++q)
                 if ((have >> q) & 1u) r[q / 2] |= atomicAdd(&s.cnt[bk(q)], 1u) << (16 * (q & 1));
             lds_barrier();
-            // owners: blocks this tile starts (consecutive ids), lines it completes
+            // owners: overflow blocks this tile starts (consecutive ids), lines it completes
             for (int j = t; j < nb; j += ST) {
                 const uint32_t cc = s.cur[j], e = cc + s.cnt[j];
-                if (e > cc) {
-                    const uint32_t kf = (cc % L2B) ? cc / L2B + 1 : cc / L2B, kl = (e - 1) / L2B;
+                if (e > g.RL && e > cc) {
+                    const uint32_t oc = cc > g.RL ? cc - g.RL : 0u, oe = e - g.RL;
+                    const uint32_t kf = (oc % L2B) ? oc / L2B + 1 : oc / L2B, kl = (oe - 1) / L2B;
                     if (kl >= kf) {
                         const uint32_t nn = kl - kf + 1;
                         const uint32_t b0 = atomicAdd(&s.next, nn);
                         s.nbase[j] = (int32_t)b0 - (int32_t)kf;
                         for (uint32_t u = 0; u < nn; ++u)
-                            bmeta[(uint64_t)RB + b0 + u] = ((uint64_t)j << 32) | (uint64_t)(kf + u);
+                            bmeta[g.OB + b0 + u] = ((uint64_t)j << 32) | (uint64_t)(kf + u);
                     }
-                    if (e / L != cc / L) s.list[atomicAdd(&s.nlist, 1u)] = (uint16_t)j;
                 }
+                if (e / L != cc / L) s.list[atomicAdd(&s.nlist, 1u)] = (uint16_t)j;
             }
             lds_barrier();
             // records of the current line into LDS, of lines this tile fills
@@ -1336,7 +1355,7 @@ __global__ void __launch_bounds__(ST) part_l2_blocks_kernel(const uint64_t *in_k
 #pragma unroll
                         for (int a = 0; a < NA; ++a) s.line[a][j][p % L] = x[a][q];
                     } else if (p / L != e / L) {
-                        const uint64_t o = ((uint64_t)RB + l2b_block(s, j, p)) * L2B + p % L2B;
+                        const uint64_t o = l2b_rec(s, g, j, p);
 #pragma unroll
                         for (int a = 0; a < NA; ++a) out[a][o] = x[a][q];
                     } else {
@@ -1350,8 +1369,7 @@ __global__ void __launch_bounds__(ST) part_l2_blocks_kernel(const uint64_t *in_k
             const uint32_t nl = s.nlist;
             for (uint32_t i = t / L; i < nl; i += ST / L) {
                 const int j = s.list[i], l = t & (L - 1);
-                const uint32_t p = (s.cur[j] / L) * L + l;
-                const uint64_t o = ((uint64_t)RB + l2b_block(s, j, p)) * L2B + p % L2B;
+                const uint64_t o = l2b_rec(s, g, j, (s.cur[j] / L) * L + l);
 #pragma unroll
                 for (int a = 0; a < NA; ++a) out[a][o] = s.line[a][j][l];
             }
@@ -1365,7 +1383,10 @@ __global__ void __launch_bounds__(ST) part_l2_blocks_kernel(const uint64_t *in_k
                 }
             for (int j = t; j < nb; j += ST) {
                 const uint32_t e = s.cur[j] + s.cnt[j];
-                if (e % L2B) s.cb[j] = l2b_block(s, j, e);
+                if (e > g.RL && ((e - g.RL) % L2B) != 0) {
+                    const uint64_t rec = l2b_rec(s, g, j, e);
+                    s.cb[j] = (uint32_t)(rec / L2B - g.OB);
+                }
                 s.cur[j] = e;
                 s.cnt[j] = 0;
             }
@@ -1375,33 +1396,38 @@ __global__ void __launch_bounds__(ST) part_l2_blocks_kernel(const uint64_t *in_k
         if (lo >= hi) load_tile(sn.start, sn.end, k);        // (an empty segment prefetched nothing)
         if ((sg.hstride >> 33) & 1) {                          // the bucket's last segment: finish it
             const uint32_t bi = (uint32_t)sg.hbase;
-            // partial lines (positions < cur, so their block is cb)
+            // partial lines: positions below cur (in the run, or the block cb)
             for (int j = t; j < nb; j += ST) {
                 const uint32_t cc = s.cur[j];
-                if (cc % L) {
-                    const uint64_t o = ((uint64_t)RB + s.cb[j]) * L2B + ((cc / L) * L) % L2B;
-                    for (uint32_t l = 0; l < cc % L; ++l)
+                for (uint32_t pp = (cc / L) * L; pp < cc; ++pp) {
+                    const uint64_t o = pp < g.RL ? (g.RB + (uint64_t)j * g.R) * L2B + pp
+                                                 : (g.OB + s.cb[j]) * L2B + (pp - g.RL) % L2B;
 #pragma unroll
-                        for (int a = 0; a < NA; ++a) out[a][o + l] = s.line[a][j][l];
+                    for (int a = 0; a < NA; ++a) out[a][o] = s.line[a][j][pp % L];
                 }
-                s.cnt[j] = (cc + L2B - 1) / L2B;                 // blocks of j
+                s.cnt[j] = cc > g.RL ? (cc - g.RL + L2B - 1) / L2B : 0u;       // overflow blocks of j
             }
             lds_barrier();
             block_excl_scan<ST>(s.cnt, (uint32_t *)s.nbase, nb, s.wsum);
             const uint64_t f0 = (uint64_t)bi << b2;
             for (int j = t; j < nb; j += ST) {
-                fcnt[f0 + j] = s.cur[j];
-                floff[f0 + j] = RB + (uint32_t)s.nbase[j];
+                uint32_t *d = desc + (f0 + j) * DESC_W;
+                d[0] = s.cur[j];
+                d[1] = (uint32_t)g.OB + (uint32_t)s.nbase[j];
+                d[2] = (uint32_t)(g.RB + (uint64_t)j * g.R);
+                d[3] = g.RL;
             }
-            // the block lists, in block order within each sub-bucket: bmeta was
-            // written by the waves of this workgroup (their stores complete
+            // the overflow lists, in block order within each sub-bucket: bmeta
+            // was written by the waves of this workgroup (their stores complete
             // before the barrier) and no line of this region was read before,
             // so the loads miss the L1 and read L2
             __syncthreads();
             const uint32_t nblk = s.next;
             for (uint32_t u = t; u < nblk; u += ST) {
-                const uint64_t m = bmeta[(uint64_t)RB + u];
-                blist[RB + (uint32_t)s.nbase[(int)(m >> 32)] + (uint32_t)m] = RB + u;
+                const uint64_t m = bmeta[g.OB + u];
+                const int j = (int)(m >> 32);
+                const uint32_t kk = (uint32_t)m;
+                blist[(uint32_t)g.OB + (uint32_t)s.nbase[j] + kk] = (uint32_t)g.OB + u;
             }
             lds_barrier();                                     // (LDS reused by the next bucket)
         }
@@ -1411,48 +1437,105 @@ __global__ void __launch_bounds__(ST) part_l2_blocks_kernel(const uint64_t *in_k
 
 // ---- final buckets: LDS grouping -------------------------------------------------
 // Records of a final bucket: contiguous [starts[f], starts[f+1]) (BLK false),
-// or fcnt[f] records in the blocks blist[floff[f] ..] of part_l2_blocks_kernel
-// (BLK true).  Bucket-local index i; lo = 0 for blocks.
+// or laid out by part_l2_blocks_kernel (BLK true): descriptor desc[f] =
+// DESC_W u32 words {records n, first overflow-list entry, run block, run
+// records}: record i < run records lies in the run, the others in the
+// overflow blocks of the list.  Bucket-local index i (lo = 0 for
+// blocks).  A kernel loads a bucket's descriptor one bucket ahead, so its
+// records cost one memory latency, as with the contiguous layout.
 struct BlkArg {
-    const uint32_t *fcnt, *floff, *blist;
+    const uint32_t *desc, *blist;
 };
 template <bool BLK>
-struct RecAt {
-    const uint32_t *blist;
-    uint32_t l0;
-    __device__ __forceinline__ int64_t at(int64_t i) const {
-        if constexpr (BLK) return (int64_t)blist[l0 + (uint32_t)(i / L2B)] * L2B + (i % L2B);
-        else return i;
+struct Bkt {
+    int64_t lo = 0, hi = 0;                      // contiguous: [lo, hi)
+    const uint32_t *dsc = nullptr;               // blocks: the descriptor,
+    const uint32_t *blist = nullptr;
+    uint32_t dv = 0;                             //   its word lane % DESC_W
+    // the bucket-local range (waits for the descriptor)
+    __device__ __forceinline__ void range(int64_t &a, int64_t &b) const {
+        if constexpr (BLK) {
+            a = 0;
+            b = (int64_t)__builtin_amdgcn_readlane(dv, 0);
+        } else {
+            a = lo;
+            b = hi;
+        }
     }
-    // records rb + q * WAVE + lane start here (rb a multiple of WAVE,
-    // wave-uniform): the block is wave-uniform, so its list entry is a scalar
-    // load and the pointer a scalar base (the lists carry WV_Q entries of
-    // padding: a batch's last entries may lie past the bucket's blocks)
+    __device__ __forceinline__ uint64_t run0() const {          // the run's first record
+        return (uint64_t)__builtin_amdgcn_readlane(dv, 2) * L2B;
+    }
+    __device__ __forceinline__ uint32_t run_len() const { return __builtin_amdgcn_readlane(dv, 3); }
+    // record i (i / L2B wave-uniform; no branch: the overflow list entry is
+    // read either way, of block 0 for a record in the run)
+    __device__ __forceinline__ int64_t at(int64_t i) const {
+        if constexpr (BLK) {
+            const uint32_t rl = run_len();
+            const bool inrun = (uint64_t)i < rl;
+            const uint32_t ob = __builtin_amdgcn_readfirstlane(inrun ? 0u : (uint32_t)((i - rl) / L2B));
+            const uint32_t b = blist[__builtin_amdgcn_readlane(dv, 1) + ob];
+            return inrun ? (int64_t)(run0() + (uint64_t)i) : (int64_t)b * L2B + (i % L2B);
+        } else {
+            return i;
+        }
+    }
+    // record i, any i per lane
+    __device__ __forceinline__ int64_t at_lane(int64_t i) const {
+        if constexpr (BLK) {
+            const uint32_t rl = dsc[3];
+            if ((uint64_t)i < rl) return (int64_t)((uint64_t)dsc[2] * L2B + (uint64_t)i);
+            return (int64_t)blist[dsc[1] + (uint32_t)((i - rl) / L2B)] * L2B + (i % L2B);
+        } else {
+            return i;
+        }
+    }
+    // the records of a batch of Q wave-wide loads from rb (below hi) lie in
+    // the run (the common case: a bucket within its run)
+    __device__ __forceinline__ bool inline_batch(int64_t rb, int Q, int64_t hi) const {
+        if constexpr (BLK) return min(hi, rb + (int64_t)Q * WAVE) <= (int64_t)run_len();
+        else return true;
+    }
+    // (inline_batch) records rb + q * WAVE + lane start here.  Blocks: the
+    // pointer is made a scalar value, so the load takes it as its scalar base
+    // with the lane offset in one VGPR (left to itself the compiler hoists 16
+    // per-q 64-bit lane offsets out of the bucket loop and spills them)
+    __device__ __forceinline__ const uint64_t *wave_base_inl(const uint64_t *p, int64_t rb, int q) const {
+        if constexpr (BLK) {
+            const uint64_t a = (uint64_t)(p + run0() + rb + (int64_t)q * WAVE);
+            return (const uint64_t *)(((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(a >> 32)) << 32) |
+                                      __builtin_amdgcn_readfirstlane((uint32_t)a));
+        } else {
+            return p + rb + (int64_t)q * WAVE;
+        }
+    }
+    // records rb + q * WAVE + lane start here (rb a multiple of WAVE, wave-uniform)
     __device__ __forceinline__ const uint64_t *wave_base(const uint64_t *p, int64_t rb, int q) const {
         if constexpr (BLK) {
             static_assert(L2B == WAVE, "one block per wave-wide load");
-            const uint32_t li = __builtin_amdgcn_readfirstlane(l0 + (uint32_t)(rb / L2B) + (uint32_t)q);
-            return p + (uint64_t)blist[li] * L2B;
+            const int64_t i = rb + (int64_t)q * WAVE;
+            const uint32_t rl = run_len();
+            const bool inrun = (uint64_t)i < rl;
+            const uint32_t ob = __builtin_amdgcn_readfirstlane(inrun ? 0u : (uint32_t)((i - rl) / L2B));
+            const uint32_t b = blist[__builtin_amdgcn_readlane(dv, 1) + ob];
+            return inrun ? p + run0() + i : p + (uint64_t)b * L2B;
         } else {
             return p + rb + (int64_t)q * WAVE;
         }
     }
 };
-// bucket f's range and record mapping
+// issue the loads of bucket f's range / descriptor
 template <bool BLK>
-__device__ __forceinline__ RecAt<BLK> bucket_of(const uint64_t *starts, const BlkArg &ba, int64_t f, int64_t &lo,
-                                                int64_t &hi) {
-    RecAt<BLK> ra{nullptr, 0};
+__device__ __forceinline__ Bkt<BLK> bucket_load(const uint64_t *starts, const BlkArg &ba, int64_t f) {
+    Bkt<BLK> k;
     if constexpr (BLK) {
-        lo = 0;
-        hi = ba.fcnt[f];
-        ra.blist = ba.blist;
-        ra.l0 = ba.floff[f];
+        k.blist = ba.blist;
+        k.dsc = ba.desc + f * DESC_W;
+        k.dv = k.dsc[threadIdx.x & (DESC_W - 1)];
     } else {
-        lo = starts[f];
-        hi = starts[f + 1];
+        k.lo = starts[f];
+        k.hi = starts[f + 1];
     }
-    return ra;
+    return k;
 }
 
 constexpr int DT = 1024;                // dedup threads per workgroup
@@ -1480,13 +1563,13 @@ __global__ void __launch_bounds__(DTU) part_dedup_u64_kernel(const uint64_t *in_
     // the first batch of the next bucket is loaded while this one is probed
     int64_t f = blockIdx.x;
     int64_t lo = 0, hi = 0;
-    RecAt<BLK> ra{nullptr, 0};
+    Bkt<BLK> ra, ra_n, ra_n2;                  // buckets f, f + G (records prefetched), f + 2G (range only)
     uint64_t hb[DU_BATCH];
     // per-block totals, flushed once (one global atomic per bucket would serialise
     // hundreds of thousands of device-scope atomics on a few addresses)
     uint64_t acc_groups = 0, acc_special = 0;
     bool acc_full = false;
-    auto load_batch = [&](const RecAt<BLK> &rr, int64_t from, int64_t to, uint64_t (&dst)[DU_BATCH]) {
+    auto load_batch = [&](const Bkt<BLK> &rr, int64_t from, int64_t to, uint64_t (&dst)[DU_BATCH]) {
 #pragma unroll
         for (int q = 0; q < DU_BATCH; ++q) {
             const int64_t r = from + (int64_t)q * DTU + t;
@@ -1494,18 +1577,21 @@ __global__ void __launch_bounds__(DTU) part_dedup_u64_kernel(const uint64_t *in_
         }
     };
     if (f < nbuckets) {
-        ra = bucket_of<BLK>(starts, ba, f, lo, hi);
+        ra = bucket_load<BLK>(starts, ba, f);
+        ra.range(lo, hi);
         load_batch(ra, lo, hi, hb);
     }
+    if (f + gridDim.x < nbuckets) ra_n2 = bucket_load<BLK>(starts, ba, f + gridDim.x);
     for (; f < nbuckets; f += gridDim.x) {
         const int64_t fn = f + gridDim.x;
         int64_t lo_n = 0, hi_n = 0;
-        RecAt<BLK> ra_n{nullptr, 0};
         uint64_t hn[DU_BATCH];
+        ra_n = ra_n2;
         if (fn < nbuckets) {
-            ra_n = bucket_of<BLK>(starts, ba, fn, lo_n, hi_n);
+            ra_n.range(lo_n, hi_n);
             load_batch(ra_n, lo_n, hi_n, hn);
         }
+        if (fn + gridDim.x < nbuckets) ra_n2 = bucket_load<BLK>(starts, ba, fn + gridDim.x);
         if (lo == hi) {
             if (COUNTS && t == 0) ngroups[f] = 0;
         } else {
@@ -1566,7 +1652,7 @@ __global__ void __launch_bounds__(DTU) part_dedup_u64_kernel(const uint64_t *in_
                     const uint64_t h = s_key[i];
                     if (h != EMPTY64) {
                         const uint32_t p = atomicAdd(&s_n, 1u);
-                        const int64_t o = ra.at(lo + p);
+                        const int64_t o = ra.at_lane(lo + p);
                         out_key[o] = inv_mix64(h);
                         out_cnt[o] = s_cnt[i];
                     }
@@ -1608,23 +1694,19 @@ constexpr int WV_SLOTS = 2048;          // table slots per wave (16 KB)
 constexpr int WV_Q = 20;                // records per lane per batch
 constexpr int WV_BATCH = WV_Q * WAVE;   // 1280
 template <bool BLK>
-__device__ __forceinline__ void wave_load_batch(uint64_t (&hq)[WV_Q], const uint64_t *in_h, const RecAt<BLK> &ra,
+__device__ __forceinline__ void wave_load_batch(uint64_t (&hq)[WV_Q], const uint64_t *in_h, const Bkt<BLK> &ra,
                                                 int64_t rb, int64_t hi, int lane) {
-    if constexpr (BLK) {
-        const uint32_t bl = ra.blist[ra.l0 + (uint32_t)(rb / L2B) + (uint32_t)(lane < WV_Q ? lane : WV_Q - 1)];
+    // (validity as q * WAVE < rem: a compare with a constant per q, where
+    // rb + q * WAVE + lane < hi makes the compiler hoist 64-bit q * WAVE + lane
+    // values out of the bucket loop)
+    const int64_t rem = hi - rb - lane;
+    if (ra.inline_batch(rb, WV_Q, hi)) {
 #pragma unroll
-        for (int q = 0; q < WV_Q; ++q) {
-            const int64_t r = rb + (int64_t)q * WAVE + lane;
-            const uint64_t *pb = in_h + (uint64_t)__builtin_amdgcn_readlane(bl, q) * L2B;
-            hq[q] = r < hi ? pb[lane] : EMPTY64;
-        }
+        for (int q = 0; q < WV_Q; ++q) hq[q] = (int64_t)q * WAVE < rem ? ra.wave_base_inl(in_h, rb, q)[lane] : EMPTY64;
         return;
     }
 #pragma unroll
-    for (int q = 0; q < WV_Q; ++q) {
-        const int64_t r = rb + (int64_t)q * WAVE + lane;
-        hq[q] = r < hi ? ra.wave_base(in_h, rb, q)[lane] : EMPTY64;
-    }
+    for (int q = 0; q < WV_Q; ++q) hq[q] = (int64_t)q * WAVE < rem ? ra.wave_base(in_h, rb, q)[lane] : EMPTY64;
 }
 // Two-phase wave dedup (round 3).  The round-2 register-queue loop (each lane
 // walking its own queue of records, deleted in round 5) paid a dependent LDS round trip plus a shift of
@@ -1672,7 +1754,7 @@ __device__ __forceinline__ uint32_t wave2_probe(uint64_t *T, uint64_t x, bool &f
 // one batch (records rb + q * 64 + lane, q < WV_Q, below hi) -> new groups of this lane
 template <int MODE, bool LIMIT, bool BLK>
 __device__ __forceinline__ uint32_t wave2_insert(uint64_t *T, uint64_t *O, const uint64_t (&hq)[WV_Q],
-                                                 const uint64_t *in_h, const RecAt<BLK> &ra, int64_t rb, int64_t hi,
+                                                 const uint64_t *in_h, const Bkt<BLK> &ra, int64_t rb, int64_t hi,
                                                  int lane, bool &full) {
     const int64_t rem = hi - rb - lane;
     const int left = rem <= 0 ? 0 : (int)min((int64_t)WV_Q, (rem + WAVE - 1) / WAVE);
@@ -1749,21 +1831,24 @@ __global__ void __launch_bounds__(WV_W * WAVE) part_dedup_u64_wave2_kernel(const
     const int64_t stride = (int64_t)gridDim.x * WV_W;
     int64_t f = (int64_t)__builtin_amdgcn_readfirstlane((int)(blockIdx.x * WV_W + w));
     int64_t lo = 0, hi = 0;
-    RecAt<BLK> ra{nullptr, 0};
+    Bkt<BLK> ra, ra_n, ra_n2;                  // buckets f, f + stride (records prefetched), f + 2 stride
     uint64_t hq[WV_Q];
     if (f < nbuckets) {
-        ra = bucket_of<BLK>(starts, ba, f, lo, hi);
+        ra = bucket_load<BLK>(starts, ba, f);
+        ra.range(lo, hi);
         wave_load_batch<BLK>(hq, in_h, ra, lo, hi, lane);
     }
+    if (f + stride < nbuckets) ra_n2 = bucket_load<BLK>(starts, ba, f + stride);
     uint64_t hn[WV_Q];
     auto step = [&](uint64_t (&cur)[WV_Q], uint64_t (&nxt)[WV_Q]) {
         const int64_t fn = f + stride;
         int64_t lo_n = 0, hi_n = 0;
-        RecAt<BLK> ra_n{nullptr, 0};
+        ra_n = ra_n2;
         if (fn < nbuckets) {
-            ra_n = bucket_of<BLK>(starts, ba, fn, lo_n, hi_n);
+            ra_n.range(lo_n, hi_n);
             wave_load_batch<BLK>(nxt, in_h, ra_n, lo_n, hi_n, lane);
         }
+        if (fn + stride < nbuckets) ra_n2 = bucket_load<BLK>(starts, ba, fn + stride);
         if (lo != hi) {
             ulonglong2 *T2 = (ulonglong2 *)T;
 #pragma unroll
@@ -1822,25 +1907,19 @@ constexpr int WH_Q = 16;                        // records per lane per batch (1
 constexpr int WH_BATCH = WH_Q * WAVE;
 constexpr int WH_OVF = 256;                     // collision-list entries per wave (2 KB)
 template <bool BLK>
-__device__ __forceinline__ void wave_load_batch16(uint64_t (&hq)[WH_Q], const uint64_t *in_h, const RecAt<BLK> &ra,
+__device__ __forceinline__ void wave_load_batch16(uint64_t (&hq)[WH_Q], const uint64_t *in_h, const Bkt<BLK> &ra,
                                                   int64_t rb, int64_t hi, int lane) {
-    if constexpr (BLK) {
-        // the batch's WH_Q list entries in one load (lane q holds block q),
-        // handed to the loads by readlane
-        const uint32_t bl = ra.blist[ra.l0 + (uint32_t)(rb / L2B) + (uint32_t)(lane < WH_Q ? lane : WH_Q - 1)];
+    // (validity as q * WAVE < rem: a compare with a constant per q, where
+    // rb + q * WAVE + lane < hi makes the compiler hoist 64-bit q * WAVE + lane
+    // values out of the bucket loop)
+    const int64_t rem = hi - rb - lane;
+    if (ra.inline_batch(rb, WH_Q, hi)) {
 #pragma unroll
-        for (int q = 0; q < WH_Q; ++q) {
-            const int64_t r = rb + (int64_t)q * WAVE + lane;
-            const uint64_t *pb = in_h + (uint64_t)__builtin_amdgcn_readlane(bl, q) * L2B;
-            hq[q] = r < hi ? pb[lane] : EMPTY64;
-        }
+        for (int q = 0; q < WH_Q; ++q) hq[q] = (int64_t)q * WAVE < rem ? ra.wave_base_inl(in_h, rb, q)[lane] : EMPTY64;
         return;
     }
 #pragma unroll
-    for (int q = 0; q < WH_Q; ++q) {
-        const int64_t r = rb + (int64_t)q * WAVE + lane;
-        hq[q] = r < hi ? ra.wave_base(in_h, rb, q)[lane] : EMPTY64;
-    }
+    for (int q = 0; q < WH_Q; ++q) hq[q] = (int64_t)q * WAVE < rem ? ra.wave_base(in_h, rb, q)[lane] : EMPTY64;
 }
 template <int MODE, bool LIMIT>
 __device__ __forceinline__ uint32_t wh_probe(uint64_t *T, uint64_t x, bool &full) {
@@ -1863,7 +1942,7 @@ __device__ __forceinline__ uint32_t wh_probe(uint64_t *T, uint64_t x, bool &full
 // the records of half `hb` (hash bit 10) among this lane's batch -> new groups
 template <int MODE, bool LIMIT, bool BLK>
 __device__ __forceinline__ uint32_t wh_insert(uint64_t *T, uint64_t *O, const uint64_t (&hq)[WH_Q],
-                                              const uint64_t *in_h, const RecAt<BLK> &ra, int64_t rb, int64_t hi,
+                                              const uint64_t *in_h, const Bkt<BLK> &ra, int64_t rb, int64_t hi,
                                               int lane, uint32_t hb, bool &full) {
     const int64_t rem = hi - rb - lane;
     const int left = rem <= 0 ? 0 : (int)min((int64_t)WH_Q, (rem + WAVE - 1) / WAVE);
@@ -1939,9 +2018,16 @@ __global__ void __launch_bounds__(WV_W * WAVE, 4) part_dedup_u64_half_kernel(con
     uint64_t groups = 0;
     bool full = false;
     const int64_t stride = (int64_t)gridDim.x * WV_W;
-    for (int64_t f = (int64_t)blockIdx.x * WV_W + w; f < nbuckets; f += stride) {
+    Bkt<BLK> ra_n;                             // the next bucket's range / descriptor, one bucket ahead
+    // (blocks: the bucket index in a scalar register, so are the descriptor addresses)
+    const int64_t f0 = BLK ? (int64_t)__builtin_amdgcn_readfirstlane((int)(blockIdx.x * WV_W + w))
+                           : (int64_t)blockIdx.x * WV_W + w;
+    if (f0 < nbuckets) ra_n = bucket_load<BLK>(starts, ba, f0);
+    for (int64_t f = f0; f < nbuckets; f += stride) {
         int64_t lo, hi;
-        const RecAt<BLK> ra = bucket_of<BLK>(starts, ba, f, lo, hi);
+        const Bkt<BLK> ra = ra_n;
+        ra.range(lo, hi);
+        if (f + stride < nbuckets) ra_n = bucket_load<BLK>(starts, ba, f + stride);
         uint32_t fresh = 0;
         if (lo != hi) {
             uint64_t hq[WH_Q];
@@ -1996,7 +2082,7 @@ struct DRound {
 };
 template <bool BLK>
 __device__ __forceinline__ void dedup_load_round(DRound &r, const uint64_t *in_k0, const uint64_t *in_k1,
-                                                 const uint64_t *in_meta, const RecAt<BLK> &ra, int64_t rb,
+                                                 const uint64_t *in_meta, const Bkt<BLK> &ra, int64_t rb,
                                                  int64_t hi) {
 #pragma unroll
     for (int q = 0; q < D_RPT; ++q) {
@@ -2029,24 +2115,27 @@ __global__ void __launch_bounds__(DT) part_dedup_bytes_kernel(const uint64_t *in
     uint64_t acc_groups = 0;
     bool acc_full = false, acc_coll = false;
     int64_t f = blockIdx.x, lo = 0, hi = 0;
-    RecAt<BLK> ra{nullptr, 0};
+    Bkt<BLK> ra, ra_n, ra_n2;                  // buckets f, f + G (first round prefetched), f + 2G
     DRound cur, nxt;
     for (int i = t; i < D_B; i += DT) {                 // once: buckets reset only their own slots
         s_h[i] = EMPTY64;
         s_cnt[i] = 0;
     }
     if (f < nbuckets) {
-        ra = bucket_of<BLK>(starts, ba, f, lo, hi);
+        ra = bucket_load<BLK>(starts, ba, f);
+        ra.range(lo, hi);
         dedup_load_round<BLK>(cur, in_k0, in_k1, in_meta, ra, lo, hi);
     }
+    if (f + gridDim.x < nbuckets) ra_n2 = bucket_load<BLK>(starts, ba, f + gridDim.x);
     for (; f < nbuckets; f += gridDim.x) {
         const int64_t fn = f + gridDim.x;
         int64_t lo_n = 0, hi_n = 0;
-        RecAt<BLK> ra_n{nullptr, 0};
+        ra_n = ra_n2;
         if (fn < nbuckets) {                                     // next bucket in flight
-            ra_n = bucket_of<BLK>(starts, ba, fn, lo_n, hi_n);
+            ra_n.range(lo_n, hi_n);
             dedup_load_round<BLK>(nxt, in_k0, in_k1, in_meta, ra_n, lo_n, hi_n);
         }
+        if (fn + gridDim.x < nbuckets) ra_n2 = bucket_load<BLK>(starts, ba, fn + gridDim.x);
         if (lo == hi) {
             if (t == 0) ngroups[f] = 0;
         } else {
@@ -2157,7 +2246,8 @@ __global__ void __launch_bounds__(PT) part_compact_kernel(const uint64_t *src_a,
                                                           uint64_t *dst_a, uint64_t *dst_b) {
     for (int64_t f = blockIdx.x; f < nbuckets; f += gridDim.x) {
         int64_t lo, hi;
-        const RecAt<BLK> ra = bucket_of<BLK>(starts, ba, f, lo, hi);
+        const Bkt<BLK> ra = bucket_load<BLK>(starts, ba, f);
+        ra.range(lo, hi);
         const int64_t o = out_off[f];
         const uint32_t m = ngroups[f];
         for (uint32_t i = threadIdx.x; i < m; i += PT) {
@@ -2776,16 +2866,16 @@ int sdp_part_dedup(const sdp_records *in, int32_t is_bytes, const sdp_bytes_colu
                    int64_t nbuckets, int32_t with_counts, uint64_t *d_out_key, uint64_t *d_out_cnt,
                    uint32_t *d_ngroups, uint64_t *d_stats, void *stream) {
     if (d_starts == nullptr) return set_error(SDP_EINVAL, "part_dedup: args");
-    return dedup_launch<false>(in, is_bytes, bcol, d_starts, BlkArg{nullptr, nullptr, nullptr}, nbuckets, with_counts,
+    return dedup_launch<false>(in, is_bytes, bcol, d_starts, BlkArg{nullptr, nullptr}, nbuckets, with_counts,
                                d_out_key, d_out_cnt, d_ngroups, d_stats, stream);
 }
 
 int sdp_part_dedup_blocks(const sdp_records *in, int32_t is_bytes, const sdp_bytes_column *bcol, const sdp_blocks *blk,
                           int64_t nbuckets, int32_t with_counts, uint64_t *d_out_key, uint64_t *d_out_cnt,
                           uint32_t *d_ngroups, uint64_t *d_stats, void *stream) {
-    if (blk == nullptr || blk->d_fcnt == nullptr || blk->d_floff == nullptr || blk->d_list == nullptr)
+    if (blk == nullptr || blk->d_desc == nullptr || blk->d_list == nullptr)
         return set_error(SDP_EINVAL, "part_dedup_blocks: blocks");
-    return dedup_launch<true>(in, is_bytes, bcol, nullptr, BlkArg{blk->d_fcnt, blk->d_floff, blk->d_list}, nbuckets,
+    return dedup_launch<true>(in, is_bytes, bcol, nullptr, BlkArg{blk->d_desc, blk->d_list}, nbuckets,
                               with_counts, d_out_key, d_out_cnt, d_ngroups, d_stats, stream);
 }
 
@@ -2793,7 +2883,7 @@ int sdp_part_l2_blocks(const sdp_records *in, int32_t is_bytes, const sdp_chunk 
                        int32_t nwg, int32_t b1, int32_t b2, const sdp_records *out, uint64_t *d_bmeta,
                        const sdp_blocks *blk, void *stream) {
     if (in == nullptr || out == nullptr || d_segs == nullptr || d_soff == nullptr || d_bmeta == nullptr ||
-        blk == nullptr || blk->d_fcnt == nullptr || blk->d_floff == nullptr || blk->d_list == nullptr ||
+        blk == nullptr || blk->d_desc == nullptr || blk->d_list == nullptr ||
         nwg < 1 || nwg > 65535 || b1 < 0 || b2 < 1 || b1 + b2 > 63)
         return set_error(SDP_EINVAL, "part_l2_blocks: args");
     if ((1 << b2) > (is_bytes ? L2BCfg<true>::NBM : L2BCfg<false>::NBM))
@@ -2804,12 +2894,10 @@ int sdp_part_l2_blocks(const sdp_records *in, int32_t is_bytes, const sdp_chunk 
     const Chunk *sg = (const Chunk *)d_segs;
     if (is_bytes)
         hipLaunchKernelGGL(part_l2_blocks_kernel<true>, dim3(nwg), dim3(ST), 0, s, in->d_k0, in->d_k1, in->d_meta,
-                           sg, d_soff, b1, b2, out->d_k0, out->d_k1, out->d_meta, d_bmeta, blk->d_list, blk->d_fcnt,
-                           blk->d_floff);
+                           sg, d_soff, b1, b2, out->d_k0, out->d_k1, out->d_meta, d_bmeta, blk->d_list, blk->d_desc);
     else
         hipLaunchKernelGGL(part_l2_blocks_kernel<false>, dim3(nwg), dim3(ST), 0, s, in->d_k0, nullptr, nullptr, sg,
-                           d_soff, b1, b2, out->d_k0, nullptr, nullptr, d_bmeta, blk->d_list, blk->d_fcnt,
-                           blk->d_floff);
+                           d_soff, b1, b2, out->d_k0, nullptr, nullptr, d_bmeta, blk->d_list, blk->d_desc);
     return check_launch("part_l2_blocks_kernel");
 }
 
@@ -2819,7 +2907,7 @@ int sdp_part_compact(const uint64_t *d_src_a, const uint64_t *d_src_b, const uin
     if (d_src_a == nullptr || d_dst_a == nullptr || nbuckets < 1 || (d_src_b != nullptr) != (d_dst_b != nullptr))
         return set_error(SDP_EINVAL, "part_compact: args");
     hipLaunchKernelGGL(part_compact_kernel<false>, dim3(grid_of(nbuckets, 8192)), dim3(PT), 0, (hipStream_t)stream,
-                       d_src_a, d_src_b, d_starts, BlkArg{nullptr, nullptr, nullptr}, d_ngroups, d_out_offsets,
+                       d_src_a, d_src_b, d_starts, BlkArg{nullptr, nullptr}, d_ngroups, d_out_offsets,
                        nbuckets, d_dst_a, d_dst_b);
     return check_launch("part_compact_kernel");
 }
@@ -2828,10 +2916,10 @@ int sdp_part_compact_blocks(const uint64_t *d_src_a, const uint64_t *d_src_b, co
                             const uint32_t *d_ngroups, const uint64_t *d_out_offsets, int64_t nbuckets,
                             uint64_t *d_dst_a, uint64_t *d_dst_b, void *stream) {
     if (d_src_a == nullptr || d_dst_a == nullptr || nbuckets < 1 || (d_src_b != nullptr) != (d_dst_b != nullptr) ||
-        blk == nullptr || blk->d_fcnt == nullptr || blk->d_floff == nullptr || blk->d_list == nullptr)
+        blk == nullptr || blk->d_desc == nullptr || blk->d_list == nullptr)
         return set_error(SDP_EINVAL, "part_compact_blocks: args");
     hipLaunchKernelGGL(part_compact_kernel<true>, dim3(grid_of(nbuckets, 8192)), dim3(PT), 0, (hipStream_t)stream,
-                       d_src_a, d_src_b, nullptr, BlkArg{blk->d_fcnt, blk->d_floff, blk->d_list}, d_ngroups,
+                       d_src_a, d_src_b, nullptr, BlkArg{blk->d_desc, blk->d_list}, d_ngroups,
                        d_out_offsets, nbuckets, d_dst_a, d_dst_b);
     return check_launch("part_compact_kernel");
 }

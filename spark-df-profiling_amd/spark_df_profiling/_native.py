@@ -35,6 +35,7 @@ PART_SAMPLE = 16384          # SDP_PART_SAMPLE
 PART_SAMPLE_BYTES = 65536    # SDP_PART_SAMPLE_BYTES
 PART_CHUNK = 131072          # SDP_PART_CHUNK
 L2_BLOCK = 64                # SDP_L2_BLOCK: records per block of sdp_part_l2_blocks
+L2_DESC_W = 4                # SDP_L2_DESC_W: u32 words per final-bucket descriptor
 GSORT_MAX = 8192             # SDP_GSORT_MAX
 BYTE_RECORD_ARRAYS = 3       # byte-key records: k0[], k1[], meta[] (sdp_records)
 RECORD_WORD = 8              # bytes between one record's words in each array
@@ -151,7 +152,7 @@ class SdpTopkResult(ctypes.Structure):             # sdp_topk_result (sdp_value_
 
 
 class SdpBlocks(ctypes.Structure):                 # sdp_blocks (sdp_part_l2_blocks)
-    _fields_ = [('d_fcnt', ctypes.c_void_p), ('d_floff', ctypes.c_void_p), ('d_list', ctypes.c_void_p)]
+    _fields_ = [('d_desc', ctypes.c_void_p), ('d_list', ctypes.c_void_p)]
 
 
 QUANTILES_MAX = 16       # SDP_QUANTILES_MAX

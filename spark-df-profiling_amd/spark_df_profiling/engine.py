@@ -1208,7 +1208,12 @@ class Engine:
         seg_bucket = np.asarray(seg_bucket, dtype=np.int64)
         nb2 = 1 << b2
         sizes = np.bincount(seg_bucket, weights=seg_hi - seg_lo, minlength=nbk).astype(np.int64)
-        nblk = (-(-sizes // L2_BLOCK) + nb2 + 7) // 8 * 8        # regions on 64-byte lines of bmeta
+        # sub-bucket runs of mean + 4 sigma records (a near-unique column's
+        # sub-buckets practically never spill into overflow blocks); the
+        # overflow space covers every record, so nothing can overflow
+        mean = sizes / float(nb2)
+        R = np.ceil((mean + 4.0 * np.sqrt(mean) + 16.0) / L2_BLOCK).astype(np.int64)
+        nblk = (nb2 * R + -(-sizes // L2_BLOCK) + 8 + 7) // 8 * 8  # regions on 64-byte lines of bmeta
         rbase = np.zeros(nbk + 1, dtype=np.int64)
         rbase[1:] = np.cumsum(nblk)
         total = int(rbase[-1])
@@ -1231,7 +1236,7 @@ class Engine:
         tab[:, 0] = seg_lo[order]
         tab[:, 1] = seg_hi[order]
         tab[:, 2] = sb
-        tab[:, 3] = rbase[sb] | (first.astype(np.int64) << 32) | (last.astype(np.int64) << 33)
+        tab[:, 3] = rbase[sb] | (first.astype(np.int64) << 32) | (last.astype(np.int64) << 33) | (R[sb] << 40)
         soff = np.zeros(G + 1, dtype=np.int64)
         soff[1:] = np.cumsum(np.bincount(wg[sb], minlength=G))
         dt = self._h2d(np.concatenate([tab.reshape(-1), soff]))
@@ -1239,8 +1244,8 @@ class Engine:
         bmeta = self._u64(total)
         # (the dedup kernels read a batch's list entries in one load: padding)
         lst = torch.empty(total + 32, dtype=torch.int32, device=self.device)
-        fc = torch.empty(2 * nbk * nb2, dtype=torch.int32, device=self.device)
-        blk = nat.SdpBlocks(fc.data_ptr(), fc.data_ptr() + 4 * nbk * nb2, lst.data_ptr())
+        fc = torch.empty(nbk * nb2 * nat.L2_DESC_W, dtype=torch.int32, device=self.device)
+        blk = nat.SdpBlocks(fc.data_ptr(), lst.data_ptr())
         sdp.sdp_part_l2_blocks(ctypes.byref(r1), int(isb), ptr(dt), ctypes.c_void_p(dt.data_ptr() + 8 * tab.size), G,
                                b1, b2, ctypes.byref(rf), ptr(bmeta), ctypes.byref(blk), self._s())
         del bmeta, dt
