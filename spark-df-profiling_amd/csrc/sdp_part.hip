@@ -1451,30 +1451,32 @@ struct Bkt {
     int64_t lo = 0, hi = 0;                      // contiguous: [lo, hi)
     const uint32_t *dsc = nullptr;               // blocks: the descriptor,
     const uint32_t *blist = nullptr;
-    uint32_t dv = 0;                             //   its word lane % DESC_W
-    // the bucket-local range (waits for the descriptor)
-    __device__ __forceinline__ void range(int64_t &a, int64_t &b) const {
+    uint32_t dv = 0;                             //   its word lane % DESC_W as loaded,
+    uint32_t rl = 0, l0 = 0;                     //   run records, first list entry and
+    uint64_t r0 = 0;                             //   the run's first record (wave-uniform, from range())
+    // the bucket-local range; blocks: waits for the descriptor and takes its
+    // words out of the lanes that loaded them.  Call it where every lane of
+    // the wave is active (a lane that skipped the load holds no word)
+    __device__ __forceinline__ void range(int64_t &a, int64_t &b) {
         if constexpr (BLK) {
             a = 0;
             b = (int64_t)__builtin_amdgcn_readlane(dv, 0);
+            l0 = __builtin_amdgcn_readlane(dv, 1);
+            r0 = (uint64_t)__builtin_amdgcn_readlane(dv, 2) * L2B;
+            rl = __builtin_amdgcn_readlane(dv, 3);
         } else {
             a = lo;
             b = hi;
         }
     }
-    __device__ __forceinline__ uint64_t run0() const {          // the run's first record
-        return (uint64_t)__builtin_amdgcn_readlane(dv, 2) * L2B;
-    }
-    __device__ __forceinline__ uint32_t run_len() const { return __builtin_amdgcn_readlane(dv, 3); }
     // record i (i / L2B wave-uniform; no branch: the overflow list entry is
     // read either way, of block 0 for a record in the run)
     __device__ __forceinline__ int64_t at(int64_t i) const {
         if constexpr (BLK) {
-            const uint32_t rl = run_len();
             const bool inrun = (uint64_t)i < rl;
             const uint32_t ob = __builtin_amdgcn_readfirstlane(inrun ? 0u : (uint32_t)((i - rl) / L2B));
-            const uint32_t b = blist[__builtin_amdgcn_readlane(dv, 1) + ob];
-            return inrun ? (int64_t)(run0() + (uint64_t)i) : (int64_t)b * L2B + (i % L2B);
+            const uint32_t b = blist[l0 + ob];
+            return inrun ? (int64_t)(r0 + (uint64_t)i) : (int64_t)b * L2B + (i % L2B);
         } else {
             return i;
         }
@@ -1482,17 +1484,16 @@ struct Bkt {
     // record i, any i per lane
     __device__ __forceinline__ int64_t at_lane(int64_t i) const {
         if constexpr (BLK) {
-            const uint32_t rl = dsc[3];
-            if ((uint64_t)i < rl) return (int64_t)((uint64_t)dsc[2] * L2B + (uint64_t)i);
-            return (int64_t)blist[dsc[1] + (uint32_t)((i - rl) / L2B)] * L2B + (i % L2B);
+            if ((uint64_t)i < rl) return (int64_t)(r0 + (uint64_t)i);
+            return (int64_t)blist[l0 + (uint32_t)((i - rl) / L2B)] * L2B + (i % L2B);
         } else {
             return i;
         }
     }
     // the records of a batch of Q wave-wide loads from rb (below hi) lie in
     // the run (the common case: a bucket within its run)
-    __device__ __forceinline__ bool inline_batch(int64_t rb, int Q, int64_t hi) const {
-        if constexpr (BLK) return min(hi, rb + (int64_t)Q * WAVE) <= (int64_t)run_len();
+    __device__ __forceinline__ bool inline_batch(int64_t rb, int Q, int64_t hi_) const {
+        if constexpr (BLK) return min(hi_, rb + (int64_t)Q * WAVE) <= (int64_t)rl;
         else return true;
     }
     // (inline_batch) records rb + q * WAVE + lane start here.  Blocks: the
@@ -1501,7 +1502,7 @@ struct Bkt {
     // per-q 64-bit lane offsets out of the bucket loop and spills them)
     __device__ __forceinline__ const uint64_t *wave_base_inl(const uint64_t *p, int64_t rb, int q) const {
         if constexpr (BLK) {
-            const uint64_t a = (uint64_t)(p + run0() + rb + (int64_t)q * WAVE);
+            const uint64_t a = (uint64_t)(p + r0 + rb + (int64_t)q * WAVE);
             return (const uint64_t *)(((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(a >> 32)) << 32) |
                                       __builtin_amdgcn_readfirstlane((uint32_t)a));
         } else {
@@ -1513,11 +1514,10 @@ struct Bkt {
         if constexpr (BLK) {
             static_assert(L2B == WAVE, "one block per wave-wide load");
             const int64_t i = rb + (int64_t)q * WAVE;
-            const uint32_t rl = run_len();
             const bool inrun = (uint64_t)i < rl;
             const uint32_t ob = __builtin_amdgcn_readfirstlane(inrun ? 0u : (uint32_t)((i - rl) / L2B));
-            const uint32_t b = blist[__builtin_amdgcn_readlane(dv, 1) + ob];
-            return inrun ? p + run0() + i : p + (uint64_t)b * L2B;
+            const uint32_t b = blist[l0 + ob];
+            return inrun ? p + r0 + i : p + (uint64_t)b * L2B;
         } else {
             return p + rb + (int64_t)q * WAVE;
         }
@@ -2025,7 +2025,7 @@ __global__ void __launch_bounds__(WV_W * WAVE, 4) part_dedup_u64_half_kernel(con
     if (f0 < nbuckets) ra_n = bucket_load<BLK>(starts, ba, f0);
     for (int64_t f = f0; f < nbuckets; f += stride) {
         int64_t lo, hi;
-        const Bkt<BLK> ra = ra_n;
+        Bkt<BLK> ra = ra_n;
         ra.range(lo, hi);
         if (f + stride < nbuckets) ra_n = bucket_load<BLK>(starts, ba, f + stride);
         uint32_t fresh = 0;
@@ -2246,7 +2246,7 @@ __global__ void __launch_bounds__(PT) part_compact_kernel(const uint64_t *src_a,
                                                           uint64_t *dst_a, uint64_t *dst_b) {
     for (int64_t f = blockIdx.x; f < nbuckets; f += gridDim.x) {
         int64_t lo, hi;
-        const Bkt<BLK> ra = bucket_load<BLK>(starts, ba, f);
+        Bkt<BLK> ra = bucket_load<BLK>(starts, ba, f);
         ra.range(lo, hi);
         const int64_t o = out_off[f];
         const uint32_t m = ngroups[f];

@@ -2251,7 +2251,7 @@ class Engine:
             off = 0
             for (i, ctx), m in zip(done, sizes):
                 out[i] = self._group_end(ctx, allst[off:off + m], True)
-                for key in ('out_key', 'out_cnt', 'starts', 'ngroups', 'stats_dev'):
+                for key in ('out_key', 'out_cnt', 'starts', 'ngroups', 'stats_dev', 'blk', 'blk_keep'):
                     ctx.pop(key, None)
                 off += m
             done.clear()
@@ -2659,6 +2659,8 @@ class Engine:
     def row_bytes_values(self, src: DeviceColumn, rows, col: DeviceColumn):
         if not rows:
             return []
+        if min(rows) < 0 or max(rows) >= src.length:        # (checked here, not by a device-side assert)
+            raise nat.NativeError('row_bytes_values: a group row outside the column')
         if src.fixed_width:
             w = src.fixed_width
             starts = [r * w for r in rows]
