@@ -636,6 +636,8 @@ typedef struct sdp_blocks {
 int sdp_part_l2_blocks(const sdp_records *in, int32_t is_bytes, const sdp_chunk *d_segs, const int64_t *d_soff,
                        int32_t nwg, int32_t b1, int32_t b2, const sdp_records *out, uint64_t *d_bmeta,
                        const sdp_blocks *blk, void *stream);
+/* Test builds only (-DSDP_DEBUG_BOUNDS): bounds flags of the block layout. */
+int sdp_debug_bounds(uint64_t cap_rec, uint64_t cap_blk, uint64_t *flags_out, int32_t reset);
 /* sdp_part_dedup over the final buckets of sdp_part_l2_blocks (the same modes
  * and outputs; groups of f go to the block positions of its records 0 ..
  * d_ngroups[f]). */

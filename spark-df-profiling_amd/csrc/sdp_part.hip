@@ -32,6 +32,26 @@
 
 namespace sdp {
 
+// SDP_DEBUG_BOUNDS builds (tools/debug_bounds.sh, never the shipped library):
+// block-layout indices are checked against the record / block capacities of
+// the last sdp_part_l2_blocks call, and an index outside them raises a flag
+// bit (read by sdp_debug_bounds) and is replaced by 0 instead of faulting
+#ifdef SDP_DEBUG_BOUNDS
+__device__ unsigned long long dbg_flags, dbg_cap_rec, dbg_cap_blk;
+__device__ __forceinline__ int64_t dbg_chk(int64_t i, unsigned long long cap, int code) {
+    if ((unsigned long long)i >= cap) {
+        atomicOr(&dbg_flags, 1ull << code);
+        return 0;
+    }
+    return i;
+}
+#define DBG_REC(i, code) dbg_chk((int64_t)(i), dbg_cap_rec, (code))
+#define DBG_BLK(i, code) dbg_chk((int64_t)(i), dbg_cap_blk, (code))
+#else
+#define DBG_REC(i, code) (i)
+#define DBG_BLK(i, code) (i)
+#endif
+
 constexpr int PT = 256;                 // threads of the small helper kernels
 constexpr uint64_t RMASK40 = (1ull << 40) - 1ull;
 constexpr uint64_t LEN_MAX = (1ull << 24) - 1ull;
@@ -1335,7 +1355,7 @@ __global__ void __launch_bounds__(ST) part_l2_blocks_kernel(const uint64_t *in_k
                         const uint32_t b0 = atomicAdd(&s.next, nn);
                         s.nbase[j] = (int32_t)b0 - (int32_t)kf;
                         for (uint32_t u = 0; u < nn; ++u)
-                            bmeta[g.OB + b0 + u] = ((uint64_t)j << 32) | (uint64_t)(kf + u);
+                            bmeta[DBG_BLK(g.OB + b0 + u, 9)] = ((uint64_t)j << 32) | (uint64_t)(kf + u);
                     }
                 }
                 if (e / L != cc / L) s.list[atomicAdd(&s.nlist, 1u)] = (uint16_t)j;
@@ -1355,7 +1375,7 @@ __global__ void __launch_bounds__(ST) part_l2_blocks_kernel(const uint64_t *in_k
 #pragma unroll
                         for (int a = 0; a < NA; ++a) s.line[a][j][p % L] = x[a][q];
                     } else if (p / L != e / L) {
-                        const uint64_t o = l2b_rec(s, g, j, p);
+                        const uint64_t o = DBG_REC(l2b_rec(s, g, j, p), 8);
 #pragma unroll
                         for (int a = 0; a < NA; ++a) out[a][o] = x[a][q];
                     } else {
@@ -1369,7 +1389,7 @@ __global__ void __launch_bounds__(ST) part_l2_blocks_kernel(const uint64_t *in_k
             const uint32_t nl = s.nlist;
             for (uint32_t i = t / L; i < nl; i += ST / L) {
                 const int j = s.list[i], l = t & (L - 1);
-                const uint64_t o = l2b_rec(s, g, j, (s.cur[j] / L) * L + l);
+                const uint64_t o = DBG_REC(l2b_rec(s, g, j, (s.cur[j] / L) * L + l), 11);
 #pragma unroll
                 for (int a = 0; a < NA; ++a) out[a][o] = s.line[a][j][l];
             }
@@ -1400,8 +1420,8 @@ __global__ void __launch_bounds__(ST) part_l2_blocks_kernel(const uint64_t *in_k
             for (int j = t; j < nb; j += ST) {
                 const uint32_t cc = s.cur[j];
                 for (uint32_t pp = (cc / L) * L; pp < cc; ++pp) {
-                    const uint64_t o = pp < g.RL ? (g.RB + (uint64_t)j * g.R) * L2B + pp
-                                                 : (g.OB + s.cb[j]) * L2B + (pp - g.RL) % L2B;
+                    const uint64_t o = DBG_REC(pp < g.RL ? (g.RB + (uint64_t)j * g.R) * L2B + pp
+                                                         : (g.OB + s.cb[j]) * L2B + (pp - g.RL) % L2B, 12);
 #pragma unroll
                     for (int a = 0; a < NA; ++a) out[a][o] = s.line[a][j][pp % L];
                 }
@@ -1424,10 +1444,10 @@ __global__ void __launch_bounds__(ST) part_l2_blocks_kernel(const uint64_t *in_k
             __syncthreads();
             const uint32_t nblk = s.next;
             for (uint32_t u = t; u < nblk; u += ST) {
-                const uint64_t m = bmeta[g.OB + u];
+                const uint64_t m = bmeta[DBG_BLK(g.OB + u, 13)];
                 const int j = (int)(m >> 32);
                 const uint32_t kk = (uint32_t)m;
-                blist[(uint32_t)g.OB + (uint32_t)s.nbase[j] + kk] = (uint32_t)g.OB + u;
+                blist[DBG_BLK((uint32_t)g.OB + (uint32_t)s.nbase[j] + kk, 10)] = (uint32_t)g.OB + u;
             }
             lds_barrier();                                     // (LDS reused by the next bucket)
         }
@@ -1446,37 +1466,34 @@ __global__ void __launch_bounds__(ST) part_l2_blocks_kernel(const uint64_t *in_k
 struct BlkArg {
     const uint32_t *desc, *blist;
 };
+// scalar (constant address space) loads of data no kernel writes while it runs
+typedef __attribute__((address_space(4))) const uint32_t cu32;
+__device__ __forceinline__ uint32_t sload(const uint32_t *p, uint32_t i) { return ((cu32 *)p)[i]; }
+
 template <bool BLK>
 struct Bkt {
     int64_t lo = 0, hi = 0;                      // contiguous: [lo, hi)
-    const uint32_t *dsc = nullptr;               // blocks: the descriptor,
-    const uint32_t *blist = nullptr;
-    uint32_t dv = 0;                             //   its word lane % DESC_W as loaded,
-    uint32_t rl = 0, l0 = 0;                     //   run records, first list entry and
-    uint64_t r0 = 0;                             //   the run's first record (wave-uniform, from range())
-    // the bucket-local range; blocks: waits for the descriptor and takes its
-    // words out of the lanes that loaded them.  Call it where every lane of
-    // the wave is active (a lane that skipped the load holds no word)
-    __device__ __forceinline__ void range(int64_t &a, int64_t &b) {
+    const uint32_t *blist = nullptr;             // blocks: the overflow lists,
+    uint4 d = {0, 0, 0, 0};                      //   the descriptor {n, first list entry, run block, run records}
+    // the bucket-local range (contiguous: lo, hi; blocks: 0, n)
+    __device__ __forceinline__ void range(int64_t &a, int64_t &b) const {
         if constexpr (BLK) {
             a = 0;
-            b = (int64_t)__builtin_amdgcn_readlane(dv, 0);
-            l0 = __builtin_amdgcn_readlane(dv, 1);
-            r0 = (uint64_t)__builtin_amdgcn_readlane(dv, 2) * L2B;
-            rl = __builtin_amdgcn_readlane(dv, 3);
+            b = (int64_t)d.x;
         } else {
             a = lo;
             b = hi;
         }
     }
+    __device__ __forceinline__ uint64_t r0() const { return (uint64_t)d.z * L2B; }
     // record i (i / L2B wave-uniform; no branch: the overflow list entry is
     // read either way, of block 0 for a record in the run)
     __device__ __forceinline__ int64_t at(int64_t i) const {
         if constexpr (BLK) {
-            const bool inrun = (uint64_t)i < rl;
-            const uint32_t ob = __builtin_amdgcn_readfirstlane(inrun ? 0u : (uint32_t)((i - rl) / L2B));
-            const uint32_t b = blist[l0 + ob];
-            return inrun ? (int64_t)(r0 + (uint64_t)i) : (int64_t)b * L2B + (i % L2B);
+            const bool inrun = (uint64_t)i < d.w;
+            const uint32_t ob = __builtin_amdgcn_readfirstlane(inrun ? 0u : (uint32_t)((i - d.w) / L2B));
+            const uint32_t b = sload(blist, DBG_BLK(d.y + ob, 5));
+            return DBG_REC(inrun ? (int64_t)(r0() + (uint64_t)i) : (int64_t)b * L2B + (i % L2B), 1);
         } else {
             return i;
         }
@@ -1484,8 +1501,8 @@ struct Bkt {
     // record i, any i per lane
     __device__ __forceinline__ int64_t at_lane(int64_t i) const {
         if constexpr (BLK) {
-            if ((uint64_t)i < rl) return (int64_t)(r0 + (uint64_t)i);
-            return (int64_t)blist[l0 + (uint32_t)((i - rl) / L2B)] * L2B + (i % L2B);
+            if ((uint64_t)i < d.w) return DBG_REC((int64_t)(r0() + (uint64_t)i), 2);
+            return DBG_REC((int64_t)blist[DBG_BLK(d.y + (uint32_t)((i - d.w) / L2B), 6)] * L2B + (i % L2B), 2);
         } else {
             return i;
         }
@@ -1493,7 +1510,7 @@ struct Bkt {
     // the records of a batch of Q wave-wide loads from rb (below hi) lie in
     // the run (the common case: a bucket within its run)
     __device__ __forceinline__ bool inline_batch(int64_t rb, int Q, int64_t hi_) const {
-        if constexpr (BLK) return min(hi_, rb + (int64_t)Q * WAVE) <= (int64_t)rl;
+        if constexpr (BLK) return min(hi_, rb + (int64_t)Q * WAVE) <= (int64_t)d.w;
         else return true;
     }
     // (inline_batch) records rb + q * WAVE + lane start here.  Blocks: the
@@ -1502,35 +1519,36 @@ struct Bkt {
     // per-q 64-bit lane offsets out of the bucket loop and spills them)
     __device__ __forceinline__ const uint64_t *wave_base_inl(const uint64_t *p, int64_t rb, int q) const {
         if constexpr (BLK) {
-            const uint64_t a = (uint64_t)(p + r0 + rb + (int64_t)q * WAVE);
+            const uint64_t a = (uint64_t)(p + DBG_REC(r0() + rb + (int64_t)q * WAVE, 4));
             return (const uint64_t *)(((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(a >> 32)) << 32) |
                                       __builtin_amdgcn_readfirstlane((uint32_t)a));
         } else {
             return p + rb + (int64_t)q * WAVE;
         }
     }
-    // records rb + q * WAVE + lane start here (rb a multiple of WAVE, wave-uniform)
+    // records rb + q * WAVE + lane start here (rb a multiple of WAVE and q
+    // wave-uniform)
     __device__ __forceinline__ const uint64_t *wave_base(const uint64_t *p, int64_t rb, int q) const {
         if constexpr (BLK) {
             static_assert(L2B == WAVE, "one block per wave-wide load");
             const int64_t i = rb + (int64_t)q * WAVE;
-            const bool inrun = (uint64_t)i < rl;
-            const uint32_t ob = __builtin_amdgcn_readfirstlane(inrun ? 0u : (uint32_t)((i - rl) / L2B));
-            const uint32_t b = blist[l0 + ob];
-            return inrun ? p + r0 + i : p + (uint64_t)b * L2B;
+            const bool inrun = (uint64_t)i < d.w;
+            const uint32_t ob = inrun ? 0u : (uint32_t)((i - d.w) / L2B);
+            const uint32_t b = sload(blist, DBG_BLK(d.y + ob, 7));
+            return p + DBG_REC(inrun ? r0() + i : (uint64_t)b * L2B, 3);
         } else {
             return p + rb + (int64_t)q * WAVE;
         }
     }
 };
-// issue the loads of bucket f's range / descriptor
+// bucket f's range / descriptor (f wave-uniform: scalar loads, waited for at use)
 template <bool BLK>
 __device__ __forceinline__ Bkt<BLK> bucket_load(const uint64_t *starts, const BlkArg &ba, int64_t f) {
     Bkt<BLK> k;
     if constexpr (BLK) {
         k.blist = ba.blist;
-        k.dsc = ba.desc + f * DESC_W;
-        k.dv = k.dsc[threadIdx.x & (DESC_W - 1)];
+        const uint32_t o = (uint32_t)f * DESC_W;
+        k.d = make_uint4(sload(ba.desc, o), sload(ba.desc, o + 1), sload(ba.desc, o + 2), sload(ba.desc, o + 3));
     } else {
         k.lo = starts[f];
         k.hi = starts[f + 1];
@@ -1809,7 +1827,7 @@ __device__ __forceinline__ uint32_t wave2_insert(uint64_t *T, uint64_t *O, const
     while (late) {                                           // list overflow: re-read from L2
         const int q = __builtin_ctz(late);
         late &= late - 1;
-        fresh += wave2_probe<MODE, LIMIT>(T, ra.wave_base(in_h, rb, q)[lane], full);
+        fresh += wave2_probe<MODE, LIMIT>(T, in_h[ra.at_lane(rb + (int64_t)q * WAVE + lane)], full);
     }
     __builtin_amdgcn_wave_barrier();
     return fresh;
@@ -1999,7 +2017,7 @@ __device__ __forceinline__ uint32_t wh_insert(uint64_t *T, uint64_t *O, const ui
     while (late) {
         const int q = __builtin_ctz(late);
         late &= late - 1;
-        fresh += wh_probe<MODE, LIMIT>(T, ra.wave_base(in_h, rb, q)[lane], full);
+        fresh += wh_probe<MODE, LIMIT>(T, in_h[ra.at_lane(rb + (int64_t)q * WAVE + lane)], full);
     }
     __builtin_amdgcn_wave_barrier();
     return fresh;
@@ -2922,6 +2940,29 @@ int sdp_part_compact_blocks(const uint64_t *d_src_a, const uint64_t *d_src_b, co
                        d_src_a, d_src_b, nullptr, BlkArg{blk->d_desc, blk->d_list}, d_ngroups,
                        d_out_offsets, nbuckets, d_dst_a, d_dst_b);
     return check_launch("part_compact_kernel");
+}
+
+// (SDP_DEBUG_BOUNDS builds) set the capacities the checks use (cap_rec > 0),
+// then read and optionally clear the flags
+int sdp_debug_bounds(uint64_t cap_rec, uint64_t cap_blk, uint64_t *flags_out, int32_t reset) {
+#ifdef SDP_DEBUG_BOUNDS
+    if (cap_rec) {
+        unsigned long long a = cap_rec, b = cap_blk;
+        hipMemcpyToSymbol(HIP_SYMBOL(dbg_cap_rec), &a, 8);
+        hipMemcpyToSymbol(HIP_SYMBOL(dbg_cap_blk), &b, 8);
+    }
+    unsigned long long f = 0;
+    hipMemcpyFromSymbol(&f, HIP_SYMBOL(dbg_flags), 8);
+    if (flags_out) *flags_out = f;
+    if (reset) {
+        f = 0;
+        hipMemcpyToSymbol(HIP_SYMBOL(dbg_flags), &f, 8);
+    }
+    return SDP_OK;
+#else
+    (void)cap_rec; (void)cap_blk; (void)flags_out; (void)reset;
+    return set_error(SDP_EINVAL, "sdp_debug_bounds: not an SDP_DEBUG_BOUNDS build");
+#endif
 }
 
 int64_t sdp_scan_workspace_bytes(int64_t n) {

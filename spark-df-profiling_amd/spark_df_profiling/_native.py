@@ -278,6 +278,7 @@ _SIGNATURES = {
     'sdp_part_dedup_blocks': (ctypes.c_int, [_REC, _I32, _BCOL, ctypes.POINTER(SdpBlocks), _I64, _I32, _P, _P, _P,
                                              _P, _P]),
     'sdp_part_compact_blocks': (ctypes.c_int, [_P, _P, ctypes.POINTER(SdpBlocks), _P, _P, _I64, _P, _P, _P]),
+    'sdp_debug_bounds': (ctypes.c_int, [_U64, _U64, _P, _I32]),
     'sdp_distinct32_workspace_bytes': (_I64, [_I64]),
     'sdp_distinct32': (ctypes.c_int, [_COL, _I64, _P, _P, _I64, _P, _P]),
     'sdp_scan_workspace_bytes': (_I64, [_I64]),

@@ -72,6 +72,7 @@ PASS2_BATCH = os.environ.get('SDP_PASS2_BATCH', '1') != '0'
 # level 2 (sdp_part_recs phase 0 + 1) for A/B runs
 L2_BLOCKS = os.environ.get('SDP_L2_BLOCKS', '1') != '0'
 L2_BLOCK = nat.L2_BLOCK
+DEBUG_BOUNDS = os.environ.get('SDP_DEBUG_BOUNDS', '') == '1'      # a tools/debug_bounds.sh library is loaded
 CAND_FULL_BUDGET = 1 << 30   # bytes of room-for-every-row candidate slots per pass-1 batch
 
 # Test knob for the quantile edge paths (never set in production):
@@ -1246,6 +1247,8 @@ class Engine:
         lst = torch.empty(total + 32, dtype=torch.int32, device=self.device)
         fc = torch.empty(nbk * nb2 * nat.L2_DESC_W, dtype=torch.int32, device=self.device)
         blk = nat.SdpBlocks(fc.data_ptr(), lst.data_ptr())
+        if DEBUG_BOUNDS:                   # (test builds: the capacities the bounds checks use)
+            sdp.sdp_debug_bounds(total * L2_BLOCK, total + 32, None, 0)
         sdp.sdp_part_l2_blocks(ctypes.byref(r1), int(isb), ptr(dt), ctypes.c_void_p(dt.data_ptr() + 8 * tab.size), G,
                                b1, b2, ctypes.byref(rf), ptr(bmeta), ctypes.byref(blk), self._s())
         del bmeta, dt
