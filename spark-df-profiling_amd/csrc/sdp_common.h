@@ -39,6 +39,15 @@ __host__ __device__ __forceinline__ uint64_t f64_key(double d) {
     if (d != d) b = 0x7FF8000000000000ull;     // one NaN
     return (b >> 63) ? ~b : (b | 0x8000000000000000ull);
 }
+// f64_key of a non-NaN value: -0.0 becomes +0.0 by adding +0.0 (IEEE
+// round-to-nearest; the kernels preserve denormals, so no other value
+// changes), then the sign flip -- five VALU instead of the zero test's selects
+__device__ __forceinline__ uint64_t f64_key_nn(double d) {
+    const double z = d + 0.0;
+    const uint64_t b = (uint64_t)__double_as_longlong(z);
+    const uint64_t m = (uint64_t)((int64_t)b >> 63);
+    return b ^ (m | 0x8000000000000000ull);
+}
 __host__ __device__ __forceinline__ double key_f64(uint64_t k) {
     uint64_t b = (k >> 63) ? (k & 0x7FFFFFFFFFFFFFFFull) : ~k;
     double d;
@@ -59,12 +68,14 @@ template <> struct Elem<double> {
     __device__ static double d(double v) { return v; }
     __device__ static int64_t i(double) { return 0; }
     __device__ static uint64_t key(double v) { return f64_key(v); }
+    __device__ static uint64_t key_nn(double v) { return f64_key_nn(v); }   // v not NaN
 };
 template <> struct Elem<float> {
     static constexpr bool is_float = true;
     __device__ static double d(float v) { return (double)v; }
     __device__ static int64_t i(float) { return 0; }
     __device__ static uint64_t key(float v) { return f64_key((double)v); }
+    __device__ static uint64_t key_nn(float v) { return f64_key_nn((double)v); }
 };
 #define SDP_INT_ELEM(T)                                                          \
     template <> struct Elem<T> {                                                 \
@@ -72,6 +83,7 @@ template <> struct Elem<float> {
         __device__ static double d(T v) { return (double)(int64_t)v; }           \
         __device__ static int64_t i(T v) { return (int64_t)v; }                  \
         __device__ static uint64_t key(T v) { return i64_key((int64_t)v); }      \
+        __device__ static uint64_t key_nn(T v) { return i64_key((int64_t)v); }   \
     };
 // 32-bit order-preserving keys of 4-byte types (pass 1's inclusive window
 // tests): key32 is monotone in the value and widen(key32) is the element's
@@ -83,6 +95,11 @@ template <> struct Key32<float> {
     __device__ static uint32_t key(float v) {            // v not NaN; -0.0 groups with 0.0
         const uint32_t b = v == 0.0f ? 0u : __float_as_uint(v);
         return (b >> 31) ? ~b : (b | 0x80000000u);
+    }
+    __device__ static uint32_t key_nn(float v) {         // key() by sign flip of v + 0.0f (-0.0 -> +0.0)
+        const uint32_t b = __float_as_uint(v + 0.0f);
+        const uint32_t m = (uint32_t)((int32_t)b >> 31);
+        return b ^ (m | 0x80000000u);
     }
     // 64-bit key of the element with key k; keys below -inf's / above +inf's
     // (NaN patterns, never a valid element's) map to 0 / UINT64_MAX so that the
@@ -101,12 +118,14 @@ template <> struct Key32<float> {
 template <> struct Key32<int32_t> {
     static constexpr bool ok = true;
     __device__ static uint32_t key(int32_t v) { return (uint32_t)v ^ 0x80000000u; }
+    __device__ static uint32_t key_nn(int32_t v) { return key(v); }
     __device__ static uint64_t widen(uint32_t k) { return i64_key((int64_t)(int32_t)(k ^ 0x80000000u)); }
     __device__ static uint64_t widen_valid(uint32_t k) { return widen(k); }
 };
 template <> struct Key32<uint32_t> {
     static constexpr bool ok = true;
     __device__ static uint32_t key(uint32_t v) { return v; }
+    __device__ static uint32_t key_nn(uint32_t v) { return v; }
     __device__ static uint64_t widen(uint32_t k) { return i64_key((int64_t)k); }
     __device__ static uint64_t widen_valid(uint32_t k) { return widen(k); }
 };

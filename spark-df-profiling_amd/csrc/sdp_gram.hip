@@ -18,6 +18,10 @@
 namespace sdp {
 
 typedef double d4 __attribute__((ext_vector_type(4)));
+// the LDS images' rows sit on 16-byte (not 32-byte) boundaries (pitches of
+// G16_P / GW_PITCH doubles): accessed through this 16-byte-aligned type, so no
+// access assumes d4's natural 32-byte alignment (ds_*_b128 pairs either way)
+typedef double d4u __attribute__((ext_vector_type(4), aligned(16)));
 
 constexpr int G_WAVES = 4;
 constexpr int G_BLOCK = G_WAVES * WAVE;
@@ -449,7 +453,7 @@ __device__ __forceinline__ void g16_stage(const GwRaw &x, uint32_t kb, double K,
 #pragma unroll
     for (int m = 0; m < 4; ++m) y[m] = ((kb >> m) & 1u) ? v[m] - K : 0.0;
     csum += (y[0] + y[1]) + (y[2] + y[3]);
-    *(d4 *)dst = d4{y[0], y[1], y[2], y[3]};
+    *(d4u *)dst = d4u{y[0], y[1], y[2], y[3]};
 }
 __device__ __forceinline__ void g16_stage_any(int dt, const GwRaw &x, uint32_t kb, double K, double &csum,
                                               double *dst) {
@@ -463,7 +467,7 @@ __device__ __forceinline__ void g16_stage_any(int dt, const GwRaw &x, uint32_t k
     case SDP_U16: g16_stage<SDP_U16>(x, kb, K, csum, dst); break;
     case SDP_I8: g16_stage<SDP_I8>(x, kb, K, csum, dst); break;
     case SDP_U8: g16_stage<SDP_U8>(x, kb, K, csum, dst); break;
-    default: *(d4 *)dst = d4{0.0, 0.0, 0.0, 0.0};    // padding column
+    default: *(d4u *)dst = d4u{0.0, 0.0, 0.0, 0.0};   // padding column
     }
 }
 
@@ -554,7 +558,7 @@ __global__ void __launch_bounds__(G16_BLOCK, 4 / G16_Q) gram16_kernel(const Gram
         // this wave's row groups wid + 4 g: MFMA m takes row 4q + m of the group
 #pragma unroll
         for (int g = 0; g < 4 * G16_QN; ++g) {
-            const d4 v = *(const d4 *)&s_y[cl * G16_P + 16 * (wid + G16_W * g) + 4 * q];
+            const d4u v = *(const d4u *)&s_y[cl * G16_P + 16 * (wid + G16_W * g) + 4 * q];
 #pragma unroll
             for (int m = 0; m < 4; ++m) acc = __builtin_amdgcn_mfma_f64_16x16x4f64(v[m], v[m], acc, 0, 0, 0);
         }
@@ -687,7 +691,7 @@ __device__ __forceinline__ void gram_wide_unit(int L, const GramCol *cols, int n
         for (int m = 0; m < 4; ++m) y[m] = ((kb >> m) & 1u) ? x[m] - sk[i] : 0.0;
         if (diag) csum[i] += (y[0] + y[1]) + (y[2] + y[3]);
         double *dst = (c < GW_TILE ? pa[buf] : pb[buf]) + (c & (GW_TILE - 1)) * GW_PITCH + 4 * squad;
-        *(d4 *)dst = d4{y[0], y[1], y[2], y[3]};
+        *(d4u *)dst = d4u{y[0], y[1], y[2], y[3]};
     };
     // MFMA operands of 4-row group kk out of buffer `buf`
     auto read_ops = [&](int buf, int kk, double (&va)[4], double (&vb)[4]) {

@@ -19,6 +19,12 @@ namespace sdp {
 constexpr int P1_BLOCK = 256;
 constexpr int P1_UNROLL = 2;          // 16-B vectors per thread per tile (x2: the next tile is prefetched)
 constexpr int P1_MAX_GRID = 1024;     // 4 blocks per CU on 256 CUs
+#ifndef P1_STAGES
+#define P1_STAGES 3                   // tiles of pass 1's whole-tile ring (2 in flight)
+#endif
+#ifndef P1_U32
+#define P1_U32 2                      // 16-byte vectors per thread per tile, 4-byte types
+#endif
 constexpr int SORT_MAX = 16384;       // one-workgroup LDS bitonic sort (128 KiB)
 
 #define SDP_DISPATCH_NUMERIC(DT, ...)                                             \
@@ -368,7 +374,8 @@ struct P1Partial {
 };
 
 struct P1Thread {
-    uint32_t count, n_valid, n_nan, n_zero, n_skip;
+    uint32_t count, n_valid, n_zero;
+    uint32_t ncalls;                  // p1_elem calls (wave-uniform): skipped = ncalls - count
     int64_t isum, imin, imax;
     double dmin, dmax;
     double s1, s1c, s2, s3, s3c, s4;
@@ -392,17 +399,22 @@ struct P1Ctx {
 // Window counts use the key with skipped elements (null, NaN, padding) mapped
 // to key 0: no skipped element is above a bound or strictly inside a window,
 // and the ones counted as equal to a bound of 0 are taken off in the block
-// epilogue (n_skip), as are eqhi counts of windows with lo == hi -- so each
-// window costs two compare-and-carry counts, one equality count and the
-// inside test, with no per-element validity masking.
+// epilogue (ncalls - count skipped elements), as are eqhi counts of windows
+// with lo == hi -- so each window costs two compare-and-carry counts, one
+// equality count and the inside test, with no per-element validity masking.
+// Per element only `count` is kept among the element counters: n_valid is
+// added per vector from its validity bits (p1_valid), NaNs are n_valid -
+// count and skipped elements ncalls - count (round 6: 64 -> ~40 VALU per f64
+// element).  The key of a kept element is built inside the `ok` branch from
+// a value with -0.0 turned into +0.0 by adding +0.0 (IEEE round-to-nearest;
+// denormals are preserved in these kernels), so it needs no zero test.
 template <typename T, bool WIN, bool INCL = false, bool K32 = false>
 __device__ __forceinline__ void p1_elem(P1Thread &st, const P1Ctx &cx, T x, bool valid) {
     const double xd = Elem<T>::d(x);
-    const bool isnan_ = Elem<T>::is_float && (xd != xd);
-    const bool ok = valid && !isnan_;
-    st.n_valid += valid;
-    st.n_nan += (valid && isnan_);
-    st.n_skip += !ok;
+    bool ok = valid;
+    if constexpr (Elem<T>::is_float) ok = valid && !(xd != xd);
+    uint64_t key = 0ull;
+    uint32_t k32 = 0u;
     if (ok) {
         st.count += 1;
         if (Elem<T>::is_float) {
@@ -425,27 +437,27 @@ __device__ __forceinline__ void p1_elem(P1Thread &st, const P1Ctx &cx, T x, bool
         st.s2 += d2;
         st.t3 = fma(d2, d, st.t3);
         st.s4 = fma(d2, d2, st.s4);
+        if constexpr (WIN) {
+            if constexpr (INCL && K32) k32 = Key32<T>::key_nn(x);
+            else key = Elem<T>::key_nn(x);
+        }
     }
     if (!WIN) return;                   // no quantile windows (date/timestamp min/max)
-    const uint64_t key = ok ? Elem<T>::key(x) : 0ull;
     if constexpr (INCL && K32) {
         // 4-byte types: the same inclusive test on 32-bit keys against bounds
         // mapped into the 32-bit key space (pass1_body; every lo32 > 0, so the
         // skipped elements' key 0 is below every window); a candidate is
-        // stored as its 64-bit key
-        const uint32_t k32 = ok ? Key32<T>::key(x) : 0u;
+        // stored as its 32-bit key (widened after the sweep)
 #pragma unroll
         for (int w = 0; w < SDP_MAX_WINDOWS; ++w) {
             const uint32_t lo = cx.lo32[w], hi = cx.hi32[w];
-            st.gt[w] += (uint32_t)(k32 < lo);
-            const bool ge = k32 >= lo, le = k32 <= hi;
-            const bool in = ge & le;
-            const uint64_t m = __builtin_amdgcn_ballot_w64(ge) & __builtin_amdgcn_ballot_w64(le);
+            const bool lt = k32 < lo, le = k32 <= hi;
+            st.gt[w] += (uint32_t)lt;
+            const uint64_t m = __builtin_amdgcn_ballot_w64(le) & ~__builtin_amdgcn_ballot_w64(lt);
             if (m) {
                 const uint32_t c = st.wcur[w];
                 const uint32_t pos = c + (uint32_t)lane_rank(m);
-                // the 32-bit key; pass1_sweep widens the wave's slots after its sweep
-                if (in && (int64_t)pos < cx.cap) cx.seg[w][pos] = (uint64_t)k32;
+                if (le && !lt && (int64_t)pos < cx.cap) cx.seg[w][pos] = (uint64_t)k32;
                 st.wcur[w] = c + (uint32_t)__popcll(m);
             }
         }
@@ -454,22 +466,20 @@ __device__ __forceinline__ void p1_elem(P1Thread &st, const P1Ctx &cx, T x, bool
     if constexpr (INCL) {
         // Inclusive windows (every bound key rare in the sample, lo > 0): one
         // count #(key < lo) -- held in gt[] and turned into #(key > hi) in the
-        // epilogue -- and candidates lo <= key <= hi: 2 compares fewer per
-        // window than the exclusive form below.  Skipped elements (key 0) are
-        // below every lo; unused windows have lo > hi (never inside).
+        // epilogue -- and candidates lo <= key <= hi, from the same two
+        // compares (the inside mask is ballot(le) & ~ballot(lt): three VALU per
+        // window).  Skipped elements (key 0) are below every lo; unused
+        // windows have lo > hi (never inside).
 #pragma unroll
         for (int w = 0; w < SDP_MAX_WINDOWS; ++w) {
             const uint64_t lo = cx.lo[w], hi = cx.hi[w];
-            st.gt[w] += (uint32_t)(key < lo);
-            // the lane's own compare result is both the ballot and the store's
-            // exec mask (no lane-bit test of the ballot)
-            const bool ge = key >= lo, le = key <= hi;
-            const bool in = ge & le;
-            const uint64_t m = __builtin_amdgcn_ballot_w64(ge) & __builtin_amdgcn_ballot_w64(le);
+            const bool lt = key < lo, le = key <= hi;
+            st.gt[w] += (uint32_t)lt;
+            const uint64_t m = __builtin_amdgcn_ballot_w64(le) & ~__builtin_amdgcn_ballot_w64(lt);
             if (m) {
                 const uint32_t c = st.wcur[w];
                 const uint32_t pos = c + (uint32_t)lane_rank(m);
-                if (in && (int64_t)pos < cx.cap) cx.seg[w][pos] = key;
+                if (le && !lt && (int64_t)pos < cx.cap) cx.seg[w][pos] = key;
                 st.wcur[w] = c + (uint32_t)__popcll(m);
             }
         }
@@ -512,7 +522,7 @@ __device__ __forceinline__ void pass1_sweep(P1Thread &st, const P1Ctx &cx, const
     const int64_t nvec = n / VPT;
     const Vec16<T> *vals = (const Vec16<T> *)col.d_values;
     // 8-byte types: 2 vectors per tile; narrower ones 1 (4-16 elements already)
-    constexpr int U = sizeof(T) >= 8 ? P1_UNROLL : 1;
+    constexpr int U = sizeof(T) >= 8 ? P1_UNROLL : sizeof(T) == 4 ? P1_U32 : 1;
     const int64_t tile_vecs = (int64_t)P1_BLOCK * U;
     const int64_t ntiles = (nvec + tile_vecs - 1) / tile_vecs;
     // ping-pong tiles: tile i + 1 is loading while tile i is worked on
@@ -526,12 +536,80 @@ __device__ __forceinline__ void pass1_sweep(P1Thread &st, const P1Ctx &cx, const
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             const uint32_t vbits = x[u].bits(vbm);
+            st.n_valid += (uint32_t)__popc(vbits);
+            st.ncalls += VPT;
 #pragma unroll
             for (int e = 0; e < VPT; ++e) p1_elem<T, WIN, INCL, K32>(st, cx, x[u].v.v[e], (vbits >> e) & 1u);
         }
         p1_fold(st);
     };
+    // Whole tiles of a column without a bitmap or with a bitmap starting on a
+    // 32-bit word (the common case, workgroup-uniform test): loads from a
+    // tile base in scalar registers plus a per-lane constant, no clamping, and
+    // ONE validity dword per vector, whose word and shift are per-lane
+    // constants (a tile covers a multiple of 32 rows).  The general path below
+    // (clamped vectors, two validity dwords and an alignbit per vector) takes
+    // the last, partial tile and unaligned bitmaps.
+    const bool fast = vbm.none || (vbm.bit0 & 31) == 0;
+    const int64_t nfull = fast ? nvec / tile_vecs : 0;
     int64_t tile = bx;
+    if (tile < nfull) {
+        typedef uint32_t u32x4g __attribute__((ext_vector_type(4)));
+        typedef const __attribute__((address_space(1))) u32x4g gvec;
+        typedef const __attribute__((address_space(1))) uint32_t gword;
+        const int t = threadIdx.x;
+        const uint32_t lsh = (uint32_t)(t * VPT) & 31u;                      // this lane's first bit in its word
+        const int64_t w0 = vbm.bit0 >> 5;
+        struct FIn {
+            Vec16<T> v[U];
+            uint32_t w[U];
+        };
+        auto loadf = [&](FIn &x, int64_t tl) {
+            const int64_t vb = tl * tile_vecs;                                // wave-uniform
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const u32x4g raw = ((gvec *)(vals + vb + (int64_t)u * P1_BLOCK))[t];
+                __builtin_memcpy(&x.v[u], &raw, 16);
+                x.w[u] = vbm.none ? 0xFFFFFFFFu
+                                  : ((gword *)vbm.base + w0 + (((vb + (int64_t)u * P1_BLOCK) * VPT) >> 5))[(t * VPT) >> 5];
+            }
+        };
+        auto workf = [&](const FIn &x) {
+            constexpr uint32_t full = VPT >= 32 ? 0xFFFFFFFFu : ((1u << VPT) - 1u);
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const uint32_t vbits = (x.w[u] >> lsh) & full;
+                st.n_valid += (uint32_t)__popc(vbits);
+                st.ncalls += VPT;
+#pragma unroll
+                for (int e = 0; e < VPT; ++e) p1_elem<T, WIN, INCL, K32>(st, cx, x.v[u].v[e], (vbits >> e) & 1u);
+            }
+            p1_fold(st);
+        };
+        // a ring of P1_STAGES tiles: P1_STAGES - 1 in flight while one is
+        // worked on (ping-pong kept ~32 KB per CU in flight, latency-bound;
+        // an HBM miss wants ~72 KB, MI355X_MICROARCH.md)
+        constexpr int S = INCL ? P1_STAGES : 2;       // (the exclusive-window counters leave no room for a third tile)
+        FIn r[S];
+        const int64_t last = nfull - 1;
+        auto clampt = [&](int64_t x) { return x <= last ? x : last; };   // past the last whole tile: re-read it
+#pragma unroll
+        for (int k = 0; k < S - 1; ++k) loadf(r[k], clampt(tile + (int64_t)k * G));
+        bool go = true;
+        while (go) {
+#pragma unroll
+            for (int k = 0; k < S; ++k) {
+                if (go) {
+                    loadf(r[(k + S - 1) % S], clampt(tile + (int64_t)(S - 1) * G));
+                    workf(r[k]);
+                    tile += G;
+                    go = tile < nfull;
+                }
+            }
+        }
+    }
+    // the general path: every tile (fast == false) or the partial last one
+    tile = fast ? (nfull < ntiles && bx == (int)(nfull % G) ? nfull : ntiles) : bx;
     if (tile < ntiles) {
         load(ta, tile);
         while (true) {
@@ -551,6 +629,8 @@ __device__ __forceinline__ void pass1_sweep(P1Thread &st, const P1Ctx &cx, const
         const bool inb = i < n;
         T x = inb ? ((const T *)col.d_values)[i] : (T)0;
         const bool valid = inb && valid_bit(col.d_validity, col.validity_bit_offset, i);
+        st.n_valid += valid;
+        st.ncalls += 1;
         p1_elem<T, WIN, INCL, K32>(st, cx, x, valid);
         p1_fold(st);
     }
@@ -620,7 +700,7 @@ __device__ __forceinline__ void pass1_body(const sdp_column &col, const sdp_qpla
     }
 
     P1Thread st;
-    st.count = st.n_valid = st.n_nan = st.n_zero = st.n_skip = 0;
+    st.count = st.n_valid = st.n_zero = st.ncalls = 0;
     st.isum = 0;
     st.imin = INT64_MAX;
     st.imax = INT64_MIN;
@@ -651,14 +731,14 @@ __device__ __forceinline__ void pass1_body(const sdp_column &col, const sdp_qpla
         const double dmn = wave_min_f64(st.dmin), dmx = wave_max_f64(st.dmax);
         const int64_t isum = wave_sum_i64(st.isum), imn = wave_min_i64(st.imin), imx = wave_max_i64(st.imax);
         const uint64_t c0 = wave_sum_u64(st.count), c1 = wave_sum_u64(st.n_valid);
-        const uint64_t c2 = wave_sum_u64(st.n_nan), c3 = wave_sum_u64(st.n_zero);
+        const uint64_t c2 = Elem<T>::is_float ? c1 - c0 : 0ull, c3 = wave_sum_u64(st.n_zero);
         if (lane == 0) {
             s_d[wid][0] = h; s_d[wid][1] = l; s_d[wid][2] = s2; s_d[wid][3] = h3;
             s_d[wid][4] = l3; s_d[wid][5] = s4; s_d[wid][6] = dmn; s_d[wid][7] = dmx;
             s_i[wid][0] = isum; s_i[wid][1] = imn; s_i[wid][2] = imx;
             s_u[wid][0] = c0; s_u[wid][1] = c1; s_u[wid][2] = c2; s_u[wid][3] = c3;
         }
-        const uint64_t skip = wave_sum_u64(st.n_skip);
+        const uint64_t skip = wave_sum_u64(st.ncalls) - c0;
 #pragma unroll
         for (int w = 0; w < W_; ++w) {
             uint64_t g = wave_sum_u64(st.gt[w]);

@@ -515,8 +515,10 @@ def describe(df, bins=10, corr_reject=0.9, **kwargs):
     images = {name: (fut.result() if hasattr(fut, 'result') else fut) for name, fut in pending.items()}
     if plots and sharded:
         # one exchange of the rendered strings (~28 KB per NUM column),
-        # in one round: the cap every rank derives from the same column count
-        for part in engine.comm.allgather_object(images, cap=IMAGE_CAP_PER_COLUMN * len(table.columns)):
+        # in one round: the cap every rank derives from the same count of
+        # plotted (NUM) columns -- the types come from global statistics
+        n_plot = sum(1 for d in ldesc.values() if d['type'] == 'NUM')
+        for part in engine.comm.allgather_object(images, cap=IMAGE_CAP_PER_COLUMN * max(1, n_plot)):
             images.update(part)
     for name, (hist, mini) in images.items():
         ldesc[name]['histogram'], ldesc[name]['mini_histogram'] = hist, mini

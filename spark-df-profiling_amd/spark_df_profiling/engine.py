@@ -68,9 +68,12 @@ BITS32 = os.environ.get('SDP_BITS32', '1') != '0'
 # SDP_PASS2_BATCH=0: one sdp_pass2_count launch per column on wide tables too
 PASS2_BATCH = os.environ.get('SDP_PASS2_BATCH', '1') != '0'
 # level 2 into blocks, one workgroup per level-1 bucket, no count pass
-# (sdp_part_l2_blocks, round 6); SDP_L2_BLOCKS=0: the counted exact-offset
-# level 2 (sdp_part_recs phase 0 + 1) for A/B runs
-L2_BLOCKS = os.environ.get('SDP_L2_BLOCKS', '1') != '0'
+# (sdp_part_l2_blocks, round 6).  OFF by default: the C5 describe (512 fused
+# columns) and the two-rank sharded describe hit an illegal memory access on
+# the GPU with it (gpurun_out r06b); the counted exact-offset
+# level 2 (sdp_part_recs phase 0 + 1) is the shipped path.  SDP_L2_BLOCKS=1
+# only for debugging it (tools/debug_bounds.sh).
+L2_BLOCKS = os.environ.get('SDP_L2_BLOCKS', '0') == '1'
 L2_BLOCK = nat.L2_BLOCK
 DEBUG_BOUNDS = os.environ.get('SDP_DEBUG_BOUNDS', '') == '1'      # a tools/debug_bounds.sh library is loaded
 CAND_FULL_BUDGET = 1 << 30   # bytes of room-for-every-row candidate slots per pass-1 batch
@@ -220,8 +223,11 @@ class Engine:
         return cls.from_buffer_copy(b)
 
     def _to_dev(self, struct):
-        raw = bytes(struct)
-        return to_dev(np.frombuffer(bytearray(raw), dtype=np.uint8), torch.uint8, self.device)
+        # (through _h2d: on self.stream, ahead of the kernels that read the
+        # table there; comm.to_dev stays for tensors torch ops consume on the
+        # current stream)
+        return self._h2d(np.frombuffer(bytearray(bytes(struct)), dtype=np.uint8))
+
 
     def _h2d(self, arr):
         """Host numpy array -> device tensor without a host round trip: staged
@@ -2695,7 +2701,7 @@ class Engine:
         keep = torch.empty((n + 31) // 32 + 1, dtype=torch.int32, device=self.device)
         nat.annotate('', sum(n / 8.0 for c in cols if c.validity is not None))
         sdp.sdp_rowmask(arr, cn, C, ptr(work), work.numel(), ptr(keep), self._s())
-        sh = to_dev([float(x) for x in shifts], torch.float64, self.device)
+        sh = self._h2d(np.array([float(x) for x in shifts], dtype=np.float64))   # (on self.stream, before sdp_gram)
         G = torch.empty(C * C, dtype=torch.float64, device=self.device)
         s = torch.empty(C, dtype=torch.float64, device=self.device)
         nn = torch.empty(1, dtype=torch.float64, device=self.device)

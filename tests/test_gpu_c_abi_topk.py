@@ -75,6 +75,21 @@ def test_topk_more_than_256_heavy_string_keys():
     assert [(vals[r], c) for r, c in got] == want
 
 
+def test_topk_small_column_heavy_keys_capped_to_row_kernels():
+    # a few thousand rows (b1 == 0: the row kernels, whose heavy tables hold
+    # SDP_HEAVY_MAX keys) with 400 labels seen >= 3 times in the whole-column
+    # sample: sdp_api.cpp's cap_to trims the heavy keys to 256, the rest
+    # become partition records; groups, rows and top-k as Counter says
+    g = datagen.rng(34)
+    vals = ['H%03d' % i for i in range(400)] * 10 + ['s%d' % i for i in range(600)]
+    vals = [vals[i] for i in g.permutation(len(vals))]
+    assert sum(1 for c in Counter(vals).values() if c >= 3) > 256
+    res, got = _topk(pa.array(vals, type=pa.large_string()), 50)
+    want, groups = _want(vals, 50)
+    assert (res.groups, res.rows) == (groups, len(vals))
+    assert [(vals[r], c) for r, c in got] == want
+
+
 def test_topk_fixed_ties_beyond_gsort_max():
     g = datagen.rng(32)
     tied = _distinct_ints(g, -10 ** 9, 10 ** 9, 20_000)

@@ -15,9 +15,10 @@ for k, c in sorted(v.items()):
     if 'SQ_WAIT_ANY' in c:
         wc = c['SQ_WAVE_CYCLES'] or 1
         print('%-64s wave_cyc %.3g busy %.3g wait_any %.2f wait_inst %.2f active %.2f valu %.2f lds %.2f '
-              'bankconf/lds %.2f' % (k, wc, c['SQ_BUSY_CYCLES'], c['SQ_WAIT_ANY'] / wc, c['SQ_WAIT_INST_ANY'] / wc,
-                                     c['SQ_ACTIVE_INST_ANY'] / wc, c['SQ_ACTIVE_INST_VALU'] / wc,
-                                     c['SQ_ACTIVE_INST_LDS'] / wc,
-                                     c['SQ_LDS_BANK_CONFLICT'] / max(1, c['SQ_ACTIVE_INST_LDS'])))
+              'sca %.2f bankconf/lds %.2f' % (k, wc, c['SQ_BUSY_CYCLES'], c['SQ_WAIT_ANY'] / wc,
+                                              c['SQ_WAIT_INST_ANY'] / wc, c['SQ_ACTIVE_INST_ANY'] / wc,
+                                              c['SQ_ACTIVE_INST_VALU'] / wc, c['SQ_ACTIVE_INST_LDS'] / wc,
+                                              c.get('SQ_ACTIVE_INST_SCA', 0) / wc,
+                                              c.get('SQ_LDS_BANK_CONFLICT', 0) / max(1, c['SQ_ACTIVE_INST_LDS'])))
     else:
         print('%-64s %s' % (k, '  '.join('%s %.4g' % (n.replace('SQ_', '').lower(), x) for n, x in sorted(c.items()))))
