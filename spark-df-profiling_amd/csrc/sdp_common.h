@@ -222,6 +222,14 @@ struct VecIn {
         const uint32_t x = vb.none ? full : (__builtin_amdgcn_alignbit(w1, w0, sh) & full);
         return in ? x : 0u;
     }
+    // bits() without a branch on vb.none (a branch between a load and its use
+    // made the compiler wait vmcnt(0) there, draining the prefetched next
+    // tile; pass 1 -- in pass 2 the extra live words spilled)
+    __device__ __forceinline__ uint32_t bits_nb(const VBits &vb) const {
+        constexpr uint32_t full = VPT >= 32 ? 0xFFFFFFFFu : ((1u << VPT) - 1u);
+        const uint32_t x = (__builtin_amdgcn_alignbit(w1, w0, sh) | (vb.none ? 0xFFFFFFFFu : 0u)) & full;
+        return in ? x : 0u;
+    }
 };
 
 __device__ __forceinline__ bool valid_bit(const uint8_t *bm, int64_t bitoff, int64_t idx) {
@@ -290,6 +298,17 @@ __device__ __forceinline__ int64_t wave_sum_i64(int64_t v) {
 
 __device__ __forceinline__ int lane_id() { return threadIdx.x & (WAVE - 1); }
 
+// Wave-uniform copies of lane values (lane 0's / the first active lane's).
+// __builtin_amdgcn_readfirstlane returns int: widened straight to 64 bits it
+// sign-extends, so a word >= 2^31 turned a rebuilt 64-bit pointer into garbage
+// (the round-6 illegal accesses of the block-layout dedup and of pass 1's
+// candidate slots).  Every use goes through these helpers
+// (tests/test_sources_cpu.py checks that).
+__device__ __forceinline__ uint32_t uniform_u32(uint32_t v) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)v); }
+__device__ __forceinline__ uint64_t uniform_u64(uint64_t v) {
+    return ((uint64_t)uniform_u32((uint32_t)(v >> 32)) << 32) | (uint64_t)uniform_u32((uint32_t)v);
+}
+template <typename P> __device__ __forceinline__ P *uniform_ptr(P *p) { return (P *)uniform_u64((uint64_t)p); }
 // Workgroup barrier for LDS hand-offs only.  __syncthreads() carries a
 // workgroup release/acquire fence, which drains vmcnt: every global load still
 // in flight (a prefetched next tile) would be waited for at the barrier.  This

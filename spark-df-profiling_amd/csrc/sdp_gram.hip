@@ -477,7 +477,7 @@ __global__ void __launch_bounds__(G16_BLOCK, 4 / G16_Q) gram16_kernel(const Gram
     __shared__ double s_y[16 * G16_P];
     const int s = blockIdx.x;
     const int lane = lane_id();
-    const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x / WAVE);
+    const int wid = (int)uniform_u32(threadIdx.x / WAVE);
     const int q = lane >> 4, cl = lane & 15;
     const int64_t c0 = (int64_t)s * rows_per_chunk;
     const int64_t c1 = min(n, c0 + rows_per_chunk);
@@ -608,7 +608,7 @@ __device__ __forceinline__ void gram_wide_unit(int L, const GramCol *cols, int n
     const int tj = ti + rem;
     constexpr bool diag = DIAG;
     const int tid = threadIdx.x, lane = lane_id();
-    const int wid = __builtin_amdgcn_readfirstlane(tid / WAVE);
+    const int wid = (int)uniform_u32(tid / WAVE);
     const int q = lane >> 4, cl = lane & 15;
     const int qa = wid >> 2, qb = wid & 3;
     constexpr int NSLOT = DIAG ? GW_SLOTS / 2 : GW_SLOTS;    // diagonal tiles stage panel A only

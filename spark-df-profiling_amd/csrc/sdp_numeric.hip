@@ -408,6 +408,13 @@ struct P1Ctx {
 // element).  The key of a kept element is built inside the `ok` branch from
 // a value with -0.0 turned into +0.0 by adding +0.0 (IEEE round-to-nearest;
 // denormals are preserved in these kernels), so it needs no zero test.
+// A candidate store through the global address space: a flat store (the
+// slot pointers come from a task table, so they are generic) is unordered
+// against the loads on vmcnt, and one in flight made the compiler wait
+// vmcnt(0) -- draining the prefetched tiles -- before every use of a tile.
+__device__ __forceinline__ void gstore(uint64_t *p, uint32_t i, uint64_t v) {
+    ((__attribute__((address_space(1))) uint64_t *)p)[i] = v;
+}
 template <typename T, bool WIN, bool INCL = false, bool K32 = false>
 __device__ __forceinline__ void p1_elem(P1Thread &st, const P1Ctx &cx, T x, bool valid) {
     const double xd = Elem<T>::d(x);
@@ -437,12 +444,15 @@ __device__ __forceinline__ void p1_elem(P1Thread &st, const P1Ctx &cx, T x, bool
         st.s2 += d2;
         st.t3 = fma(d2, d, st.t3);
         st.s4 = fma(d2, d2, st.s4);
-        if constexpr (WIN) {
-            if constexpr (INCL && K32) k32 = Key32<T>::key_nn(x);
+        if constexpr (WIN && INCL) {
+            if constexpr (K32) k32 = Key32<T>::key_nn(x);
             else key = Elem<T>::key_nn(x);
         }
     }
     if (!WIN) return;                   // no quantile windows (date/timestamp min/max)
+    // (exclusive windows: the key after the branch -- built inside it, it
+    // stayed live beside the moments and spilled the window counters)
+    if constexpr (!INCL) key = ok ? Elem<T>::key(x) : 0ull;
     if constexpr (INCL && K32) {
         // 4-byte types: the same inclusive test on 32-bit keys against bounds
         // mapped into the 32-bit key space (pass1_body; every lo32 > 0, so the
@@ -457,7 +467,7 @@ __device__ __forceinline__ void p1_elem(P1Thread &st, const P1Ctx &cx, T x, bool
             if (m) {
                 const uint32_t c = st.wcur[w];
                 const uint32_t pos = c + (uint32_t)lane_rank(m);
-                if (le && !lt && (int64_t)pos < cx.cap) cx.seg[w][pos] = (uint64_t)k32;
+                if (le && !lt && (int64_t)pos < cx.cap) gstore(cx.seg[w], pos, (uint64_t)k32);
                 st.wcur[w] = c + (uint32_t)__popcll(m);
             }
         }
@@ -479,7 +489,7 @@ __device__ __forceinline__ void p1_elem(P1Thread &st, const P1Ctx &cx, T x, bool
             if (m) {
                 const uint32_t c = st.wcur[w];
                 const uint32_t pos = c + (uint32_t)lane_rank(m);
-                if (le && !lt && (int64_t)pos < cx.cap) cx.seg[w][pos] = key;
+                if (le && !lt && (int64_t)pos < cx.cap) gstore(cx.seg[w], pos, key);
                 st.wcur[w] = c + (uint32_t)__popcll(m);
             }
         }
@@ -500,7 +510,7 @@ __device__ __forceinline__ void p1_elem(P1Thread &st, const P1Ctx &cx, T x, bool
         if (m) {   // wave-uniform; no atomics: this wave owns its slot range
             const uint32_t c = st.wcur[w];
             const uint32_t pos = c + (uint32_t)lane_rank(m);
-            if (in && (int64_t)pos < cx.cap) cx.seg[w][pos] = key;
+            if (in && (int64_t)pos < cx.cap) gstore(cx.seg[w], pos, key);
             st.wcur[w] = c + (uint32_t)__popcll(m);
         }
     }
@@ -535,7 +545,7 @@ __device__ __forceinline__ void pass1_sweep(P1Thread &st, const P1Ctx &cx, const
     auto work = [&](const VecIn<T> (&x)[U]) {
 #pragma unroll
         for (int u = 0; u < U; ++u) {
-            const uint32_t vbits = x[u].bits(vbm);
+            const uint32_t vbits = x[u].bits_nb(vbm);
             st.n_valid += (uint32_t)__popc(vbits);
             st.ncalls += VPT;
 #pragma unroll
@@ -550,16 +560,20 @@ __device__ __forceinline__ void pass1_sweep(P1Thread &st, const P1Ctx &cx, const
     // constants (a tile covers a multiple of 32 rows).  The general path below
     // (clamped vectors, two validity dwords and an alignbit per vector) takes
     // the last, partial tile and unaligned bitmaps.
-    const bool fast = vbm.none || (vbm.bit0 & 31) == 0;
+    // (exclusive windows keep the general path: their counters leave no
+    // registers for the whole-tile loop, which spilled them -- 5.9 -> 9.4 ms
+    // for C3's int64 columns, profiles/r06e_kernel_stats.csv)
+    const bool fast = INCL && (vbm.none || (vbm.bit0 & 31) == 0);
     const int64_t nfull = fast ? nvec / tile_vecs : 0;
     int64_t tile = bx;
-    if (tile < nfull) {
+    if constexpr (INCL) if (tile < nfull) {
         typedef uint32_t u32x4g __attribute__((ext_vector_type(4)));
         typedef const __attribute__((address_space(1))) u32x4g gvec;
         typedef const __attribute__((address_space(1))) uint32_t gword;
         const int t = threadIdx.x;
         const uint32_t lsh = (uint32_t)(t * VPT) & 31u;                      // this lane's first bit in its word
         const int64_t w0 = vbm.bit0 >> 5;
+        const uint32_t wnone = vbm.none ? 0xFFFFFFFFu : 0u;
         struct FIn {
             Vec16<T> v[U];
             uint32_t w[U];
@@ -570,8 +584,10 @@ __device__ __forceinline__ void pass1_sweep(P1Thread &st, const P1Ctx &cx, const
             for (int u = 0; u < U; ++u) {
                 const u32x4g raw = ((gvec *)(vals + vb + (int64_t)u * P1_BLOCK))[t];
                 __builtin_memcpy(&x.v[u], &raw, 16);
-                x.w[u] = vbm.none ? 0xFFFFFFFFu
-                                  : ((gword *)vbm.base + w0 + (((vb + (int64_t)u * P1_BLOCK) * VPT) >> 5))[(t * VPT) >> 5];
+                // (loaded either way -- without a bitmap from the values, which
+                // are longer -- and OR-ed with all ones: a load under a branch
+                // made the compiler drain the ring with vmcnt(0))
+                x.w[u] = ((gword *)vbm.base + w0 + (((vb + (int64_t)u * P1_BLOCK) * VPT) >> 5))[(t * VPT) >> 5] | wnone;
             }
         };
         auto workf = [&](const FIn &x) {
@@ -661,7 +677,10 @@ __device__ __forceinline__ void pass1_body(const sdp_column &col, const sdp_qpla
         cx.lo[w] = w < cx.nw ? plan->lo[w] : EMPTY64;
         cx.hi[w] = w < cx.nw ? plan->hi[w] : (INCL ? EMPTY64 - 1 : EMPTY64);
         const int64_t seg = ((int64_t)w * G + bx) * P1_WPB + (threadIdx.x / WAVE);
-        cx.seg[w] = cand + seg * cap;
+        // (wave-uniform: held in scalar registers -- as lane values these ten
+        // VGPRs spilled the exclusive-window kernels, whose reloads then put a
+        // full vmcnt(0) drain into every element)
+        cx.seg[w] = uniform_ptr(cand + seg * cap);
     }
     cx.K = plan->shift;
     cx.cap = cap;

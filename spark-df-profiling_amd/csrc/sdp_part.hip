@@ -1018,8 +1018,8 @@ __global__ void __launch_bounds__(ST) part_scatter_recs_kernel(const uint64_t *i
     // chunk headers are wave-uniform: kept in scalar registers
     auto uniform_chunk = [](const Chunk &x) {
         auto u = [](int64_t v) {
-            const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v);
-            const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)((uint64_t)v >> 32));
+            const uint32_t lo = uniform_u32((uint32_t)v);
+            const uint32_t hi = uniform_u32((uint32_t)((uint64_t)v >> 32));
             return (int64_t)(((uint64_t)hi << 32) | lo);
         };
         return Chunk{u(x.start), u(x.end), u(x.hbase), u(x.hstride)};
@@ -1140,8 +1140,8 @@ __global__ void __launch_bounds__(ST) part_scatter_recs_wc_kernel(const uint64_t
     };
     auto uniform_chunk = [](const Chunk &x) {
         auto u = [](int64_t v) {
-            const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v);
-            const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)((uint64_t)v >> 32));
+            const uint32_t lo = uniform_u32((uint32_t)v);
+            const uint32_t hi = uniform_u32((uint32_t)((uint64_t)v >> 32));
             return (int64_t)(((uint64_t)hi << 32) | lo);
         };
         return Chunk{u(x.start), u(x.end), u(x.hbase), u(x.hstride)};
@@ -1296,8 +1296,8 @@ __global__ void __launch_bounds__(ST) part_l2_blocks_kernel(const uint64_t *in_k
     };
     auto uniform_seg = [](const Chunk &x) {
         auto u = [](int64_t v) {
-            const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v);
-            const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)((uint64_t)v >> 32));
+            const uint32_t lo = uniform_u32((uint32_t)v);
+            const uint32_t hi = uniform_u32((uint32_t)((uint64_t)v >> 32));
             return (int64_t)(((uint64_t)hi << 32) | lo);
         };
         return Chunk{u(x.start), u(x.end), u(x.hbase), u(x.hstride)};
@@ -1491,7 +1491,7 @@ struct Bkt {
     __device__ __forceinline__ int64_t at(int64_t i) const {
         if constexpr (BLK) {
             const bool inrun = (uint64_t)i < d.w;
-            const uint32_t ob = __builtin_amdgcn_readfirstlane(inrun ? 0u : (uint32_t)((i - d.w) / L2B));
+            const uint32_t ob = uniform_u32(inrun ? 0u : (uint32_t)((i - d.w) / L2B));
             const uint32_t b = sload(blist, DBG_BLK(d.y + ob, 5));
             return DBG_REC(inrun ? (int64_t)(r0() + (uint64_t)i) : (int64_t)b * L2B + (i % L2B), 1);
         } else {
@@ -1520,8 +1520,7 @@ struct Bkt {
     __device__ __forceinline__ const uint64_t *wave_base_inl(const uint64_t *p, int64_t rb, int q) const {
         if constexpr (BLK) {
             const uint64_t a = (uint64_t)(p + DBG_REC(r0() + rb + (int64_t)q * WAVE, 4));
-            return (const uint64_t *)(((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(a >> 32)) << 32) |
-                                      __builtin_amdgcn_readfirstlane((uint32_t)a));
+            return (const uint64_t *)uniform_u64(a);
         } else {
             return p + rb + (int64_t)q * WAVE;
         }
@@ -1847,7 +1846,7 @@ __global__ void __launch_bounds__(WV_W * WAVE) part_dedup_u64_wave2_kernel(const
     uint64_t groups = 0;
     bool full = false;
     const int64_t stride = (int64_t)gridDim.x * WV_W;
-    int64_t f = (int64_t)__builtin_amdgcn_readfirstlane((int)(blockIdx.x * WV_W + w));
+    int64_t f = (int64_t)uniform_u32(blockIdx.x * WV_W + w);
     int64_t lo = 0, hi = 0;
     Bkt<BLK> ra, ra_n, ra_n2;                  // buckets f, f + stride (records prefetched), f + 2 stride
     uint64_t hq[WV_Q];
@@ -2038,7 +2037,7 @@ __global__ void __launch_bounds__(WV_W * WAVE, 4) part_dedup_u64_half_kernel(con
     const int64_t stride = (int64_t)gridDim.x * WV_W;
     Bkt<BLK> ra_n;                             // the next bucket's range / descriptor, one bucket ahead
     // (blocks: the bucket index in a scalar register, so are the descriptor addresses)
-    const int64_t f0 = BLK ? (int64_t)__builtin_amdgcn_readfirstlane((int)(blockIdx.x * WV_W + w))
+    const int64_t f0 = BLK ? (int64_t)uniform_u32(blockIdx.x * WV_W + w)
                            : (int64_t)blockIdx.x * WV_W + w;
     if (f0 < nbuckets) ra_n = bucket_load<BLK>(starts, ba, f0);
     for (int64_t f = f0; f < nbuckets; f += stride) {
