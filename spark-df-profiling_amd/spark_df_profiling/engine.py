@@ -68,12 +68,11 @@ BITS32 = os.environ.get('SDP_BITS32', '1') != '0'
 # SDP_PASS2_BATCH=0: one sdp_pass2_count launch per column on wide tables too
 PASS2_BATCH = os.environ.get('SDP_PASS2_BATCH', '1') != '0'
 # level 2 into blocks, one workgroup per level-1 bucket, no count pass
-# (sdp_part_l2_blocks, round 6).  OFF by default: the C5 describe (512 fused
-# columns) and the two-rank sharded describe hit an illegal memory access on
-# the GPU with it (gpurun_out r06b); the counted exact-offset
-# level 2 (sdp_part_recs phase 0 + 1) is the shipped path.  SDP_L2_BLOCKS=1
-# only for debugging it (tools/debug_bounds.sh).
-L2_BLOCKS = os.environ.get('SDP_L2_BLOCKS', '0') == '1'
+# (sdp_part_l2_blocks, round 6; its illegal accesses in r06b were a
+# sign-extended readfirstlane pointer, fixed in sdp_common.h's uniform_u64;
+# bounds-checked build clean, profiles/r06h_*).  SDP_L2_BLOCKS=0: the counted
+# exact-offset level 2 (sdp_part_recs phase 0 + 1) for A/B runs
+L2_BLOCKS = os.environ.get('SDP_L2_BLOCKS', '1') != '0'
 L2_BLOCK = nat.L2_BLOCK
 DEBUG_BOUNDS = os.environ.get('SDP_DEBUG_BOUNDS', '') == '1'      # a tools/debug_bounds.sh library is loaded
 CAND_FULL_BUDGET = 1 << 30   # bytes of room-for-every-row candidate slots per pass-1 batch
