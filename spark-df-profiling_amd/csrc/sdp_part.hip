@@ -1718,8 +1718,9 @@ __device__ __forceinline__ void wave_load_batch(uint64_t (&hq)[WV_Q], const uint
     // values out of the bucket loop)
     const int64_t rem = hi - rb - lane;
     if (ra.inline_batch(rb, WV_Q, hi)) {
+        const uint64_t *base = ra.wave_base_inl(in_h, rb, 0);      // (one scalar base: wave_load_batch16)
 #pragma unroll
-        for (int q = 0; q < WV_Q; ++q) hq[q] = (int64_t)q * WAVE < rem ? ra.wave_base_inl(in_h, rb, q)[lane] : EMPTY64;
+        for (int q = 0; q < WV_Q; ++q) hq[q] = (int64_t)q * WAVE < rem ? base[q * WAVE + lane] : EMPTY64;
         return;
     }
 #pragma unroll
@@ -1931,8 +1932,12 @@ __device__ __forceinline__ void wave_load_batch16(uint64_t (&hq)[WH_Q], const ui
     // values out of the bucket loop)
     const int64_t rem = hi - rb - lane;
     if (ra.inline_batch(rb, WH_Q, hi)) {
+        // the contiguous form's loads from the run's first record (scalar
+        // per-q pointers, 16 of them held across the bucket, spilled the block
+        // kernel: profiles/r06k_*, r06l_*)
+        const uint64_t *p = in_h + (BLK ? ra.r0() : 0);
 #pragma unroll
-        for (int q = 0; q < WH_Q; ++q) hq[q] = (int64_t)q * WAVE < rem ? ra.wave_base_inl(in_h, rb, q)[lane] : EMPTY64;
+        for (int q = 0; q < WH_Q; ++q) hq[q] = (int64_t)q * WAVE < rem ? p[rb + (int64_t)q * WAVE + lane] : EMPTY64;
         return;
     }
 #pragma unroll
