@@ -319,13 +319,17 @@ def label_kernels(label):
         st = 'count' if stage == 'count' else 'scatter'
         if dt == 'bytes':
             return ['sdp::part_%s_rows_bytes_kernel' % st]
-        # the scatter also carries its write-combining switch: <T, true|false>
-        return ['sdp::part_%s_rows_u64_kernel<%s%s' % (st, _DT.get(dt, dt), ',' if st == 'scatter' else '>')]
+        return ['sdp::part_%s_rows_u64_kernel<%s>' % (st, _DT.get(dt, dt))]
     if name == 'sdp_part_rows_records':
         return ['sdp::part_records_rows_bytes_kernel']
     if name == 'sdp_part_dedup':
-        return ['sdp::part_dedup_bytes_kernel'] if dt == 'bytes' else ['sdp::part_dedup_u64']
-    if name in ('sdp_pass1', 'sdp_pass2', 'sdp_pass2_count'):
+        return ['sdp::part_dedup_bytes_kernel<false>'] if dt == 'bytes' else ['sdp::part_dedup_u64']
+    if name == 'sdp_part_dedup_blocks':         # the block-layout variants: <..., true>
+        return (['sdp::part_dedup_bytes_kernel<true>'] if dt == 'bytes'
+                else ['sdp::part_dedup_u64_half_kernel<1, true>', 'sdp::part_dedup_u64_wave2_kernel<0, true>'])
+    if name == 'sdp_part_l2_blocks':
+        return ['sdp::part_l2_blocks_kernel<%s>' % ('true' if dt == 'bytes' else 'false')]
+    if name in ('sdp_pass1', 'sdp_pass2', 'sdp_pass2_count', 'sdp_pass1_batch', 'sdp_pass2_count_batch'):
         return ['sdp::%s_kernel<%s' % (name[4:], _DT.get(dt, dt))]
     if name == 'sdp_distinct32':
         return ['sdp::d32_']
@@ -337,7 +341,7 @@ def label_kernels(label):
 # PMC traffic summary the bench reads `roofline.traffic` from, chosen by name
 # (never by file mtime, which a git checkout scrambles): the newest committed
 # summary of the default workload (tools/gpu_traffic.sh -> tools/traffic_summary.py).
-TRAFFIC_SUMMARY = {'c3': 'profiles/r05ai_c3_traffic.json', 'c5': 'profiles/r04f_c5_traffic.json'}
+TRAFFIC_SUMMARY = {'c3': 'profiles/r06j_c3_traffic.json', 'c5': 'profiles/r04f_c5_traffic.json'}
 
 
 def pmc_traffic(label, path, rows=None, workload=None):

@@ -1723,8 +1723,14 @@ __device__ __forceinline__ void wave_load_batch(uint64_t (&hq)[WV_Q], const uint
         for (int q = 0; q < WV_Q; ++q) hq[q] = (int64_t)q * WAVE < rem ? base[q * WAVE + lane] : EMPTY64;
         return;
     }
+    const uint64_t *pr = in_h + (BLK ? ra.r0() : 0);               // (as wave_load_batch16)
 #pragma unroll
-    for (int q = 0; q < WV_Q; ++q) hq[q] = (int64_t)q * WAVE < rem ? ra.wave_base(in_h, rb, q)[lane] : EMPTY64;
+    for (int q = 0; q < WV_Q; ++q) {
+        if (!BLK || (uint64_t)(rb + (int64_t)q * WAVE) < (uint64_t)ra.d.w)
+            hq[q] = (int64_t)q * WAVE < rem ? pr[rb + (int64_t)q * WAVE + lane] : EMPTY64;
+        else
+            hq[q] = (int64_t)q * WAVE < rem ? ra.wave_base(in_h, rb, q)[lane] : EMPTY64;
+    }
 }
 // Two-phase wave dedup (round 3).  The round-2 register-queue loop (each lane
 // walking its own queue of records, deleted in round 5) paid a dependent LDS round trip plus a shift of
@@ -1940,8 +1946,18 @@ __device__ __forceinline__ void wave_load_batch16(uint64_t (&hq)[WH_Q], const ui
         for (int q = 0; q < WH_Q; ++q) hq[q] = (int64_t)q * WAVE < rem ? p[rb + (int64_t)q * WAVE + lane] : EMPTY64;
         return;
     }
+    // a batch reaching past the run: the wave-wide loads still inside it in
+    // the contiguous form, the list read only for those in overflow blocks
+    // (a column of repeated keys overflows many runs: whole groups of copies
+    // land in one sub-bucket)
+    const uint64_t *pr = in_h + (BLK ? ra.r0() : 0);
 #pragma unroll
-    for (int q = 0; q < WH_Q; ++q) hq[q] = (int64_t)q * WAVE < rem ? ra.wave_base(in_h, rb, q)[lane] : EMPTY64;
+    for (int q = 0; q < WH_Q; ++q) {
+        if (!BLK || (uint64_t)(rb + (int64_t)q * WAVE) < (uint64_t)ra.d.w)         // (wave-uniform)
+            hq[q] = (int64_t)q * WAVE < rem ? pr[rb + (int64_t)q * WAVE + lane] : EMPTY64;
+        else
+            hq[q] = (int64_t)q * WAVE < rem ? ra.wave_base(in_h, rb, q)[lane] : EMPTY64;
+    }
 }
 template <int MODE, bool LIMIT>
 __device__ __forceinline__ uint32_t wh_probe(uint64_t *T, uint64_t x, bool &full) {

@@ -1195,9 +1195,16 @@ class Engine:
         return r, keep
 
     @staticmethod
-    def _l2b_ok(isb, b2):
+    def _l2b_ok(isb, b2, heavy=False):
         """sdp_part_l2_blocks takes this level 2 (<= 1024 sub-buckets of fixed
-        keys, <= 512 of byte keys: the LDS lines of one workgroup)."""
+        keys, <= 512 of byte keys: the LDS lines of one workgroup) -- but not
+        for fixed keys with heavy keys in the sample: a skewed column's copies
+        land in whole groups, so many sub-buckets overflow their runs and the
+        block dedup reads them through the lists (i64_zipf: count + scatter +
+        dedup 6.5 ms counted vs 9.7 ms in blocks; near-unique and byte columns
+        gain, profiles/r06m_*)."""
+        if heavy and not isb:
+            return False
         return L2_BLOCKS and 1 <= b2 and (1 << b2) <= (512 if isb else 1024)
 
     L2B_WG = 256                       # persistent workgroups of sdp_part_l2_blocks (one per CU)
@@ -1561,7 +1568,7 @@ class Engine:
         if b2 == 0 or nrec == 0:
             starts = torch.cat([bstarts, o1[-1:]]) if b2 == 0 else self._u64(nb1 * nb2 + 1, zero=True)
             rf, keepf = r1, keep1
-        elif self._l2b_ok(isb, b2):
+        elif self._l2b_ok(isb, b2, bool(hv and hv['n'])):
             nat.annotate(('bytes' if isb else 'u64') + '/l2blocks', 2 * nrec * recw)
             rf, keepf, blk, blk_keep = self._l2_blocks(r1, isb, b1, b2, bsn[:-1], bsn[1:], np.arange(nb1), nb1)
             del keep1, r1
@@ -1702,7 +1709,7 @@ class Engine:
         del shared
         nfinal = nb1 * nb2
         nf = nfinal * len(ctxs)
-        if self._l2b_ok(False, b2):
+        if self._l2b_ok(False, b2, any(c['hv'] and c['hv']['n'] for c in ctxs)):
             # level 2 of every column's level-1 buckets into blocks: one
             # workgroup per (column, bucket), no count pass
             bst = np.concatenate([bs[:-1] for bs in bsns] + [[total]]).astype(np.int64)
@@ -1981,7 +1988,7 @@ class Engine:
             st0 = part_base[:, None] + np.concatenate([np.zeros((world, 1), np.int64),
                                                       np.cumsum(S, axis=1)[:, :-1]], axis=1)
             rin = nat.SdpRecords(recv.data_ptr(), None, None)
-            if self._l2b_ok(False, b2):
+            if self._l2b_ok(False, b2, bool(ctx['hv'] and ctx['hv']['n'])):
                 # level 2 into blocks: bucket bi = one segment per source rank
                 lo_s = st0.T.reshape(-1)
                 nat.annotate('u64/l2blocks', 2 * nrecv * 8)

@@ -49,7 +49,8 @@ def test_run_ranks_reprints_rank0_line_and_rc(capsys):
 
 
 @pytest.mark.parametrize('label', ['sdp_part_rows[f64/scatter]', 'sdp_part_rows[i64/scatter]',
-                                   'sdp_part_rows_records[bytes/records]'])
+                                   'sdp_part_rows_records[bytes/records]', 'sdp_part_dedup_blocks[u64]',
+                                   'sdp_part_l2_blocks[u64/l2blocks]', 'sdp_pass1_batch[f64/batch]'])
 def test_committed_traffic_summary_covers_dominant_kernels(label):
     """roofline.traffic comes from the committed PMC summary: each kernel that
     has been the C3 bench's dominant one must map to its rocprof name there."""
