@@ -22,6 +22,9 @@ constexpr int P1_MAX_GRID = 1024;     // 4 blocks per CU on 256 CUs
 #ifndef P1_STAGES
 #define P1_STAGES 3                   // tiles of pass 1's whole-tile ring (2 in flight)
 #endif
+#ifndef P1_EXCL_FAST
+#define P1_EXCL_FAST 1                // exclusive windows on the whole-tile ring too (2-pair ring; 3.12 -> 3.05 ms per i64 column, profiles/r06p_ab.log)
+#endif
 #ifndef P1_U32
 #define P1_U32 2                      // 16-byte vectors per thread per tile, 4-byte types
 #endif
@@ -560,13 +563,13 @@ __device__ __forceinline__ void pass1_sweep(P1Thread &st, const P1Ctx &cx, const
     // constants (a tile covers a multiple of 32 rows).  The general path below
     // (clamped vectors, two validity dwords and an alignbit per vector) takes
     // the last, partial tile and unaligned bitmaps.
-    // (exclusive windows keep the general path: their counters leave no
-    // registers for the whole-tile loop, which spilled them -- 5.9 -> 9.4 ms
-    // for C3's int64 columns, profiles/r06e_kernel_stats.csv)
-    const bool fast = INCL && (vbm.none || (vbm.bit0 & 31) == 0);
+    // (exclusive windows: a two-tile ring -- their counters leave no room for
+    // a third; with the slot pointers in VGPRs this loop spilled them, 5.9 ->
+    // 9.4 ms for C3's int64 columns, profiles/r06e_kernel_stats.csv)
+    const bool fast = (INCL || P1_EXCL_FAST) && (vbm.none || (vbm.bit0 & 31) == 0);
     const int64_t nfull = fast ? nvec / tile_vecs : 0;
     int64_t tile = bx;
-    if constexpr (INCL) if (tile < nfull) {
+    if constexpr (INCL || P1_EXCL_FAST) if (tile < nfull) {
         typedef uint32_t u32x4g __attribute__((ext_vector_type(4)));
         typedef const __attribute__((address_space(1))) u32x4g gvec;
         typedef const __attribute__((address_space(1))) uint32_t gword;
