@@ -341,7 +341,7 @@ def label_kernels(label):
 # PMC traffic summary the bench reads `roofline.traffic` from, chosen by name
 # (never by file mtime, which a git checkout scrambles): the newest committed
 # summary of the default workload (tools/gpu_traffic.sh -> tools/traffic_summary.py).
-TRAFFIC_SUMMARY = {'c3': 'profiles/r06j_c3_traffic.json', 'c5': 'profiles/r06o_c5_traffic.json'}
+TRAFFIC_SUMMARY = {'c3': 'profiles/r06s_c3_traffic.json', 'c5': 'profiles/r06o_c5_traffic.json'}
 
 
 def pmc_traffic(label, path, rows=None, workload=None):
