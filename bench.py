@@ -325,8 +325,10 @@ def label_kernels(label):
     if name == 'sdp_part_dedup':
         return ['sdp::part_dedup_bytes_kernel<false>'] if dt == 'bytes' else ['sdp::part_dedup_u64']
     if name == 'sdp_part_dedup_blocks':         # the block-layout variants: <..., true>
+        # (fixed keys: C3's block-layout columns are the near-unique ones, on
+        # the half-space kernel; skewed columns keep the counted layout)
         return (['sdp::part_dedup_bytes_kernel<true>'] if dt == 'bytes'
-                else ['sdp::part_dedup_u64_half_kernel<1, true>', 'sdp::part_dedup_u64_wave2_kernel<0, true>'])
+                else ['sdp::part_dedup_u64_half_kernel<1, true>'])
     if name == 'sdp_part_l2_blocks':
         return ['sdp::part_l2_blocks_kernel<%s>' % ('true' if dt == 'bytes' else 'false')]
     if name in ('sdp_pass1', 'sdp_pass2', 'sdp_pass2_count', 'sdp_pass1_batch', 'sdp_pass2_count_batch'):
