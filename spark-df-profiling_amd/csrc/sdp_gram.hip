@@ -546,7 +546,10 @@ __global__ void __launch_bounds__(G16_BLOCK, 4 / G16_Q) gram16_kernel(const Gram
             if (r0 + G16_R > c1) kb[k] &= r >= c1 ? 0u : (r + 4 > c1 ? (1u << (int)(c1 - r)) - 1u : 0xFu);
             if (wid == 0) nkeep += (double)__popc(kb[k]);
         }
-        __syncthreads();                               // the previous k-step's operand reads are done
+        // (LDS-only barriers: __syncthreads()' release fence waited vmcnt(0),
+        // draining the next k-step's loads issued just before the second one --
+        // the prefetch never overlapped the MFMAs)
+        lds_barrier();                                 // the previous k-step's operand reads are done
 #pragma unroll
         for (int k = 0; k < G16_QN; ++k)
 #pragma unroll
@@ -554,7 +557,7 @@ __global__ void __launch_bounds__(G16_BLOCK, 4 / G16_Q) gram16_kernel(const Gram
                 g16_stage_any(gc[j].dtype, raw[k][j], kb[k], K[j], csum[j],
                               &s_y[(wid + G16_W * j) * G16_P + 4 * lane + 4 * WAVE * k]);
         if (r0 + G16_R < c1) load(r0 + G16_R);
-        __syncthreads();
+        lds_barrier();
         // this wave's row groups wid + 4 g: MFMA m takes row 4q + m of the group
 #pragma unroll
         for (int g = 0; g < 4 * G16_QN; ++g) {
