@@ -528,6 +528,25 @@ int sdp_pass2_count_batch(const sdp_pass2_task *d_tasks, int32_t ntasks, int32_t
 int sdp_gather_bytes(const uint8_t *d_data, const int64_t *d_starts, const int64_t *d_lens,
                      const int64_t *d_offs, int64_t n, uint8_t *d_out, void *stream);
 
+/* Owner order of the sharded exchange (replaces the torch sort + searchsorted +
+ * prefix sum + gathers of distributed.py's exchange_fixed_groups /
+ * exchange_bytes_groups_batch, round 5).  Group i is entry e = d_sel[i] (or i
+ * when d_sel is NULL) of d_keys / d_counts; the groups come out ordered by
+ * owner rank, stable within an owner, at positions p = 0 .. n-1.
+ *   bcol NULL (fixed keys): owner = ((key * 0x9E3779B97F4A7C15) >> 40 & 0xFFFFFF)
+ *     % world; d_out_keys[p] = key, d_out_counts[p] = d_counts[e] (if non-NULL).
+ *   bcol set (d_keys = byte-table slots, tag << 40 | row + 1): owner = tag % world;
+ *     d_starts[p] / d_lens[p] = the row's key bytes in bcol (lengths < 2^32),
+ *     d_meta[2p], d_meta[2p+1] = (length, d_counts[e]), d_offs[0 .. n] = exclusive
+ *     prefix of the lengths (the key's place in the owner-major payload).
+ * d_per[o] = groups of owner o, d_per[world + o] = their key bytes (0 for fixed
+ * keys).  world <= 2048; d_work: sdp_owner_order_workspace_bytes(n, world). */
+int64_t sdp_owner_order_workspace_bytes(int64_t n, int32_t world);
+int sdp_owner_order(const uint64_t *d_keys, const uint64_t *d_sel, const int64_t *d_counts, int64_t n,
+                    int32_t world, const sdp_bytes_column *bcol, uint64_t *d_out_keys, int64_t *d_out_counts,
+                    int64_t *d_starts, int64_t *d_lens, int64_t *d_meta, uint64_t *d_offs, int64_t *d_per,
+                    void *d_work, int64_t work_bytes, void *stream);
+
 /* Rows per partition workgroup (grid = ceil(length / this)). */
 int64_t sdp_part_rows_per_block(int64_t length, int32_t is_bytes);
 /* Mean records per final bucket the dedup tables are sized for. */

@@ -619,3 +619,227 @@ extern "C" int sdp_gather_bytes(const uint8_t *d_data, const int64_t *d_starts, 
                        d_lens, d_offs, n, d_out);
     return check_launch("gather_bytes_kernel");
 }
+
+// ---- owner order of the sharded exchange (distributed.py) --------------------
+// Every rank sends each of its groups to the key's owner rank.  The groups go
+// owner-major and, within an owner, in their table order (a stable counting
+// sort by owner): per 2048-group chunk an owner histogram, one exclusive scan
+// of the owner-major [owner][chunk] counts, then a scatter that ranks each
+// group among the same-owner groups before it in its chunk.  Byte groups also
+// get their key's (start, length) in the column, the (length, count) pair the
+// owner re-aggregates with, and (a second scan) the byte offset of the key in
+// the owner-major payload that sdp_gather_bytes packs.  Replaces a torch sort +
+// searchsorted + prefix sum + gathers (round 5's exchange).
+constexpr int OWN_T = 256;
+constexpr int OWN_W = OWN_T / WAVE;
+constexpr int OWN_PER = 8;
+constexpr int OWN_CH = OWN_T * OWN_PER;       // groups per chunk
+constexpr int OWN_MAX_WORLD = 2048;      // scatter LDS 5 x 4 B per owner: <= 40 KB
+
+struct OwnerSrc {
+    const uint64_t *keys;       // u64 keys, or byte-table slots (24-bit tag << 40 | row + 1)
+    const uint64_t *sel;        // group i is entry sel[i] (NULL: entry i)
+    const int64_t *counts;      // per entry, or NULL
+    sdp_bytes_column col;       // byte groups: the column the rows index
+    int64_t n;
+    int32_t world;
+    int32_t is_bytes;
+};
+
+struct OwnerOut {
+    uint64_t *keys;             // fixed keys
+    int64_t *counts;            // fixed keys' counts (NULL: none)
+    int64_t *starts, *lens;     // byte groups
+    int64_t *meta;              // byte groups: (length, count) pairs
+    uint32_t *lens32;           // byte groups: lengths for the offsets scan
+};
+
+__device__ __forceinline__ uint32_t owner_of(const OwnerSrc &s, uint64_t k) {
+    // distributed._owner_u64 (fixed keys: multiplicative hash) / the byte slot's tag
+    const uint64_t h = s.is_bytes ? k : k * 0x9E3779B97F4A7C15ull;
+    return (uint32_t)((h >> 40) & 0xFFFFFFull) % (uint32_t)s.world;
+}
+
+// lanes of this wave with the same owner: rank among the lower such lanes and
+// their number (one round per distinct owner in the wave)
+__device__ __forceinline__ void wave_owner_match(uint32_t o, bool act, uint32_t &rank, uint32_t &size) {
+    uint64_t rem = __ballot(act);
+    rank = 0;
+    size = 0;
+    while (rem) {
+        const int l = __ffsll((unsigned long long)rem) - 1;
+        const uint32_t lo = (uint32_t)__shfl((int)o, l, WAVE);
+        const uint64_t m = __ballot(act && o == lo);
+        if (act && o == lo) {
+            rank = (uint32_t)lane_rank(m);
+            size = (uint32_t)__popcll(m);
+        }
+        rem &= ~m;
+    }
+}
+
+__global__ void __launch_bounds__(OWN_T) owner_hist_kernel(OwnerSrc s, int64_t nchunks, uint32_t *hist) {
+    extern __shared__ uint32_t s_own[];       // [world]
+    for (int o = threadIdx.x; o < s.world; o += OWN_T) s_own[o] = 0;
+    __syncthreads();
+    const int64_t c = blockIdx.x;
+    for (int k = 0; k < OWN_PER; ++k) {
+        const int64_t i = c * OWN_CH + (int64_t)k * OWN_T + threadIdx.x;
+        const bool act = i < s.n;
+        uint32_t o = 0;
+        if (act) o = owner_of(s, s.keys[s.sel ? (int64_t)s.sel[i] : i]);
+        uint32_t rank, size;
+        wave_owner_match(o, act, rank, size);
+        if (act && rank == 0) atomicAdd(&s_own[o], size);
+    }
+    __syncthreads();
+    for (int o = threadIdx.x; o < s.world; o += OWN_T) hist[(int64_t)o * nchunks + c] = s_own[o];
+}
+
+__global__ void __launch_bounds__(OWN_T) owner_scatter_kernel(OwnerSrc s, int64_t nchunks, const uint64_t *hoffs,
+                                                              OwnerOut out) {
+    extern __shared__ uint32_t s_own[];       // run[world] | per-wave counts [OWN_W][world]
+    uint32_t *s_run = s_own, *s_wc = s_own + s.world;
+    for (int o = threadIdx.x; o < s.world * (1 + OWN_W); o += OWN_T) s_own[o] = 0;
+    __syncthreads();
+    const int w = threadIdx.x / WAVE;
+    const int64_t c = blockIdx.x;
+    for (int k = 0; k < OWN_PER; ++k) {
+        const int64_t i = c * OWN_CH + (int64_t)k * OWN_T + threadIdx.x;
+        const bool act = i < s.n;
+        int64_t e = 0;
+        uint64_t key = 0;
+        uint32_t o = 0;
+        if (act) {
+            e = s.sel ? (int64_t)s.sel[i] : i;
+            key = s.keys[e];
+            o = owner_of(s, key);
+        }
+        uint32_t rank, size;
+        wave_owner_match(o, act, rank, size);
+        if (act && rank == 0) s_wc[w * s.world + o] = size;
+        lds_barrier();
+        uint64_t p = 0;
+        if (act) {
+            uint32_t before = s_run[o];
+            for (int v = 0; v < w; ++v) before += s_wc[v * s.world + o];
+            p = hoffs[(int64_t)o * nchunks + c] + before + rank;
+        }
+        lds_barrier();
+        for (int t = threadIdx.x; t < s.world; t += OWN_T) {
+            uint32_t a = 0;
+            for (int v = 0; v < OWN_W; ++v) {
+                a += s_wc[v * s.world + t];
+                s_wc[v * s.world + t] = 0;
+            }
+            s_run[t] += a;
+        }
+        lds_barrier();
+        if (!act) continue;
+        const int64_t cnt = s.counts ? s.counts[e] : 0;
+        if (!s.is_bytes) {
+            out.keys[p] = key;
+            if (out.counts) out.counts[p] = cnt;
+            continue;
+        }
+        const int64_t row = (int64_t)(key & ROW_MASK) - 1;
+        int64_t st, len;
+        if (s.col.fixed_width > 0) {
+            st = row * s.col.fixed_width;
+            len = s.col.fixed_width;
+        } else if (s.col.offset_width == 4) {
+            const int32_t *off = (const int32_t *)s.col.d_offsets;
+            st = off[row];
+            len = (int64_t)off[row + 1] - st;
+        } else {
+            const int64_t *off = (const int64_t *)s.col.d_offsets;
+            st = off[row];
+            len = off[row + 1] - st;
+        }
+        out.starts[p] = st;
+        out.lens[p] = len;
+        out.meta[2 * p] = len;
+        out.meta[2 * p + 1] = cnt;
+        out.lens32[p] = (uint32_t)len;
+    }
+}
+
+__global__ void __launch_bounds__(OWN_T) owner_totals_kernel(const uint64_t *hoffs, int64_t nchunks, int world,
+                                                             const uint64_t *boffs, int64_t *per) {
+    for (int o = threadIdx.x; o < world; o += OWN_T) {
+        const uint64_t g0 = hoffs[(int64_t)o * nchunks], g1 = hoffs[(int64_t)(o + 1) * nchunks];
+        per[o] = (int64_t)(g1 - g0);
+        per[world + o] = boffs ? (int64_t)(boffs[g1] - boffs[g0]) : 0;
+    }
+}
+
+static int64_t align16(int64_t b) { return (b + 15) & ~(int64_t)15; }
+
+extern "C" int64_t sdp_owner_order_workspace_bytes(int64_t n, int32_t world) {
+    if (n < 0 || world < 1) return 0;
+    const int64_t nchunks = (n + OWN_CH - 1) / OWN_CH;
+    const int64_t nh = (int64_t)world * nchunks;
+    int64_t scan = sdp_scan_workspace_bytes(nh > 0 ? nh : 1);
+    const int64_t scan_n = sdp_scan_workspace_bytes(n > 0 ? n : 1);
+    if (scan_n > scan) scan = scan_n;
+    return align16(nh * 4) + align16((nh + 1) * 8) + align16(n * 4) + align16(scan);
+}
+
+extern "C" int sdp_owner_order(const uint64_t *d_keys, const uint64_t *d_sel, const int64_t *d_counts, int64_t n,
+                               int32_t world, const sdp_bytes_column *bcol, uint64_t *d_out_keys,
+                               int64_t *d_out_counts, int64_t *d_starts, int64_t *d_lens, int64_t *d_meta,
+                               uint64_t *d_offs, int64_t *d_per, void *d_work, int64_t work_bytes, void *stream) {
+    if (n < 0 || world < 1 || world > OWN_MAX_WORLD || d_per == nullptr)
+        return set_error(SDP_EINVAL, "sdp_owner_order: n %lld world %d", (long long)n, (int)world);
+    const bool isb = bcol != nullptr;
+    if (isb ? (d_starts == nullptr || d_lens == nullptr || d_meta == nullptr || d_offs == nullptr ||
+               (bcol->fixed_width <= 0 && (bcol->d_offsets == nullptr ||
+                                           (bcol->offset_width != 4 && bcol->offset_width != 8))))
+            : d_out_keys == nullptr)
+        return set_error(SDP_EINVAL, "sdp_owner_order: outputs");
+    if (d_out_counts != nullptr && d_counts == nullptr)
+        return set_error(SDP_EINVAL, "sdp_owner_order: counts out without counts in");
+    if (isb && d_counts == nullptr) return set_error(SDP_EINVAL, "sdp_owner_order: byte groups need counts");
+    if (work_bytes < sdp_owner_order_workspace_bytes(n, world))
+        return set_error(SDP_ECAP, "sdp_owner_order: workspace too small");
+    hipStream_t s = (hipStream_t)stream;
+    if (n == 0) {
+        if (hipMemsetAsync(d_per, 0, (size_t)world * 2 * sizeof(int64_t), s) != hipSuccess ||
+            (isb && hipMemsetAsync(d_offs, 0, sizeof(uint64_t), s) != hipSuccess))
+            return set_error(SDP_EHIP, "sdp_owner_order: memset");
+        return 0;
+    }
+    const int64_t nchunks = (n + OWN_CH - 1) / OWN_CH;
+    if (nchunks > 0x7FFFFFFF) return set_error(SDP_EINVAL, "sdp_owner_order: too many groups");
+    const int64_t nh = (int64_t)world * nchunks;
+    uint8_t *wp = (uint8_t *)d_work;
+    uint32_t *hist = (uint32_t *)wp;
+    wp += align16(nh * 4);
+    uint64_t *hoffs = (uint64_t *)wp;
+    wp += align16((nh + 1) * 8);
+    uint32_t *lens32 = (uint32_t *)wp;
+    wp += align16(n * 4);
+    void *scan = wp;
+    const int64_t scan_bytes = work_bytes - (wp - (uint8_t *)d_work);
+    OwnerSrc src;
+    src.keys = d_keys;
+    src.sel = d_sel;
+    src.counts = d_counts;
+    src.col = isb ? *bcol : sdp_bytes_column{};
+    src.n = n;
+    src.world = world;
+    src.is_bytes = isb ? 1 : 0;
+    OwnerOut out{d_out_keys, d_out_counts, d_starts, d_lens, d_meta, lens32};
+    hipLaunchKernelGGL(owner_hist_kernel, dim3((unsigned)nchunks), dim3(OWN_T), (size_t)world * 4, s, src, nchunks,
+                       hist);
+    int rc = check_launch("owner_hist_kernel");
+    if (rc) return rc;
+    if ((rc = sdp_scan_u32(hist, nh, hoffs, scan, scan_bytes, stream))) return rc;
+    hipLaunchKernelGGL(owner_scatter_kernel, dim3((unsigned)nchunks), dim3(OWN_T), (size_t)world * 4 * (1 + OWN_W),
+                       s, src, nchunks, (const uint64_t *)hoffs, out);
+    if ((rc = check_launch("owner_scatter_kernel"))) return rc;
+    if (isb && (rc = sdp_scan_u32(lens32, n, d_offs, scan, scan_bytes, stream))) return rc;
+    hipLaunchKernelGGL(owner_totals_kernel, dim3(1), dim3(OWN_T), 0, s, (const uint64_t *)hoffs, nchunks, (int)world,
+                       isb ? (const uint64_t *)d_offs : nullptr, d_per);
+    return check_launch("owner_totals_kernel");
+}

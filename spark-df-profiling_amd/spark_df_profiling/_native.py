@@ -248,6 +248,8 @@ _SIGNATURES = {
     'sdp_pass2_count': (ctypes.c_int, [_COL, _D, _P, _I32, _I32, _D, _D, _P, _I64, _P, _P, _HVY, _I32, _P, _P, _P,
                                        _P]),
     'sdp_gather_bytes': (ctypes.c_int, [_P, _P, _P, _P, _I64, _P, _P]),
+    'sdp_owner_order_workspace_bytes': (_I64, [_I64, _I32]),
+    'sdp_owner_order': (ctypes.c_int, [_P, _P, _P, _I64, _I32, _BCOL, _P, _P, _P, _P, _P, _P, _P, _P, _I64, _P]),
     'sdp_table_clear': (ctypes.c_int, [_P, _P, _I64, _I32, _P]),
     'sdp_hash_u64': (ctypes.c_int, [_COL, _P, _P, _P, _I64, _I32, _P, _P]),
     'sdp_hash_bytes': (ctypes.c_int, [_BCOL, _P, _P, _P, _I64, _P, _P]),
@@ -309,7 +311,8 @@ _VALUE_FUNCS = {'sdp_last_error', 'sdp_version', 'sdp_pass1_workspace_bytes', 's
                 'sdp_scan_workspace_bytes', 'sdp_bitmap_workspace_bytes', 'sdp_select_kth_workspace_bytes',
                 'sdp_select_rounds', 'sdp_pass2_count_workspace_bytes', 'sdp_minmax_workspace_bytes',
                 'sdp_quantiles_workspace_bytes', 'sdp_distinct_workspace_bytes', 'sdp_value_counts_workspace_bytes',
-                'sdp_pearson_workspace_bytes', 'sdp_distinct32_workspace_bytes'}
+                'sdp_pearson_workspace_bytes', 'sdp_distinct32_workspace_bytes',
+                'sdp_owner_order_workspace_bytes'}
 _STATUS_FUNCS = set(_SIGNATURES) - _VALUE_FUNCS
 
 _lib = None

@@ -10,8 +10,10 @@ rank (all-to-all), and the owner re-aggregates what it received:
 * first rows      = every rank's first k na.drop rows, concatenated in rank order
                     (rank r holds the r-th contiguous row range).
 
-The exchange itself is data movement (gather by owner, all_to_all_single);
-aggregation runs in the same HIP kernels as the single-GPU path.
+The exchange itself is data movement: the groups are put in owner order by
+one libsdp call (sdp_owner_order: owner histogram, scan, stable scatter), the
+key bytes packed by sdp_gather_bytes, then all_to_all_single; aggregation runs
+in the same HIP kernels as the single-GPU path.
 """
 
 from __future__ import annotations
@@ -25,17 +27,14 @@ from . import _native as nat
 from ._native import sdp, ptr
 from .comm import to_dev
 
-MASK40 = (1 << 40) - 1
-
-
 def _owner_u64(keys: torch.Tensor, world: int) -> torch.Tensor:
     """Owner rank of each u64 key (stored as int64): a multiplicative hash."""
     h = keys * -7046029254386353131            # 0x9E3779B97F4A7C15 as int64; wraps
     return ((h >> 40) & 0xFFFFFF) % world
 
 
-def _table_groups(engine, tab):
-    """Dense (keys, counts) of a local table (all occupied slots)."""
+def _table_sel(engine, tab):
+    """Entries of the occupied slots of a local table: (indices, count)."""
     slots, counts, cap = tab['slots'], tab['counts'], tab['capacity']
     flags = int(tab['bytes']) | (2 if tab.get('dense') else 0)
     n_local = tab['groups_local'] if 'groups_local' in tab else tab['groups']
@@ -43,27 +42,53 @@ def _table_groups(engine, tab):
     nsel = engine._u64(1, zero=True)
     sdp.sdp_table_select(ptr(slots), ptr(counts), cap, flags, 1 if counts is not None else 0,
                          (1 << 64) - 1, ptr(sel), ptr(nsel), max(n_local, 1), engine._s())
-    m = int(nsel.item())
-    sel = sel[:m]
-    keys = slots[sel]
-    cnt = counts[sel] if counts is not None else None
-    return keys, cnt
+    return sel, int(nsel.item())
+
+
+def _owner_order(engine, keys, sel, counts, n, bcol=None, with_counts=True):
+    """sdp_owner_order: the groups owner-major (stable within an owner), one
+    libsdp call.  Returns the output tensors and per = [2, world] (groups,
+    key bytes) per owner, still on the device."""
+    world = engine.comm.world
+    dev = engine.device
+    out = {'per': torch.empty(2 * world, dtype=torch.int64, device=dev)}
+    m = max(n, 1)
+    if bcol is None:
+        out['keys'] = torch.empty(m, dtype=torch.int64, device=dev)
+        out['counts'] = torch.empty(m, dtype=torch.int64, device=dev) if with_counts else None
+    else:
+        for k in ('starts', 'lens'):
+            out[k] = torch.empty(m, dtype=torch.int64, device=dev)
+        out['meta'] = torch.empty(2 * m, dtype=torch.int64, device=dev)
+        out['offs'] = torch.empty(n + 1, dtype=torch.int64, device=dev)
+    wb = sdp.sdp_owner_order_workspace_bytes(n, world)
+    work = engine._bytes(max(wb, 16))
+    sdp.sdp_owner_order(ptr(keys), ptr(sel) if sel is not None else None,
+                        ptr(counts) if counts is not None else None, n, world,
+                        ctypes.byref(bcol) if bcol is not None else None,
+                        ptr(out['keys']) if bcol is None else None,
+                        ptr(out['counts']) if bcol is None and out['counts'] is not None else None,
+                        *[ptr(out[k]) if bcol is not None else None for k in ('starts', 'lens', 'meta', 'offs')],
+                        ptr(out['per']), ptr(work), wb, engine._s())
+    for k in list(out):
+        if k not in ('per', 'offs') and out[k] is not None:
+            out[k] = out[k][:n] if k != 'meta' else out[k][:2 * n]
+    out['_work'] = work
+    return out
 
 
 def exchange_fixed_groups(engine, tab, with_counts):
     comm = engine.comm
     world = comm.world
-    keys, cnt = _table_groups(engine, tab)
-    owner = _owner_u64(keys, world)
-    order = _owner_order(owner, world)
-    keys = keys[order]
-    bounds = torch.searchsorted(owner[order], torch.arange(world + 1, dtype=owner.dtype, device=engine.device))
-    send = (bounds[1:] - bounds[:-1]).tolist()
+    sel, m = _table_sel(engine, tab)
+    oo = _owner_order(engine, tab['slots'], sel, tab['counts'] if with_counts else None, m,
+                      with_counts=with_counts)
+    send = oo['per'][:world].tolist()
     recv = comm.alltoall_counts([send])[0]
-    rkeys = comm.alltoallv_known(keys.contiguous(), send, recv)
+    rkeys = comm.alltoallv_known(oo['keys'], send, recv)
     rcnt = None
     if with_counts:
-        rcnt = comm.alltoallv_known(cnt[order].contiguous(), send, recv)
+        rcnt = comm.alltoallv_known(oo['counts'], send, recv)
     # owner table over the received keys (they are already order-preserving
     # u64 keys: a U64 column hashes them unchanged)
     from .columns import DeviceColumn
@@ -80,13 +105,6 @@ def exchange_fixed_groups(engine, tab, with_counts):
     local['rows'] = rows
     local['sharded'] = True
     return local
-
-
-def _owner_order(owner, world):
-    """Stable order of the groups by owner rank: a radix sort of 1- or 2-byte
-    keys (one or two passes) instead of an int64 argsort."""
-    key = owner.to(torch.uint8 if world <= 256 else torch.int16)
-    return torch.sort(key, stable=True)[1]
 
 
 def exchange_bytes_groups(engine, tab):
@@ -111,48 +129,29 @@ def exchange_bytes_groups_batch(engine, tabs):
         col = tab['col']
         if tab.get('dense'):
             # partitioned groups are already packed: every entry is a group
-            m = int(tab['groups_local'])
-            slots, cnt = tab['slots'][:m], tab['counts'][:m]
+            sel, m = None, int(tab['groups_local'])
         else:
-            slots, cnt = _table_groups(engine, tab)
-        rows = (slots & MASK40) - 1
-        owner = ((slots >> 40) & 0xFFFFFF) % world
-        order = _owner_order(owner, world)
-        rows, cnt, owner = rows[order], cnt[order], owner[order]
-        if col.fixed_width:
-            starts = rows * col.fixed_width
-            lens = torch.full_like(rows, col.fixed_width)
-        else:
-            o = col.offsets.to(torch.int64)
-            starts = o[rows]
-            lens = o[rows + 1] - starts
-        # groups and key bytes per owner from the owner-sorted order: range
-        # bounds by searchsorted and a prefix sum of the lengths (a scatter_add
-        # into `world` counters serialised every group's atomic on a few
-        # addresses: 4.2 ms per 1.25e8-row step, profiles/r03q_*)
-        bounds = torch.searchsorted(owner, torch.arange(world + 1, dtype=owner.dtype, device=engine.device))
-        pref = torch.zeros(lens.numel() + 1, dtype=torch.int64, device=engine.device)
-        torch.cumsum(lens, 0, out=pref[1:])
-        per = torch.stack([bounds[1:] - bounds[:-1], pref[bounds[1:]] - pref[bounds[:-1]]])
-        pers.append(per)
-        preps.append((tab, col, starts, lens, cnt, pref[:-1]))
+            sel, m = _table_sel(engine, tab)
+        bc = col.sdp_bytes()
+        oo = _owner_order(engine, tab['slots'], sel, tab['counts'], m, bcol=bc)
+        pers.append(oo['per'].view(2, world))
+        preps.append((tab, col, oo))
     allper = torch.stack(pers).cpu().tolist()                     # [column][groups | bytes][owner]
     payloads = []
-    for (tab, col, starts, lens, cnt, offs), (send_groups, send_bytes) in zip(preps, allper):
+    for (tab, col, oo), (send_groups, send_bytes) in zip(preps, allper):
         # key bytes of every group, owner-major, packed by one native gather
         tot = sum(send_bytes)
         payload = torch.empty(max(tot, 1), dtype=torch.uint8, device=engine.device)[:tot]
         if tot:
-            sdp.sdp_gather_bytes(ptr(col.data), ptr(starts.contiguous()), ptr(lens.contiguous()), ptr(offs),
-                                 lens.numel(), ptr(payload), engine._s())
+            sdp.sdp_gather_bytes(ptr(col.data), ptr(oo['starts']), ptr(oo['lens']), ptr(oo['offs']),
+                                 oo['lens'].numel(), ptr(payload), engine._s())
         payloads.append(payload)
     recv = comm.alltoall_counts([row for pr in allper for row in pr])
     launched = []
-    for j, ((tab, col, starts, lens, cnt, _), (send_groups, send_bytes), payload) in enumerate(zip(preps, allper,
-                                                                                                  payloads)):
+    for j, ((tab, col, oo), (send_groups, send_bytes), payload) in enumerate(zip(preps, allper, payloads)):
         recv_groups, recv_bytes = recv[2 * j], recv[2 * j + 1]
         # (length, count) pairs in one exchange, the key bytes in a second
-        meta = torch.stack([lens, cnt], 1).contiguous().view(-1)
+        meta = oo['meta']
         rmeta = comm.alltoallv_known(meta, [2 * g for g in send_groups], [2 * g for g in recv_groups]).view(-1, 2)
         rbytes = comm.alltoallv_known(payload.contiguous(), send_bytes, recv_bytes)
         rlens, rcnt = rmeta[:, 0].contiguous(), rmeta[:, 1].contiguous()

@@ -85,6 +85,17 @@ def test_part_argument_checks_without_gpu():
         _native.sdp.sdp_part_rows(None, None, None, 4, 0, None, None, None, None, None, None)
     with pytest.raises(_native.NativeError, match='scan_u32'):
         _native.sdp.sdp_scan_u32(None, 0, None, None, 0, None)
+    # the sharded exchange's owner order: world 1 .. 2048, outputs of its mode
+    with pytest.raises(_native.NativeError, match='owner_order: n 10 world 0'):
+        _native.sdp.sdp_owner_order(None, None, None, 10, 0, None, None, None, None, None, None, None, None, None, 0,
+                                    None)
+    with pytest.raises(_native.NativeError, match='owner_order: n 10 world 4096'):
+        _native.sdp.sdp_owner_order(None, None, None, 10, 4096, None, None, None, None, None, None, None, None, None,
+                                    0, None)
+    with pytest.raises(_native.NativeError, match='owner_order: outputs'):
+        _native.sdp.sdp_owner_order(None, None, None, 10, 8, None, None, None, None, None, None, None,
+                                    ctypes.c_void_p(16), None, 0, None)     # (d_per set: not dereferenced)
+    assert _native.sdp.sdp_owner_order_workspace_bytes(0, 8) > 0
     assert _native.sdp.sdp_part_rows_per_block(10 ** 9, 0) % 4096 == 0
     # an empty shard (a rank with no rows) still gets a positive block size: the
     # launchers divide by it
