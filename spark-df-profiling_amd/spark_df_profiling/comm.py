@@ -67,6 +67,10 @@ class LocalComm:
     def alltoall_counts(self, rows):
         return [list(r) for r in rows]
 
+    def alltoall_counts_dev(self, rows):
+        r = rows.cpu().tolist()
+        return r, [list(x) for x in r]
+
     def allgather_object(self, obj, cap=None):
         return [obj]
 
@@ -192,6 +196,21 @@ class TorchComm:
         self.dist.all_to_all_single(recv, send, group=self.group)
         r = recv.cpu().tolist()
         return [[r[src][j] for src in range(self.world)] for j in range(k)]
+
+    def alltoall_counts_dev(self, rows):
+        """alltoall_counts of counts still on the device (rows: int64 [k, world])
+        -> (sent, received), each k lists of `world` ints, with ONE readback of
+        both: the sender needs no readback of its own counts before the
+        exchange."""
+        self.calls['alltoall_counts'] += 1
+        k, w = int(rows.shape[0]), self.world
+        send = self._io(rows.t().contiguous())                       # [world, k]
+        recv = torch.empty_like(send)
+        self.dist.all_to_all_single(recv, send, group=self.group)
+        both = torch.cat([send.view(-1), recv.view(-1)]).cpu().tolist()
+        s, r = both[:w * k], both[w * k:]
+        return ([[s[d * k + j] for d in range(w)] for j in range(k)],
+                [[r[src * k + j] for src in range(w)] for j in range(k)])
 
     # bytes of a pickled object that ride the first all-gather round; a larger
     # object on any rank costs a second round sized by the largest

@@ -83,8 +83,8 @@ def exchange_fixed_groups(engine, tab, with_counts):
     sel, m = _table_sel(engine, tab)
     oo = _owner_order(engine, tab['slots'], sel, tab['counts'] if with_counts else None, m,
                       with_counts=with_counts)
-    send = oo['per'][:world].tolist()
-    recv = comm.alltoall_counts([send])[0]
+    sent, got = comm.alltoall_counts_dev(oo['per'][:world].view(1, world))
+    send, recv = sent[0], got[0]
     rkeys = comm.alltoallv_known(oo['keys'], send, recv)
     rcnt = None
     if with_counts:
@@ -116,10 +116,10 @@ def exchange_bytes_groups_batch(engine, tabs):
     """Re-partition every rank's byte-key groups of several columns by key
     hash: each group's (length, count) and its key bytes go to the owner rank,
     which re-aggregates them in a global table.  The columns share their host
-    round trips: ONE readback of every column's per-owner group and byte
-    counts, ONE all-to-all of every count of every exchange, ONE readback of
-    every owner table's statistics, ONE all-reduce of the totals (round 2 paid
-    these four per column)."""
+    round trips: ONE all-to-all + readback of every column's per-owner group
+    and byte counts (sent and received together), ONE readback of every owner
+    table's statistics, ONE all-reduce of the totals (round 2 paid four per
+    column, round 5 three per batch)."""
     comm = engine.comm
     world = comm.world
     if not tabs:
@@ -136,7 +136,10 @@ def exchange_bytes_groups_batch(engine, tabs):
         oo = _owner_order(engine, tab['slots'], sel, tab['counts'], m, bcol=bc)
         pers.append(oo['per'].view(2, world))
         preps.append((tab, col, oo))
-    allper = torch.stack(pers).cpu().tolist()                     # [column][groups | bytes][owner]
+    # every column's per-owner group and byte counts: sent and received in ONE
+    # all-to-all and one readback
+    sent, recv = comm.alltoall_counts_dev(torch.stack(pers).view(-1, world))
+    allper = [(sent[2 * j], sent[2 * j + 1]) for j in range(len(preps))]
     payloads = []
     for (tab, col, oo), (send_groups, send_bytes) in zip(preps, allper):
         # key bytes of every group, owner-major, packed by one native gather
@@ -146,7 +149,6 @@ def exchange_bytes_groups_batch(engine, tabs):
             sdp.sdp_gather_bytes(ptr(col.data), ptr(oo['starts']), ptr(oo['lens']), ptr(oo['offs']),
                                  oo['lens'].numel(), ptr(payload), engine._s())
         payloads.append(payload)
-    recv = comm.alltoall_counts([row for pr in allper for row in pr])
     launched = []
     for j, ((tab, col, oo), (send_groups, send_bytes), payload) in enumerate(zip(preps, allper, payloads)):
         recv_groups, recv_bytes = recv[2 * j], recv[2 * j + 1]

@@ -56,6 +56,9 @@ def _worker(rank, world, port, q):
         # alltoallv (all_to_all_single, as on RCCL): rank r sends (r*10 + d) repeated d+1 times to rank d
         send = torch.cat([torch.full((d + 1,), rank * 10 + d, dtype=torch.int64) for d in range(world)])
         out['alltoallv'] = comm.alltoallv(send, [d + 1 for d in range(world)]).tolist()
+        # per-owner counts still on the device: sent and received with one readback
+        rows = torch.tensor([[rank * 100 + j * 10 + d for d in range(world)] for j in range(3)], dtype=torch.int64)
+        out['a2ac'] = (comm.alltoall_counts_dev(rows), comm.alltoall_counts(rows.tolist()))
         # top-k merge: (count desc, key asc), deterministic on every rank
         local = [('b%d' % rank, 5), ('a', 3 + rank), ('z%d' % rank, 1)]
         out['topk'] = merge_topk(comm, local, 4)
@@ -105,9 +108,12 @@ def test_two_rank_merges():
         for src in range(world):
             want += [src * 10 + r] * (r + 1)
         assert o['alltoallv'] == want
+        sent, got = o['a2ac'][0]
+        assert sent == [[r * 100 + j * 10 + d for d in range(world)] for j in range(3)]
+        assert got == [[src * 100 + j * 10 + r for src in range(world)] for j in range(3)] == o['a2ac'][1]
         assert o['topk'] == [('b0', 5), ('b1', 5), ('a', 4), ('a', 3)]
         assert o['first'] == ['r0_0', 'r0_1', 'r0_2', 'r1_0']
         assert o['p1'] == (21, 23, 2 ** 63 - 2 ** 64, -1, 1, 3.0, 1)
         assert sum(o['owner']) == 1000 and min(o['owner']) > 350
-    same = {k: v for k, v in res[0].items() if k != 'alltoallv'}
-    assert same == {k: v for k, v in res[1].items() if k != 'alltoallv'}
+    same = {k: v for k, v in res[0].items() if k not in ('alltoallv', 'a2ac')}
+    assert same == {k: v for k, v in res[1].items() if k not in ('alltoallv', 'a2ac')}
