@@ -118,7 +118,7 @@ def exchange_bytes_groups_batch(engine, tabs):
     which re-aggregates them in a global table.  The columns share their host
     round trips: ONE all-to-all + readback of every column's per-owner group
     and byte counts (sent and received together), ONE readback of every owner
-    table's statistics, ONE all-reduce of the totals (round 2 paid four per
+    table's statistics with the all-reduced totals (round 2 paid four per
     column, round 5 three per batch)."""
     comm = engine.comm
     world = comm.world
@@ -169,15 +169,19 @@ def exchange_bytes_groups_batch(engine, tabs):
         data[:rbytes.numel()] = rbytes
         rc.data = data
         launched.append((tab, rc, engine.bytes_table_launch(rc, row_counts=rcnt)))
-    st = engine._host_u64(torch.cat([lt[2]['stats'] for lt in launched]))
-    locals_, sides = [], []
+    # the owner tables' statistics and the (rows, groups) totals over the ranks
+    # (summed on the device) in ONE readback
+    stats = torch.cat([lt[2]['stats'] for lt in launched]).view(-1, 4)
+    rows = to_dev([tab['rows'] for tab, _, _ in launched], torch.int64, engine.device)
+    tot = comm.allreduce_sum(torch.stack([rows, stats[:, 0]], 1).reshape(-1))
+    host = engine._host_u64(torch.cat([stats.reshape(-1), tot]))
+    st, t = host[:stats.numel()], host[stats.numel():]
+    locals_ = []
     for j, (tab, rc, pend) in enumerate(launched):
         local = engine.bytes_table_finish(pend, st[4 * j:4 * j + 4], rc)
         local['src_col'] = rc
         local['col'] = rc
         locals_.append(local)
-        sides += [tab['rows'], local['groups']]
-    t = comm.allreduce_sum(to_dev(sides, torch.int64, engine.device)).tolist()
     for j, local in enumerate(locals_):
         local['groups_local'] = local['groups']
         local['groups'] = int(t[2 * j + 1])
