@@ -73,9 +73,9 @@ __global__ void rowmask_kernel(const MaskCol *cols, int ncols, int64_t n, uint32
 // K descriptors per launch ride in the kernel arguments (copied at launch), so
 // the host array can be freed at once: no pageable copy and no
 // hipStreamSynchronize, which drained the caller's whole queue before the row
-// mask and again before the Gram (the GPU idle while the host woke and
-// launched; sdp_rowmask's HIP-event time was 5.8 ms per C3 step around a
-// 0.69 ms kernel).
+// mask and again before the Gram (r06s's bench measured 5.8 ms of HIP-event
+// time around the 0.69 ms row-mask kernel; a same-box A/B on another box was
+// even, profiles/r06aa_*).
 template <typename D, int K> struct DescBatch {
     D d[K];
 };
