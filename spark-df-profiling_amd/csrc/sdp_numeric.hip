@@ -1017,17 +1017,19 @@ __device__ __forceinline__ void stage_push(Stager &sg, bool keep, uint64_t v, ui
         base = __shfl(base, leader, WAVE);
         if (keep) sg.buf[base + lane_rank(m)] = v;
     }
-    __syncthreads();
+    // (the barriers order LDS only: the flushed stores and the caller's next
+    // loads stay in flight)
+    lds_barrier();
     const uint32_t c = *sg.cnt;
     if (c > STAGE - blockDim.x || (last && c > 0)) {
         if (threadIdx.x == 0) *sg.gbase = atomicAdd(out_n, (unsigned long long)c);
-        __syncthreads();
+        lds_barrier();
         const uint64_t b = *sg.gbase;
         for (uint32_t i = threadIdx.x; i < c; i += blockDim.x) out[b + i] = sg.buf[i];
-        __syncthreads();
+        lds_barrier();
         if (threadIdx.x == 0) *sg.cnt = 0;
     }
-    __syncthreads();
+    lds_barrier();
 }
 
 __global__ void radix_filter_kernel(const uint64_t *keys, const uint64_t *n_ptr, uint64_t prefix,
@@ -1064,6 +1066,8 @@ struct SelState {
     int32_t shift;       // bit position of the digit of the current round
     int32_t done;
     uint64_t result;
+    int32_t width;       // batched selects: bits of the current digit (<= 11)
+    int32_t _pad;
 };
 
 // d_k (nullable): the rank is read from device memory (a rank computed on the
@@ -2127,11 +2131,19 @@ __global__ void select_init_batch_kernel(const sdp_select_task *tasks, uint64_t 
     const sdp_select_task t = tasks[blockIdx.x];
     SelState *st = task_state(t);
     if (threadIdx.x == 0) {
+        // the first digit is the 11 highest bits in which the window's keys can
+        // differ (msb - 10 .. msb), later digits 11 bits each, the last one
+        // what is left (same number of rounds as 11-bit digits aligned at
+        // multiples of 11: 1 + msb / 11).  Aligned digits left a window whose
+        // keys differ in bits 44-45 (f32 quantile windows) 4 of 2048 buckets
+        // in round 0, so up to half the candidates survived into round 1.
         const uint64_t x = t.lo_key ^ t.hi_key;
-        const int shift0 = x ? ((63 - __clzll((long long)x)) / 11) * 11 : 0;
+        const int msb = x ? 63 - __clzll((long long)x) : 0;
+        const int shift0 = msb >= 11 ? msb - 10 : 0;
         st->prefix = shift0 + 11 < 64 ? (t.lo_key >> (shift0 + 11)) : 0ull;
         st->k = t.k;
         st->shift = shift0;
+        st->width = 11;
         st->done = 0;
         st->result = EMPTY64;
     }
@@ -2150,7 +2162,8 @@ __global__ void radix_hist_batch_kernel(const sdp_select_task *tasks, int round,
     for (int i = threadIdx.x; i < 2048; i += blockDim.x) h[i] = 0;
     __syncthreads();
     const uint64_t n = *n_ptr, prefix = st->prefix;
-    const int shift = st->shift, top = shift + 11;
+    const int shift = st->shift, top = shift + st->width;
+    const uint64_t dmask = (1ull << st->width) - 1;
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
     uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     constexpr int R = 4;
@@ -2160,11 +2173,11 @@ __global__ void radix_hist_batch_kernel(const sdp_select_task *tasks, int round,
         for (int r = 0; r < R; ++r) k[r] = keys[i + r * stride];
 #pragma unroll
         for (int r = 0; r < R; ++r)
-            if (top >= 64 || (k[r] >> top) == prefix) atomicAdd(&h[(k[r] >> shift) & 2047u], 1u);
+            if (top >= 64 || (k[r] >> top) == prefix) atomicAdd(&h[(k[r] >> shift) & dmask], 1u);
     }
     for (; i < n; i += stride) {
         const uint64_t k = keys[i];
-        if (top >= 64 || (k >> top) == prefix) atomicAdd(&h[(k >> shift) & 2047u], 1u);
+        if (top >= 64 || (k >> top) == prefix) atomicAdd(&h[(k >> shift) & dmask], 1u);
     }
     __syncthreads();
     uint64_t *gh = hist + (int64_t)blockIdx.y * 2048;
@@ -2213,13 +2226,14 @@ __global__ void __launch_bounds__(1024) radix_decide_batch_kernel(const sdp_sele
             *t.d_result = EMPTY64;
         } else {
             st->k = (int64_t)(k - s_before);
-            st->prefix = (st->shift + 11 >= 64 ? 0ull : (st->prefix << 11)) | (uint64_t)s_j;
+            st->prefix = (st->shift + st->width >= 64 ? 0ull : (st->prefix << st->width)) | (uint64_t)s_j;
             if (st->shift == 0) {
                 st->done = 1;
                 st->result = st->prefix;
                 *t.d_result = st->prefix;
             } else {
-                st->shift -= 11;
+                st->width = st->shift < 11 ? st->shift : 11;
+                st->shift -= st->width;
             }
         }
         *on = 0;                                   // the next round's survivor count
@@ -2242,19 +2256,23 @@ __global__ void radix_filter_hist_batch_kernel(const sdp_select_task *tasks, int
     __syncthreads();
     Stager sg{s_buf, &s_cnt, &s_gbase};
     const uint64_t n = *n_ptr, prefix = st->prefix;
-    const int shift = st->shift, top = shift + 11;
+    const int shift = st->shift, top = shift + st->width;
+    const uint64_t dmask = (1ull << st->width) - 1;
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-    const uint64_t iters = (n + stride - 1) / stride;
+    // R keys per thread loaded before any is pushed: R loads in flight, not one
+    constexpr int R = 4;
+    const uint64_t iters = (n + R * stride - 1) / (R * stride);
     for (uint64_t it = 0; it < iters; ++it) {
-        const uint64_t i = it * stride + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-        uint64_t k = 0;
-        bool keep = false;
-        if (i < n) {
-            k = keys[i];
-            keep = top >= 64 ? true : ((k >> top) == prefix);
-            if (keep) atomicAdd(&h[(k >> shift) & 2047u], 1u);
+        const uint64_t i0 = it * R * stride + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+        uint64_t k[R];
+#pragma unroll
+        for (int r = 0; r < R; ++r) k[r] = i0 + r * stride < n ? keys[i0 + r * stride] : 0;
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            const bool keep = i0 + r * stride < n && (top >= 64 || (k[r] >> top) == prefix);
+            if (keep) atomicAdd(&h[(k[r] >> shift) & dmask], 1u);
+            stage_push(sg, keep, k[r], out, (unsigned long long *)out_n, it + 1 == iters && r == R - 1);
         }
-        stage_push(sg, keep, k, out, (unsigned long long *)out_n, it + 1 == iters);
     }
     __syncthreads();
     uint64_t *gh = hist + (int64_t)blockIdx.y * 2048;
