@@ -1,7 +1,7 @@
 set -o pipefail
 # batched radix select change: GPU suite, then same-box bench A/B
 cd /root/repo; mkdir -p gpurun_out; export TMPDIR=/tmp
-[ -n "$NOTEST" ] || timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 600 --timeout-method thread > gpurun_out/${TAG:-r06ad}_tests.log 2>&1
+[ -n "$NOTEST" ] || timeout -k 10 900 python -u -m pytest ${TESTS:-tests} -m gpu -x -q --timeout 600 --timeout-method thread > gpurun_out/${TAG:-r06ad}_tests.log 2>&1
 rc=$?; tail -3 gpurun_out/${TAG:-r06ad}_tests.log; [ $rc -eq 0 ] || exit $rc
 bash tools/gpu_bench_ab.sh ${TAG:-r06ad} ${REPS:-2} > /dev/null || exit 1
 TAG=${TAG:-r06ad} REPS=${REPS:-2} python3 - <<'PY'
