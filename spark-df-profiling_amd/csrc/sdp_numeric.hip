@@ -2319,7 +2319,7 @@ __global__ void copy_segments_batch_kernel(const sdp_compact_task *tasks) {
 }
 
 static int select_batch_blocks(int32_t q) {
-    int hb = (8192 + q - 1) / q;       // ~8 K workgroups: the largest windows get enough of them
+    int hb = (16384 + q - 1) / q;      // ~16 K workgroups: the largest windows get enough of them
     return hb < 16 ? 16 : (hb > 512 ? 512 : hb);
 }
 
